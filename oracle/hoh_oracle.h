@@ -27,7 +27,7 @@ extern "C" {
 #define OR_OK 0
 #define OR_E_ARG (-1)           /* invalid argument (symbol >= range, pb out of range...)  */
 #define OR_E_ASSERT (-2)        /* a live assert() in the reference would abort here      */
-#define OR_E_UB (-3)            /* the reference has undefined behaviour on this input     */
+#define OR_E_UB (-3)            /* (reserved) undefined behaviour in the reference          */
 #define OR_E_UNREPRODUCIBLE (-4)/* the reference emits uninitialised bytes here            */
 #define OR_E_CORRUPT (-5)       /* decoder: malformed stream                               */
 #define OR_E_CAP (-6)           /* caller buffer too small                                 */

@@ -1,0 +1,132 @@
+"""The CPU oracle (oracle/hoh_oracle.c) against the golden vectors generated from the reference
+itself (tests/golden/make_golden.py).  These pin the oracle on machines without /root/reference."""
+import ctypes as C
+import hashlib
+
+import numpy as np
+import pytest
+
+from gen import make_image, make_plane, make_symbols
+
+
+def sha(b):
+    return hashlib.sha256(bytes(b)).hexdigest()
+
+
+def check(rec, data):
+    assert len(data) == rec["len"]
+    if "hex" in rec:
+        assert bytes(data).hex() == rec["hex"]
+    assert sha(data) == rec["sha256"]
+
+
+def test_esym_init(golden, orc):
+    L = orc.lib()
+
+    class ES(C.Structure):
+        _fields_ = [("rcp", C.c_uint64), ("freq", C.c_uint32), ("bias", C.c_uint32),
+                    ("cmpl", C.c_uint32), ("shift", C.c_uint32)]
+    for pb, g in golden["esym_init"].items():
+        pb = int(pb)
+        h = hashlib.sha256()
+        s = ES()
+        for f in range(1, (1 << pb) + 1):
+            start = ((1 << pb) - f) // 3
+            L.or_esym_init(C.byref(s), start, f, pb)
+            h.update(("%d,%d,%d,%d,%d,%d;" % (start, f, s.rcp, s.bias, s.cmpl, s.shift)).encode())
+        assert h.hexdigest() == g["sha256"], pb
+
+
+def test_normalize_freqs(golden, orc):
+    for c in golden["normalize_freqs"]:
+        f, _ = orc.normalize_freqs(np.array(c["freqs"], np.uint32), c["target"])
+        assert f.tolist() == c["out"], c["name"]
+
+
+def test_normalize_assert_cases(orc):
+    with pytest.raises(orc.OracleError):
+        orc.normalize_freqs(np.ones(512, np.uint32), 256)     # stattools.hpp:14 assert
+
+
+def test_encode_entropy(golden, orc):
+    for e in golden["entropy"]:
+        sp = e["spec"]
+        check(e["enc"], orc.encode_entropy(make_symbols(sp), sp["range"], sp["pb"]))
+
+
+def test_decode_entropy_roundtrip(golden, orc):
+    """corrected decoder: every decodable golden stream decodes to its input (and the payload
+    pointer lands at the end: the Q1 fix)"""
+    for e in golden["entropy"]:
+        sp = e["spec"]
+        if not e.get("decodable", True):
+            continue
+        sym = make_symbols(sp)
+        try:
+            enc = orc.encode_entropy(sym, sp["range"], sp["pb"])
+        except orc.OracleError:
+            continue
+        dec, bp = orc.decode_entropy(enc + b"\x00" * 8)
+        assert np.array_equal(dec, sym), sp
+        assert bp == len(enc), sp
+
+
+def test_predict_fastpath(golden, orc):
+    for p in golden["predict_fastpath"]:
+        plane = make_plane(p["spec"])
+        check(p["res"], orc.predict_fastpath(plane, p["depth"]).tobytes())
+
+
+def test_layer_encode(golden, orc):
+    L = orc.lib()
+    for g in golden["layer_encode_s0"]:
+        sp = g["spec"]
+        plane = np.ascontiguousarray(make_plane(sp))
+        nuke = np.zeros(plane.size, np.uint8)
+        for a, b in g["nuke_ranges"]:
+            nuke[a:b] = 1
+        out = np.empty(plane.size * 4 + 8192, np.uint8)
+        r = L.or_layer_encode_s0(plane.ctypes.data_as(orc.u16p), plane.size, sp["W"], sp["H"], g["depth"],
+                                 nuke.ctypes.data_as(orc.u8p), out.ctypes.data_as(orc.u8p))
+        assert r > 0
+        check(g["out"], out[:r].tobytes())
+
+
+def test_encode_tile(golden, orc):
+    for t in golden["encode_tile_s0"]:
+        check(t["out"], orc.encode_tile(make_image(t["spec"])))
+
+
+@pytest.mark.parametrize("idx", range(6))
+def test_choh_files(golden, orc, idx):
+    f = golden["choh_s0"][idx]
+    sp = f["spec"]
+    if sp["W"] * sp["H"] > 4096 * 4096:
+        pytest.skip("8192^2 whole-file oracle run covered by test_choh_8192 (slow)")
+    data, printed = orc.choh(make_image(sp))
+    check(f["out"], data)
+    assert printed == f["printed"]
+
+
+@pytest.mark.slow
+def test_choh_8192(golden, orc):
+    f = [f for f in golden["choh_s0"] if f["spec"]["W"] == 8192][0]
+    data, printed = orc.choh(make_image(f["spec"]))
+    check(f["out"], data)
+
+
+def test_reference_fixture_example_rgb(golden, orc):
+    """The reference's own RGB round-trip fixture: choh on a 2x2 image writes only the 8-byte
+    header and prints header + the discarded tile size."""
+    rgb = np.frombuffer(bytes.fromhex(golden["reference_fixtures"]["example.rgb"]), np.uint8).reshape(2, 2, 3)
+    data, printed = orc.choh(rgb)
+    assert data == bytes.fromhex("9948 4f48 0208 0101".replace(" ", ""))
+    assert printed > len(data)
+
+
+def test_oracle_roundtrip_files(orc):
+    from hoh_ans.synth import synth_rgb
+    for W, H, seed, noise in ((512, 512, 3, 4), (777, 600, 4, 1), (512, 300, 5, 0)):
+        img = synth_rgb(W, H, seed, noise)
+        data, _ = orc.choh(img)
+        assert np.array_equal(orc.dhoh(data), img)

@@ -1,0 +1,62 @@
+"""Direct oracle-vs-reference comparisons on fresh random inputs (runs only where the reference
+was built in place: oracle/_ref/libref.so)."""
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.skipif(O.ref() is None, reason="oracle/_ref not built (no /root/reference)")
+
+
+def ref_encode(sym, rng, pb):
+    R = O.ref()
+    out = np.empty(O.lib().or_entropy_bound(sym.size, rng, pb) + 64, np.uint8)
+    r = R.ref_encode_entropy(sym.ctypes.data_as(O.u16p), sym.size, rng, pb, out.ctypes.data_as(O.u8p))
+    return out[:r].tobytes()
+
+
+def test_random_streams():
+    rs = np.random.RandomState(7)
+    for it in range(300):
+        rng = int(rs.choice([2, 3, 17, 64, 255, 256, 300, 511, 512]))
+        pb = int(rs.choice([p for p in (9, 10, 11, 12, 13, 14, 15) if (1 << p) >= rng]))
+        n = int(rs.choice([1, 2, 10, 100, 1000, 5000]))
+        scale = rs.uniform(0.3, 60)
+        v = np.floor(rs.exponential(scale, n)).astype(np.int64) * rs.choice([-1, 1], n)
+        sym = ((rng // 2 + v) % rng).astype(np.uint16)
+        assert O.encode_entropy(sym, rng, pb) == ref_encode(sym, rng, pb), (rng, pb, n)
+
+
+def test_lz_and_tiles_random_patterns():
+    """tiles with repeats (LZ matches), few colours and flat areas"""
+    rs = np.random.RandomState(11)
+    R = O.ref()
+    for it in range(12):
+        w, h = int(rs.choice([64, 100, 256])), int(rs.choice([48, 256]))
+        base = rs.randint(0, 256, size=(h, w, 3)).astype(np.uint8)
+        pal = rs.randint(0, 256, size=(int(rs.choice([3, 20, 300])), 3)).astype(np.uint8)
+        img = pal[rs.randint(0, len(pal), size=(h, w))]
+        # repeat runs
+        for _ in range(20):
+            y, x, L = rs.randint(0, h), rs.randint(8, w), rs.randint(4, 40)
+            img[y, x:x + L] = img[y, x - 8:x - 8 + L][: max(0, min(L, w - x))]
+        if it % 3 == 0:
+            img = np.where(rs.rand(h, w, 1) < 0.7, img, base)
+        img = np.ascontiguousarray(img)
+        out = np.empty(img.size * 6 + 8192, np.uint8)
+        r = R.ref_encode_tile(img.ctypes.data_as(O.u8p), w, h, 0, out.ctypes.data_as(O.u8p))
+        try:
+            mine = O.encode_tile(img)
+        except O.OracleError as e:
+            assert int(str(e)) == -4  # unreproducible in the reference (uninitialised bytes)
+            continue
+        assert mine == out[:r].tobytes(), it
+
+
+def test_single_symbol_overrun():
+    """single-symbol streams at prob_bits 8/12/16 make the reference write one element past its
+    clamp array (entropy_encoding.hpp:72,103); the oracle drops that write -- same bytes."""
+    for n, rng, pb, v in [(65536, 256, 12, 7), (65536, 256, 8, 200), (5000, 512, 12, 3), (70000, 2, 8, 1),
+                          (100000, 256, 16, 9), (65536, 1024, 12, 5), (1, 256, 8, 3), (3, 5, 12, 4)]:
+        sym = np.full(n, v, np.uint16)
+        assert O.encode_entropy(sym, rng, pb) == ref_encode(sym, rng, pb), (n, rng, pb)
