@@ -1,0 +1,32 @@
+# Builds libhohgpu.so (all HIP kernels for gfx950 + host orchestration) in-tree, the C++ CLIs
+# (choh / dhoh drop-ins) and the CPU oracle (test infrastructure).
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+CSRC := hoh-ans_amd/csrc
+LIBDIR := hoh-ans_amd/lib
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-result
+SRCS := $(wildcard $(CSRC)/*.hip) $(wildcard $(CSRC)/*.cpp)
+OBJS := $(patsubst $(CSRC)/%,build/%.o,$(SRCS))
+HDRS := $(wildcard $(CSRC)/*.h) include/hoh_ans.h
+
+all: $(LIBDIR)/libhohgpu.so oracle/liboracle.so
+
+build/%.hip.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+build/%.cpp.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIBDIR)/libhohgpu.so: $(OBJS)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+
+oracle/liboracle.so: oracle/hoh_oracle.c oracle/hoh_oracle.h
+	gcc -O2 -shared -fPIC -o $@ oracle/hoh_oracle.c
+
+clean:
+	rm -rf build $(LIBDIR)/libhohgpu.so oracle/liboracle.so
+
+.PHONY: all clean

@@ -1,0 +1,412 @@
+// Host orchestration and C ABI of libhohgpu (include/hoh_ans.h).  All compute runs in the HIP
+// kernels of this directory; this file only sizes workspaces, launches, and moves the few bytes
+// the host must see (sizes, status words).  There is no CPU fallback: without a HIP device every
+// entry point returns HOH_E_NODEV.
+#include "hoh_internal.h"
+#include "hoh_dec.h"
+#include "../../include/hoh_ans.h"
+
+#include <string.h>
+#include <stdlib.h>
+#include <vector>
+#include <string>
+
+void launch_synth(uint8_t* rgb, int W, int H, uint64_t seed, int noise, hipStream_t s);
+
+namespace {
+
+struct Buf {
+  void* p = nullptr;
+  size_t n = 0;
+};
+
+int ensure(Buf& b, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  if (b.n >= bytes) return HOH_OK;
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.n = 0;
+  if (hipMalloc(&b.p, bytes) != hipSuccess) return HOH_E_HIP;
+  b.n = bytes;
+  return HOH_OK;
+}
+
+size_t rup(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+}  // namespace
+
+struct hoh_index {
+  Buf ck;                       // Checkpoint[]
+  Buf streams;                  // IndexStream[]
+  int nstreams = 0;
+  size_t ck_count = 0;
+};
+
+struct hoh_ctx {
+  int device = 0;
+  hipStream_t own = nullptr;
+  Buf sym, hist, candbits, matches, streams, tiles, hdr, tab_fast, tab_gen, slabs, ckpt, misc, tsizes;
+  DecWork dec;                  // decoder workspaces (k_decode.hip)
+  uint64_t* pinned = nullptr;   // small host staging (status words, sizes)
+  int profiling = 0;
+  std::vector<std::string> knames;
+  std::vector<hipEvent_t> kev;
+  std::vector<float> kms;
+};
+
+static hipStream_t pick(hoh_ctx* c, void* s) { return s ? (hipStream_t)s : c->own; }
+
+// ---------------------------------------------------------------- profiling helpers
+
+struct Prof {
+  hoh_ctx* c;
+  hipStream_t s;
+  explicit Prof(hoh_ctx* c_, hipStream_t s_) : c(c_), s(s_) {
+    if (!c->profiling) return;
+    for (auto e : c->kev) (void)hipEventDestroy(e);
+    c->kev.clear();
+    c->knames.clear();
+    mark("start");
+  }
+  void mark(const char* name) {
+    if (!c->profiling) return;
+    hipEvent_t e;
+    (void)hipEventCreate(&e);
+    (void)hipEventRecord(e, s);
+    c->kev.push_back(e);
+    c->knames.push_back(name);
+  }
+};
+
+extern "C" {
+
+const char* hoh_version(void) { return "hoh-ans_amd 0.1 (gfx950)"; }
+
+const char* hoh_strerror(int code) {
+  switch (code) {
+    case HOH_OK: return "ok";
+    case HOH_E_ARG: return "invalid argument";
+    case HOH_E_CAP: return "output capacity too small";
+    case HOH_E_HIP: return "HIP runtime error";
+    case HOH_E_RANGE: return "symbol / range / prob_bits outside the supported set";
+    case HOH_E_UNREPRODUCIBLE: return "the reference emits uninitialised bytes for this input";
+    case HOH_E_UNSUPPORTED: return "not implemented on this path";
+    case HOH_E_CORRUPT: return "malformed or undecodable bitstream";
+    case HOH_E_NODEV: return "no HIP device";
+  }
+  return "unknown error";
+}
+
+int hoh_ctx_create(hoh_ctx** out, int device) {
+  if (!out) return HOH_E_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) return HOH_E_NODEV;
+  if (hipSetDevice(device) != hipSuccess) return HOH_E_NODEV;
+  hoh_ctx* c = new hoh_ctx();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) { delete c; return HOH_E_HIP; }
+  if (hipHostMalloc((void**)&c->pinned, 4096) != hipSuccess) { delete c; return HOH_E_HIP; }
+  *out = c;
+  return HOH_OK;
+}
+
+static void freebuf(Buf& b) { if (b.p) (void)hipFree(b.p); b.p = nullptr; b.n = 0; }
+
+void hoh_ctx_destroy(hoh_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  Buf* all[] = {&c->sym, &c->hist, &c->candbits, &c->matches, &c->streams, &c->tiles, &c->hdr,
+                &c->tab_fast, &c->tab_gen, &c->slabs, &c->ckpt, &c->misc, &c->tsizes};
+  for (Buf* b : all) freebuf(*b);
+  dec_free(c->dec);
+  for (auto e : c->kev) (void)hipEventDestroy(e);
+  if (c->pinned) (void)hipHostFree(c->pinned);
+  if (c->own) (void)hipStreamDestroy(c->own);
+  delete c;
+}
+
+void hoh_set_profiling(hoh_ctx* c, int on) { if (c) c->profiling = on; }
+
+int hoh_get_kernel_ms(hoh_ctx* c, const char** names, float* ms, int max) {
+  if (!c || c->kev.size() < 2) return 0;
+  int k = 0;
+  (void)hipEventSynchronize(c->kev.back());
+  for (size_t i = 1; i < c->kev.size() && k < max; i++, k++) {
+    float v = 0;
+    (void)hipEventElapsedTime(&v, c->kev[i - 1], c->kev[i]);
+    if (names) names[k] = c->knames[i].c_str();
+    if (ms) ms[k] = v;
+  }
+  return k;
+}
+
+int hoh_tiling(int W, int H, int* xt, int* yt, int* tw, int* th) {
+  if ((W >= 512 || H >= 512) && W >= 256 && H >= 256) {                 // choh.cpp:454-461
+    *xt = W / 256; *yt = H / 256;
+    *tw = (W + *xt - 1) / *xt; *th = (H + *yt - 1) / *yt;
+    return 1;
+  }
+  *xt = *yt = 1; *tw = W; *th = H;
+  return 0;
+}
+
+size_t hoh_encode_bound(int W, int H) {
+  int xt, yt, tw, th;
+  hoh_tiling(W, H, &xt, &yt, &tw, &th);
+  return 64 + (size_t)xt * yt * 3 + 5 * (size_t)W * H + (size_t)xt * yt * 4096;
+}
+
+static size_t header_fixed(int W, int H, uint8_t* o) {
+  size_t p = 0;
+  o[p++] = 153; o[p++] = 72; o[p++] = 79; o[p++] = 72;                   // choh.cpp:437-440
+  o[p++] = 2;                                                           // :443 rgb
+  o[p++] = 8;                                                           // :446 depth
+  p = hoh_write_varint(o, (uint32_t)p, (uint64_t)W - 1);                // :449-450
+  p = hoh_write_varint(o, (uint32_t)p, (uint64_t)H - 1);
+  return p;
+}
+
+size_t hoh_file_prefix(int W, int H, const uint32_t* ts, int nt, uint8_t* out, size_t cap) {
+  int xt, yt, tw, th;
+  if (!hoh_tiling(W, H, &xt, &yt, &tw, &th) || nt != xt * yt) return 0;
+  std::vector<uint8_t> b(32 + 3 * (size_t)nt);
+  size_t p = header_fixed(W, H, b.data());
+  b[p++] = (uint8_t)(xt - 1);                                           // :457-458
+  b[p++] = (uint8_t)(yt - 1);
+  for (int i = 0; i + 1 < nt; i++) p = hoh_write_varint(b.data(), (uint32_t)p, ts[i]);   // :496-498
+  if (p > cap) return 0;
+  memcpy(out, b.data(), p);
+  return p;
+}
+
+int hoh_peek_header(const uint8_t* h, size_t size, int* W, int* H, int* xt, int* yt) {
+  if (!h || size < 8 || h[0] != 153 || h[1] != 72 || h[2] != 79 || h[3] != 72) return HOH_E_CORRUPT;
+  if (h[4] != 2 || h[5] != 8) return HOH_E_UNSUPPORTED;
+  size_t p = 6;
+  auto rv = [&](uint64_t& v) -> bool {                                  // varint.hpp:6-27
+    if (p >= size) return false;
+    uint64_t b0 = h[p++];
+    if (!(b0 & 0x80)) { v = b0; return true; }
+    if (p >= size) return false;
+    uint64_t b1 = h[p++];
+    if (!(b1 & 0x80)) { v = ((b0 & 0x7f) << 7) + b1; return true; }
+    if (p >= size) return false;
+    uint64_t b2 = h[p++];
+    v = ((b0 & 0x7f) << 14) + ((b1 & 0x7f) << 7) + b2;
+    return true;
+  };
+  uint64_t w, hh;
+  if (!rv(w) || !rv(hh)) return HOH_E_CORRUPT;
+  *W = (int)w + 1; *H = (int)hh + 1;
+  int tw, th, x, y;
+  hoh_tiling(*W, *H, &x, &y, &tw, &th);
+  if (xt) *xt = x;
+  if (yt) *yt = y;
+  return HOH_OK;
+}
+
+// ---------------------------------------------------------------- image encode
+
+static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int t0, int ntiles,
+                             uint8_t* d_out, size_t cap, uint64_t prefix, int write_table,
+                             uint32_t* d_tile_sizes, uint64_t* total_out, hoh_index* idx,
+                             hipStream_t s) {
+  int xt, yt, tw, th;
+  hoh_tiling(W, H, &xt, &yt, &tw, &th);
+  if (tw > HOH_MAX_TILE_W || (size_t)tw * th > (1u << 24)) return HOH_E_UNSUPPORTED;
+  if (t0 < 0 || ntiles <= 0 || t0 + ntiles > xt * yt) return HOH_E_ARG;
+  Prof prof(c, s);
+  EncodeJob j;
+  memset(&j, 0, sizeof(j));
+  j.rgb = d_rgb; j.W = W; j.H = H;
+  j.xt = xt; j.yt = yt; j.tw = tw; j.th = th;
+  j.t0 = t0; j.ntiles = ntiles;
+  j.npix_cap = (uint32_t)rup((size_t)tw * th, HOH_SEG > 64 ? 64 : 64);
+  j.lz_cap = (uint32_t)rup(j.npix_cap / 4 + j.npix_cap / 255 + 16, 8);
+  j.gen_stride = 512;
+  j.hdr_cap = HOH_HDR_CAP;
+  const size_t S = (size_t)ntiles * SK_PER_TILE;
+  const size_t nsym = (size_t)ntiles * 3 * j.npix_cap + (size_t)ntiles * 3 * j.lz_cap;
+  const size_t nslab = (size_t)ntiles * 3 * (j.npix_cap + 8) + (size_t)ntiles * 3 * (j.lz_cap + 8);
+  const size_t nck = S * (j.npix_cap / HOH_SEG + 2);
+  int e = HOH_OK;
+  if ((e = ensure(c->sym, nsym * 2 + 64))) return e;
+  if ((e = ensure(c->hist, S * 512 * 4))) return e;
+  if ((e = ensure(c->candbits, (size_t)ntiles * (j.npix_cap / 64) * 8))) return e;
+  if ((e = ensure(c->matches, (size_t)ntiles * 3 * (j.lz_cap + 1) * 4))) return e;
+  if ((e = ensure(c->streams, S * sizeof(StreamInfo)))) return e;
+  if ((e = ensure(c->tiles, (size_t)ntiles * sizeof(TileInfo)))) return e;
+  if ((e = ensure(c->hdr, S * HOH_HDR_CAP))) return e;
+  if ((e = ensure(c->tab_fast, S * HOH_FAST_RANGE * sizeof(EncFast)))) return e;
+  if ((e = ensure(c->tab_gen, S * 512 * sizeof(EncGen)))) return e;
+  if ((e = ensure(c->slabs, nslab * 4))) return e;
+  if ((e = ensure(c->ckpt, nck * sizeof(Checkpoint)))) return e;
+  if ((e = ensure(c->misc, 64))) return e;
+  j.sym = (uint16_t*)c->sym.p;
+  j.hist = (uint32_t*)c->hist.p;
+  j.candbits = (uint64_t*)c->candbits.p;
+  j.matches = (uint32_t*)c->matches.p;
+  j.streams = (StreamInfo*)c->streams.p;
+  j.tiles = (TileInfo*)c->tiles.p;
+  j.hdr = (uint8_t*)c->hdr.p;
+  j.tab_fast = (EncFast*)c->tab_fast.p;
+  j.tab_gen = (EncGen*)c->tab_gen.p;
+  j.slabs = (uint32_t*)c->slabs.p;
+  j.ckpt = (Checkpoint*)c->ckpt.p;
+  j.gerr = (uint32_t*)c->misc.p;
+  j.total = (uint64_t*)((uint8_t*)c->misc.p + 8);
+  j.tile_sizes = d_tile_sizes;
+  j.out = d_out;
+  j.cap = cap;
+  j.prefix = prefix;
+  j.write_table = write_table;
+  if (hipMemsetAsync(j.candbits, 0, (size_t)ntiles * (j.npix_cap / 64) * 8, s) != hipSuccess) return HOH_E_HIP;
+  if (hipMemsetAsync(c->misc.p, 0, 64, s) != hipSuccess) return HOH_E_HIP;
+  prof.mark("memset");
+  launch_front(j, s);            prof.mark("front");
+  launch_lz(j, s);               prof.mark("lz");
+  launch_tables(j, (int)S, s);   prof.mark("tables");
+  launch_rans_fast(j, nullptr, ntiles * 3, s); prof.mark("rans_enc_fast");
+  launch_rans_gen(j, (int)S, s); prof.mark("rans_enc_gen");
+  launch_finalize(j, (int)S, s); prof.mark("finalize");
+  launch_layout(j, s);           prof.mark("layout");
+  launch_assemble(j, (int)S, s); prof.mark("assemble");
+  if (hipGetLastError() != hipSuccess) return HOH_E_HIP;
+  if (idx) {
+    int r = index_capture(idx, j, s);
+    if (r) return r;
+    prof.mark("index");
+  }
+  if (hipMemcpyAsync(c->pinned, c->misc.p, 16, hipMemcpyDeviceToHost, s) != hipSuccess) return HOH_E_HIP;
+  if (hipStreamSynchronize(s) != hipSuccess) return HOH_E_HIP;
+  const uint32_t gerr = (uint32_t)c->pinned[0];
+  *total_out = c->pinned[1];
+  if (gerr) {
+    const uint32_t tf = gerr >> 8;
+    if (tf & TF_UNREPRODUCIBLE) return HOH_E_UNREPRODUCIBLE;
+    if (tf & TF_UNSUPPORTED) return HOH_E_UNSUPPORTED;
+    if (gerr & 2) return HOH_E_RANGE;
+    return HOH_E_HIP;
+  }
+  if (*total_out > cap) return HOH_E_CAP;
+  return HOH_OK;
+}
+
+int hoh_encode_tiles(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int t0, int ntiles, uint8_t* d_out,
+                     size_t cap, uint32_t* d_tile_sizes, size_t* out_size, void* stream) {
+  if (!c || !d_rgb || !d_out || !out_size || W <= 0 || H <= 0) return HOH_E_ARG;
+  (void)hipSetDevice(c->device);
+  int xt, yt, tw, th;
+  if (!hoh_tiling(W, H, &xt, &yt, &tw, &th)) return HOH_E_ARG;
+  uint64_t total = 0;
+  int r = encode_tiles_impl(c, d_rgb, W, H, t0, ntiles, d_out, cap, 0, 0, d_tile_sizes, &total, nullptr,
+                            pick(c, stream));
+  *out_size = (size_t)total;
+  return r;
+}
+
+int hoh_encode_image_ix(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int speed, uint8_t* d_out,
+                        size_t cap, size_t* out_size, size_t* printed, hoh_index* idx, void* stream) {
+  if (!c || !d_rgb || !d_out || !out_size || W <= 0 || H <= 0) return HOH_E_ARG;
+  if (speed != 0) return HOH_E_UNSUPPORTED;                             // -s1..-s4 not on this path
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick(c, stream);
+  uint8_t hb[32];
+  int xt, yt, tw, th;
+  const int tiled = hoh_tiling(W, H, &xt, &yt, &tw, &th);
+  size_t hl = header_fixed(W, H, hb);
+  if (tiled) { hb[hl++] = (uint8_t)(xt - 1); hb[hl++] = (uint8_t)(yt - 1); }
+  if (cap < hl) return HOH_E_CAP;
+  uint64_t total = 0;
+  int r;
+  if (tiled) {
+    r = encode_tiles_impl(c, d_rgb, W, H, 0, xt * yt, d_out, cap, hl, 1, nullptr, &total, idx, s);
+    if (r == HOH_OK && hipMemcpyAsync(d_out, hb, hl, hipMemcpyHostToDevice, s) != hipSuccess) r = HOH_E_HIP;
+    if (r == HOH_OK && hipStreamSynchronize(s) != hipSuccess) r = HOH_E_HIP;
+    *out_size = (size_t)total;
+    if (printed) *printed = (size_t)total;
+  } else {
+    // choh.cpp:508-520: the single tile is coded and discarded; only the header is written (Q13)
+    Buf scratch;
+    const size_t b = hoh_encode_bound(W, H);
+    if ((r = ensure(scratch, b))) return r;
+    r = encode_tiles_impl(c, d_rgb, W, H, 0, 1, (uint8_t*)scratch.p, b, 0, 0, nullptr, &total, nullptr, s);
+    freebuf(scratch);
+    if (r == HOH_OK && hipMemcpyAsync(d_out, hb, hl, hipMemcpyHostToDevice, s) != hipSuccess) r = HOH_E_HIP;
+    if (r == HOH_OK && hipStreamSynchronize(s) != hipSuccess) r = HOH_E_HIP;
+    *out_size = hl;
+    if (printed) *printed = hl + (size_t)total;
+    if (idx) idx->nstreams = 0;
+  }
+  return r;
+}
+
+int hoh_encode_image(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int speed, uint8_t* d_out, size_t cap,
+                     size_t* out_size, size_t* printed, void* stream) {
+  return hoh_encode_image_ix(c, d_rgb, W, H, speed, d_out, cap, out_size, printed, nullptr, stream);
+}
+
+int hoh_synth_rgb(hoh_ctx* c, uint8_t* d_rgb, int W, int H, uint64_t seed, int noise, void* stream) {
+  if (!c || !d_rgb || W <= 0 || H <= 0 || noise < 0) return HOH_E_ARG;
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick(c, stream);
+  launch_synth(d_rgb, W, H, seed, noise, s);
+  if (hipGetLastError() != hipSuccess) return HOH_E_HIP;
+  return hipStreamSynchronize(s) == hipSuccess ? HOH_OK : HOH_E_HIP;
+}
+
+// ---------------------------------------------------------------- decode side index
+
+int hoh_index_create(hoh_index** idx) {
+  if (!idx) return HOH_E_ARG;
+  *idx = new hoh_index();
+  return HOH_OK;
+}
+
+void hoh_index_destroy(hoh_index* idx) {
+  if (!idx) return;
+  freebuf(idx->ck);
+  freebuf(idx->streams);
+  delete idx;
+}
+
+size_t hoh_index_bytes(const hoh_index* idx) {
+  return idx ? idx->ck_count * sizeof(Checkpoint) + (size_t)idx->nstreams * sizeof(IndexStream) : 0;
+}
+
+}  // extern "C"
+
+// index capture: copy every plane stream's checkpoints + payload location (device to device)
+int index_capture(hoh_index* idx, const EncodeJob& j, hipStream_t s) {
+  const int S = j.ntiles * SK_PER_TILE;
+  const size_t per = j.npix_cap / HOH_SEG + 2;
+  int e;
+  if ((e = ensure(idx->streams, (size_t)S * sizeof(IndexStream)))) return e;
+  if ((e = ensure(idx->ck, (size_t)S * per * sizeof(Checkpoint)))) return e;
+  idx->nstreams = S;
+  idx->ck_count = (size_t)S * per;
+  launch_index_capture(j, (IndexStream*)idx->streams.p, (Checkpoint*)idx->ck.p, per, s);
+  return hipGetLastError() == hipSuccess ? HOH_OK : HOH_E_HIP;
+}
+
+const IndexStream* index_streams(const hoh_index* idx) { return idx ? (const IndexStream*)idx->streams.p : nullptr; }
+const Checkpoint* index_ckpts(const hoh_index* idx) { return idx ? (const Checkpoint*)idx->ck.p : nullptr; }
+int index_nstreams(const hoh_index* idx) { return idx ? idx->nstreams : 0; }
+DecWork& ctx_dec(hoh_ctx* c) { return c->dec; }
+hipStream_t ctx_stream(hoh_ctx* c, void* s) { return pick(c, s); }
+uint64_t* ctx_pinned(hoh_ctx* c) { return c->pinned; }
+int ctx_device(hoh_ctx* c) { return c->device; }
+void ctx_mark(hoh_ctx* c, hipStream_t s, const char* name, bool reset) {
+  if (!c->profiling) return;
+  if (reset) {
+    for (auto e : c->kev) (void)hipEventDestroy(e);
+    c->kev.clear();
+    c->knames.clear();
+  }
+  hipEvent_t e;
+  (void)hipEventCreate(&e);
+  (void)hipEventRecord(e, s);
+  c->kev.push_back(e);
+  c->knames.push_back(name);
+}

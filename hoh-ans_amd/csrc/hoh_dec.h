@@ -1,0 +1,51 @@
+// Decoder-side internal definitions (k_decode.hip, hoh_decode.cpp).
+#pragma once
+#include "hoh_internal.h"
+
+struct hoh_index;
+struct hoh_ctx;
+
+struct IndexStream {      // one stream of an encoded image, as recorded by the encoder
+  uint64_t payload_off;   // byte offset (in the .hoh) of the first rANS payload word
+  uint32_t n;             // symbols
+  uint32_t mode;          // SM_*
+  uint32_t widx_end;      // slab index of the first payload word (checkpoint widx base)
+  uint32_t ckpt_off;      // first checkpoint of the stream in the index
+  uint32_t words;
+  uint32_t pad;
+};
+
+struct DecStream {        // one stream of a .hoh, as parsed by the decoder
+  uint64_t table_off;     // where the frequency table bits start (byte), for the table kernel
+  uint64_t payload_off;   // first payload byte (rANS words or stored bits)
+  uint64_t out_off;       // element offset of the decoded symbols in the decode arena
+  uint32_t n, range, pb, mode, tsm, maxbits;
+  uint32_t words;         // rANS payload words
+  uint32_t err;
+  int32_t ix;             // matching index stream, -1 if none
+  uint32_t pad;
+};
+
+struct DecTile {
+  int32_t x0, y0, w, h;
+  uint64_t off;           // byte offset of the tile in the file
+  uint32_t mode, nmatch;
+  uint32_t err, pad;
+};
+
+struct DecWork {
+  void* bufs[16] = {nullptr};
+  size_t sizes[16] = {0};
+};
+
+void dec_free(DecWork& w);
+int index_capture(hoh_index* idx, const EncodeJob& j, hipStream_t s);
+void launch_index_capture(const EncodeJob& j, IndexStream* is, Checkpoint* ck, size_t per, hipStream_t s);
+const IndexStream* index_streams(const hoh_index* idx);
+const Checkpoint* index_ckpts(const hoh_index* idx);
+int index_nstreams(const hoh_index* idx);
+DecWork& ctx_dec(hoh_ctx* c);
+hipStream_t ctx_stream(hoh_ctx* c, void* s);
+uint64_t* ctx_pinned(hoh_ctx* c);
+int ctx_device(hoh_ctx* c);
+void ctx_mark(hoh_ctx* c, hipStream_t s, const char* name, bool reset);

@@ -1,0 +1,146 @@
+// Internal definitions shared by the HIP kernels and the host orchestration of libhohgpu.
+// Device code is written for gfx950 (wave64, 160 KiB LDS per CU).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#define HOH_WAVE 64
+#define HOH_HDR_CAP 1600          // bytes reserved per stream for varints + meta + table
+#define HOH_FAST_RANGE 512        // LDS-table fast encoder handles range <= 512 at prob_bits 15
+#define HOH_SEG 1024              // decode checkpoint spacing (symbols)
+#define HOH_MAX_TILE_W 65535
+#define HOH_LZ_WINDOW 64          // -s0 seek distance 6 -> 1 << 6 pixels back (choh.cpp:125, lz.hpp:20)
+
+// stream kinds inside a tile (stream id = tile * 6 + kind)
+enum { SK_LZ_FUTURE = 0, SK_LZ_LENGTH = 1, SK_LZ_BACKBY = 2, SK_G = 3, SK_R = 4, SK_B = 5, SK_PER_TILE = 6 };
+
+// stream coding modes (entropy_encoding.hpp)
+enum { SM_EMPTY = 0, SM_RANS = 1, SM_STORED = 2 };
+
+// tile flags
+enum {
+  TF_GREY = 1,            // R == G == B everywhere (channel.hpp:21-31)
+  TF_BINARY = 2,          // grey with <= 2 values -> bitimage mode 0, no plane data
+  TF_PALETTE_CAND = 4,    // <= 256 colours: palette_encode competes (choh.cpp:298-308)
+  TF_UNREPRODUCIBLE = 8,  // the reference copies uninitialised bytes for this tile
+  TF_UNSUPPORTED = 16,
+  TF_OVERFLOW = 32        // an internal capacity was exceeded
+};
+
+struct StreamInfo {
+  uint64_t sym_off;       // element offset of the symbols in the u16 symbol arena (16-B aligned)
+  uint64_t slab_off;      // word offset of this stream's rANS slab
+  uint64_t out_off;       // byte offset of the stream in the output buffer
+  uint32_t n;             // symbol count
+  uint32_t range;         // alphabet size
+  uint32_t pb;            // prob_bits (scale bits)
+  uint32_t slab_cap;      // words available in the slab
+  uint32_t hdr_len;       // varint(range-1) varint(n) meta table  (rANS form)
+  uint32_t vlen;          // bytes of the two header varints
+  uint32_t maxbits;       // bits of (range - 1)
+  uint32_t words;         // rANS words including the 2 flush words
+  uint32_t widx_end;      // final slab index of the first payload word
+  uint32_t mode;          // SM_*
+  uint32_t size;          // final coded bytes of the stream
+  uint32_t err;           // nonzero: error code
+  uint64_t expected_stored;
+  uint32_t fast;          // encoded by the LDS-table fast kernel
+  uint32_t ckpt_off;      // index of the first checkpoint of this stream
+};
+
+struct TileInfo {
+  int32_t x0, y0, w, h;   // tile rectangle inside the image
+  int32_t colours;        // distinct colours (<= 256) or -1 (choh.cpp:17-46)
+  uint32_t flags;         // TF_*
+  uint32_t nmatch;        // LZ matches taken
+  uint32_t ncand;         // LZ candidate positions
+  uint32_t size;          // tile bytes
+  uint32_t lz_bytes;      // 1 + the three LZ stream sizes
+  uint64_t off;           // output byte offset of the tile
+  uint32_t mode;          // internal colour mode byte (128 sub-green, 0 bitimage)
+  uint32_t pad;           // layout: byte offset of this tile's size varint
+};
+
+struct Checkpoint {       // encoder state after coding symbol k*HOH_SEG == decoder state before it
+  uint32_t xl, xh;
+  uint32_t widx;          // slab index of the next word the decoder reads
+  uint32_t pad;
+};
+
+struct EncFast {          // fast encoder symbol (16 B): quotient by exact f64 reciprocal
+  double inv;             // 1/f rounded up by two ulps
+  uint32_t f;
+  uint32_t c;             // cumulative start
+};
+
+struct EncGen {           // generic encoder symbol: rans64.hpp Rans64EncSymbol layout
+  uint64_t rcp;
+  uint32_t freq, bias, cmpl, shift;
+};
+
+__host__ __device__ inline uint32_t hoh_varint_len(uint64_t v) {
+  return v < (1u << 7) ? 1u : v < (1u << 14) ? 2u : v < (1u << 21) ? 3u : 0u;   // varint.hpp:29-45 (Q2)
+}
+
+__host__ __device__ inline uint32_t hoh_write_varint(uint8_t* b, uint32_t loc, uint64_t v) {
+  if (v < (1u << 7)) {
+    b[loc++] = (uint8_t)v;
+  } else if (v < (1u << 14)) {
+    b[loc++] = (uint8_t)((v >> 7) + 128);
+    b[loc++] = (uint8_t)(v % 128);
+  } else if (v < (1u << 21)) {
+    b[loc++] = (uint8_t)((v >> 14) + 128);
+    b[loc++] = (uint8_t)(((v >> 7) % 128) + 128);
+    b[loc++] = (uint8_t)(v % 128);
+  }
+  return loc;
+}
+
+__host__ __device__ inline uint32_t hoh_bitlen(uint64_t v) {
+  uint32_t b = 0;
+  for (; v; v >>= 1) b++;
+  return b;
+}
+
+// ---------------------------------------------------------------- kernel launch declarations
+
+struct EncodeJob {
+  // image
+  const uint8_t* rgb;
+  int W, H;
+  int xt, yt, tw, th;     // tiling (choh.cpp:454-461)
+  int t0, ntiles;         // tiles [t0, t0 + ntiles) of the image are coded
+  uint32_t npix_cap;      // max pixels of one tile (per-plane stride of the residual arena)
+  uint32_t lz_cap;        // symbols per LZ stream slot
+  // arenas
+  uint16_t* sym;          // residual planes + LZ symbols
+  uint32_t* hist;         // [stream][512]
+  uint64_t* candbits;     // [tile][npix_cap/64] LZ candidate bitmap
+  uint32_t* matches;      // [tile][lz_cap] packed (pos, len, back) triples (3 words each)
+  StreamInfo* streams;    // [ntiles * 6]
+  TileInfo* tiles;        // [ntiles]
+  uint8_t* hdr;           // [stream][HOH_HDR_CAP]
+  EncFast* tab_fast;      // [stream][512]
+  EncGen* tab_gen;        // [stream][gen_stride] (generic streams)
+  uint32_t gen_stride;    // entries per stream in tab_gen (>= range)
+  uint32_t hdr_cap;       // bytes per stream in hdr
+  uint32_t* slabs;        // rANS words
+  Checkpoint* ckpt;
+  uint32_t* gerr;         // global error word
+  uint64_t* total;        // total bytes of the tile blob
+  uint32_t* tile_sizes;   // out: per tile bytes (may be null)
+  uint8_t* out;           // output: [prefix bytes][tile size table][tiles]
+  uint64_t cap;
+  uint64_t prefix;        // bytes before the tile size table (file header, written by the host)
+  int write_table;        // write the n-1 tile size varints (a whole .hoh); 0 for a shard blob
+};
+
+void launch_front(const EncodeJob& j, hipStream_t s);
+void launch_lz(const EncodeJob& j, hipStream_t s);
+void launch_tables(const EncodeJob& j, int nstreams, hipStream_t s);
+void launch_rans_fast(const EncodeJob& j, const uint32_t* fast_ids, int nfast, hipStream_t s);
+void launch_rans_gen(const EncodeJob& j, int nstreams, hipStream_t s);
+void launch_finalize(const EncodeJob& j, int nstreams, hipStream_t s);
+void launch_layout(const EncodeJob& j, hipStream_t s);
+void launch_assemble(const EncodeJob& j, int nstreams, hipStream_t s);

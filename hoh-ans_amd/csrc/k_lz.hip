@@ -1,0 +1,164 @@
+// Greedy RGB LZ of find_lz_rgb at -s0 (lz.hpp:6-170), one wave per tile.
+// k_front marked every position whose longest match is >= 4; here the greedy scan walks those
+// candidates in order: at a candidate the 64 lanes measure the run length at the 64 back
+// distances (lane = back-1) and reduce to (longest, smallest back) exactly like lz.hpp:35-53.
+// Then the three LZ symbol streams are generated, and if any pixel was matched ("nuked") the
+// residual streams of the three planes are compacted and their histograms corrected
+// (layer_encode.hpp:93-99).  Also fills the StreamInfo of the tile's six streams.
+#include "hoh_internal.h"
+
+__device__ __forceinline__ uint32_t img_px(const EncodeJob& j, int x0, int y0, int w, uint32_t q) {
+  const uint8_t* p = j.rgb + ((size_t)(y0 + (int)(q / w)) * j.W + x0 + (int)(q % w)) * 3;
+  return p[0] | (p[1] << 8) | (p[2] << 16);
+}
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    uint64_t u = __shfl_xor(v, o);
+    v = u > v ? u : v;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(64) void k_lz(EncodeJob j) {
+  const int t = blockIdx.x, lane = threadIdx.x;
+  TileInfo ti = j.tiles[t];
+  const uint32_t npix = (uint32_t)ti.w * ti.h;
+  const uint32_t nwords = (npix + 63) / 64;
+  uint64_t* bits = j.candbits + (size_t)t * (j.npix_cap / 64);
+  uint32_t* mt = j.matches + (size_t)t * 3 * (j.lz_cap + 1);
+  int bonus = 0;                                                      // choh.cpp:139-154
+  if (ti.colours != -1) {
+    if (ti.colours <= 4) bonus = 32;
+    else if (ti.colours <= 8) bonus = 20;
+    else if (ti.colours <= 16) bonus = 10;
+    else if (ti.colours <= 32) bonus = 2;
+  }
+  const uint32_t thr = 4 + bonus;
+  uint32_t nm = 0, pos = 0;
+  bool overflow = false;
+  if (ti.ncand) {
+    while (pos < npix) {
+      // next candidate q >= pos
+      uint32_t q = 0xffffffffu;
+      for (uint32_t wi = pos >> 6; wi < nwords; wi += 64) {
+        uint64_t wv = (wi + lane < nwords) ? bits[wi + lane] : 0;
+        if (wi + lane == (pos >> 6)) wv &= ~0ull << (pos & 63);
+        uint64_t bal = __ballot(wv != 0);
+        if (bal) {
+          int l = __ffsll((unsigned long long)bal) - 1;
+          uint64_t word = __shfl(wv, l);
+          q = (wi + l) * 64 + (__ffsll((unsigned long long)word) - 1);
+          break;
+        }
+      }
+      if (q == 0xffffffffu) break;
+      const uint32_t b = lane + 1;
+      uint32_t L = 0;
+      if (b <= q) {
+        while (q + L < npix && L < 259 && img_px(j, ti.x0, ti.y0, ti.w, q + L) == img_px(j, ti.x0, ti.y0, ti.w, q + L - b)) L++;
+      }
+      uint64_t key = ((uint64_t)L << 8) | (255u - b);
+      key = wave_max_u64(key);
+      const uint32_t longest = (uint32_t)(key >> 8), best = 255u - (uint32_t)(key & 255);
+      if (longest >= thr) {
+        if (nm < j.lz_cap) {
+          if (lane == 0) { mt[3 * nm] = q; mt[3 * nm + 1] = longest; mt[3 * nm + 2] = best; }
+        } else {
+          overflow = true;
+        }
+        nm++;
+        pos = q + longest;
+      } else {
+        pos = q + 1;
+      }
+    }
+  }
+  // --- LZ symbol streams (lz.hpp:75-95): future (gaps, 255-chunked), length-4, back%256
+  uint16_t* lz0 = j.sym + (size_t)j.ntiles * 3 * j.npix_cap + (size_t)(t * 3) * j.lz_cap;
+  uint16_t* lz1 = lz0 + j.lz_cap;
+  uint16_t* lz2 = lz1 + j.lz_cap;
+  uint32_t nf = 0, prev_end = 0;
+  const uint32_t nmk = nm < j.lz_cap ? nm : j.lz_cap;
+  for (uint32_t m = 0; m <= nmk; m++) {
+    const bool tail = m == nmk;
+    const uint32_t mpos = tail ? npix : mt[3 * m];
+    const uint32_t g = mpos - prev_end;
+    const uint32_t n255 = g / 255;
+    if (nf + n255 + 1 > j.lz_cap) { overflow = true; break; }
+    for (uint32_t k = lane; k < n255; k += 64) lz0[nf + k] = 255;
+    nf += n255;
+    if (!tail) {
+      if (lane == 0) {
+        lz0[nf] = (uint16_t)(g % 255);
+        lz1[m] = (uint16_t)(mt[3 * m + 1] - 4);
+        lz2[m] = (uint16_t)(mt[3 * m + 2] % 256);
+      }
+      nf++;
+      prev_end = mpos + mt[3 * m + 1];
+    }
+  }
+  // --- nuke: compact the residual planes and fix their histograms
+  uint32_t nclean = npix;
+  if (nmk && !overflow) {
+    for (uint32_t wi = lane; wi < nwords; wi += 64) bits[wi] = 0;
+    __syncthreads();
+    for (uint32_t m = 0; m < nmk; m++) {
+      const uint32_t a = mt[3 * m], e = a + mt[3 * m + 1];
+      for (uint32_t p = a + lane; p < e; p += 64) atomicOr((unsigned long long*)&bits[p >> 6], 1ull << (p & 63));
+    }
+    __syncthreads();
+    for (int k = 0; k < 3; k++) {
+      uint16_t* r = j.sym + (size_t)(t * 3 + k) * j.npix_cap;
+      uint32_t* hk = j.hist + (size_t)(t * SK_PER_TILE + SK_G + k) * 512;
+      uint32_t outc = 0;
+      for (uint32_t base = 0; base < npix; base += 64) {
+        const uint32_t p = base + lane;
+        const bool valid = p < npix;
+        const uint16_t v = valid ? r[p] : 0;
+        const bool nuked = valid && ((bits[base >> 6] >> lane) & 1);
+        if (nuked) atomicSub(&hk[v], 1u);
+        const uint64_t keep = __ballot(valid && !nuked);
+        const uint32_t dest = outc + __popcll(keep & ((1ull << lane) - 1));
+        if (valid && !nuked) r[dest] = v;
+        outc += __popcll(keep);
+      }
+      nclean = outc;
+    }
+  }
+  if (lane == 0) {
+    if (overflow) ti.flags |= TF_OVERFLOW;
+    ti.nmatch = nm;
+    j.tiles[t] = ti;
+    const bool planes = !(ti.flags & TF_GREY);
+    const size_t pl_slab = (size_t)j.npix_cap + 8;
+    const size_t lz_slab = (size_t)j.lz_cap + 8;
+    for (int k = 0; k < SK_PER_TILE; k++) {
+      StreamInfo st;
+      memset(&st, 0, sizeof(st));
+      if (k < 3) {
+        st.sym_off = (size_t)j.ntiles * 3 * j.npix_cap + (size_t)(t * 3 + k) * j.lz_cap;
+        st.slab_off = (size_t)j.ntiles * 3 * pl_slab + (size_t)(t * 3 + k) * lz_slab;
+        st.slab_cap = (uint32_t)lz_slab;
+        st.n = k == 0 ? nf : nmk;
+        st.range = 256;
+        st.pb = 10;                                                   // lz.hpp:100-142
+      } else {
+        st.sym_off = (size_t)(t * 3 + k - 3) * j.npix_cap;
+        st.slab_off = (size_t)(t * 3 + k - 3) * pl_slab;
+        st.slab_cap = (uint32_t)pl_slab;
+        st.n = planes ? nclean : 0;
+        st.range = planes ? (k == SK_G ? 256 : 512) : 0;              // choh.cpp:221-255; 0 = absent
+        st.pb = 15;                                                   // layer_encode.hpp:59
+        st.fast = planes ? 1 : 0;
+      }
+      st.mode = SM_EMPTY;
+      st.ckpt_off = (uint32_t)((size_t)(t * SK_PER_TILE + k) * (j.npix_cap / HOH_SEG + 2));
+      j.streams[t * SK_PER_TILE + k] = st;
+    }
+  }
+}
+
+void launch_lz(const EncodeJob& j, hipStream_t s) {
+  hipLaunchKernelGGL(k_lz, dim3(j.ntiles), dim3(64), 0, s, j);
+}

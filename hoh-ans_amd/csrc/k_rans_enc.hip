@@ -1,0 +1,195 @@
+// rANS encoders (rans64.hpp:65-103, :262-278; entropy_encoding.hpp:206-238).
+//
+// Bit-exactness forces one serial coder state per stream (the reference never interleaves), so
+// the encoder is a latency-bound chain of 65,536 dependent steps per 256x256 tile plane.  The
+// fast kernel therefore spends all its effort on the length of that chain:
+//  * 12 streams per wave, one wave per CU (256 CUs x 12 = 3,072 = the planes of an 8192^2 image);
+//  * per-stream symbol tables staged in LDS, interleaved (symbol*16 + lane)*16 B so that one
+//    v_perm_b32 turns a packed u16 symbol into its LDS address;
+//  * the quotient floor(x/f) of the reciprocal step is computed exactly with two f64
+//    multiplications by 1/f rounded up two ulps (the high word first, then remainder*2^32 +
+//    low word, both < 2^53: exact floors), which is mathematically identical to the Alverson
+//    reciprocal of Rans64EncPutSymbol; the new low word is x_lo + c + ql*(2^15 - f);
+//  * symbols are prefetched two 8-symbol blocks ahead and table entries one block ahead;
+//  * each step writes its speculative output word to an LDS window and records the renorm
+//    decision in a bit mask; once per 32 steps only the emitted words are copied to the slab.
+// The generic kernel (LZ streams, other prob_bits) is the reference reciprocal step verbatim.
+// Both record decode checkpoints every HOH_SEG symbols (Recoil-style side index; the .hoh bytes
+// are unaffected).
+#include "hoh_internal.h"
+
+#define LANES 12
+#define TAB_BYTES (HOH_FAST_RANGE * 16 * 16)
+#define WIN 32
+
+__device__ __forceinline__ uint32_t plane_sid(int pi) { return (pi / 3) * SK_PER_TILE + SK_G + pi % 3; }
+
+__device__ __forceinline__ void lookup8(EncFast* e, uint4 sy, const unsigned char* lds, uint32_t lb) {
+  const uint32_t w[4] = {sy.x, sy.y, sy.z, sy.w};
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    e[k] = *(const EncFast*)(lds + __builtin_amdgcn_perm(w[k >> 1], lb, (k & 1) ? 0x0C070600u : 0x0C050400u));
+}
+
+struct Coder {
+  uint32_t xh, xl, mask, slot;
+  uint32_t widx;
+  uint32_t* slab;
+  uint32_t* win;
+};
+
+__device__ __forceinline__ void flush_win(Coder& c) {
+  uint32_t m = c.mask;
+  const uint32_t shift = WIN - c.slot;
+  while (m) {
+    const uint32_t t = __builtin_clz(m) - shift;
+    c.slab[--c.widx] = c.win[t];
+    m &= ~(0x80000000u >> (t + shift));
+  }
+  c.mask = 0;
+  c.slot = 0;
+}
+
+// one step, prob_bits 15 (x_max = f << 48)
+__device__ __forceinline__ void step15(Coder& c, const EncFast& e) {
+  c.win[c.slot] = c.xl;
+  const uint32_t f = e.f;
+  const bool emit = (c.xh >> 16) >= f;
+  const uint32_t nh = emit ? 0u : c.xh;
+  const uint32_t nl = emit ? c.xh : c.xl;
+  const uint32_t qh = (uint32_t)((double)nh * e.inv);
+  const uint32_t rh = nh - qh * f;
+  const double nd = fma((double)rh, 4294967296.0, (double)nl);
+  const uint32_t ql = (uint32_t)(nd * e.inv);
+  c.xl = nl + e.c + ql * (32768u - f);
+  c.xh = __builtin_amdgcn_alignbit(qh, ql, 17);
+  c.mask = (c.mask << 1) | (emit ? 1u : 0u);
+  c.slot++;
+}
+
+__device__ __forceinline__ void ckpt(const Coder& c, Checkpoint* ck, uint32_t k) {
+  Checkpoint p;
+  p.xl = c.xl; p.xh = c.xh; p.widx = c.widx - __popc(c.mask); p.pad = 0;
+  ck[k] = p;
+}
+
+__global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int lane = threadIdx.x;
+  const int pi0 = blockIdx.x * LANES;
+  for (int i = lane; i < HOH_FAST_RANGE * 16; i += 64) {
+    const int l = i & 15, sy = i >> 4;
+    EncFast v;
+    v.inv = 1.0; v.f = 1; v.c = 0;
+    if (l < LANES && pi0 + l < nplane) {
+      const uint32_t sid = plane_sid(pi0 + l);
+      if (j.streams[sid].fast) v = j.tab_fast[(size_t)sid * HOH_FAST_RANGE + sy];
+    }
+    ((EncFast*)lds)[i] = v;
+  }
+  __syncthreads();
+  const int pi = pi0 + lane;
+  if (lane >= LANES || pi >= nplane) return;
+  const uint32_t sid = plane_sid(pi);
+  StreamInfo st = j.streams[sid];
+  if (!st.fast || st.mode != SM_RANS || st.err || st.n == 0) return;
+  const uint32_t n = st.n;
+  Coder c;
+  c.xh = 0; c.xl = 1u << 31; c.mask = 0; c.slot = 0;
+  c.slab = j.slabs + st.slab_off;
+  c.widx = st.slab_cap;
+  c.win = (uint32_t*)(lds + TAB_BYTES + lane * WIN * 4);
+  Checkpoint* ck = j.ckpt + st.ckpt_off;
+  const uint32_t lb = lane * 16;
+  const uint16_t* sp = j.sym + st.sym_off;
+  // prologue: the top n % 32 symbols one at a time (descending); the rest is whole windows
+  const uint32_t r = n & 31, nb = (n - r) / 8;   // nb 8-symbol blocks, a multiple of 4
+  for (uint32_t i = n; i > n - r; i--) {
+    const uint32_t s = sp[i - 1];
+    const EncFast e = *(const EncFast*)(lds + ((s << 8) | lb));
+    step15(c, e);
+  }
+  flush_win(c);
+  if (((nb * 8) % HOH_SEG) == 0 && nb * 8 < n) ckpt(c, ck, nb * 8 / HOH_SEG);
+  if (nb) {
+    const uint4* sp4 = (const uint4*)sp;
+    EncFast eA[8], eB[8];
+    uint4 s1 = sp4[nb - 2];
+    uint4 s0 = sp4[nb - 3];
+    lookup8(eA, sp4[nb - 1], lds, lb);
+    for (int b = (int)nb - 1; b >= 3; b -= 4) {
+      // entering: eA = entries of block b, s1 = symbols of b-1, s0 = symbols of b-2
+      lookup8(eB, s1, lds, lb);
+      if (b - 3 >= 0) s1 = sp4[b - 3];
+#pragma unroll
+      for (int k = 7; k >= 0; --k) step15(c, eA[k]);
+      if ((b & 127) == 0) ckpt(c, ck, (uint32_t)b * 8 / HOH_SEG);
+      lookup8(eA, s0, lds, lb);
+      if (b - 4 >= 0) s0 = sp4[b - 4];
+#pragma unroll
+      for (int k = 7; k >= 0; --k) step15(c, eB[k]);
+      if (((b - 1) & 127) == 0) ckpt(c, ck, (uint32_t)(b - 1) * 8 / HOH_SEG);
+      lookup8(eB, s1, lds, lb);
+      if (b - 5 >= 0) s1 = sp4[b - 5];
+#pragma unroll
+      for (int k = 7; k >= 0; --k) step15(c, eA[k]);
+      if (((b - 2) & 127) == 0) ckpt(c, ck, (uint32_t)(b - 2) * 8 / HOH_SEG);
+      if (b - 4 >= 0) lookup8(eA, s0, lds, lb);
+      if (b - 6 >= 0) s0 = sp4[b - 6];
+#pragma unroll
+      for (int k = 7; k >= 0; --k) step15(c, eB[k]);
+      if (((b - 3) & 127) == 0) ckpt(c, ck, (uint32_t)(b - 3) * 8 / HOH_SEG);
+      flush_win(c);
+    }
+  }
+  flush_win(c);
+  c.slab[--c.widx] = c.xh;                 // Rans64EncFlush: lo at the lower address
+  c.slab[--c.widx] = c.xl;
+  if (lane < LANES) {
+    j.streams[sid].words = st.slab_cap - c.widx;
+    j.streams[sid].widx_end = c.widx;
+  }
+}
+
+// Generic: one lane per stream, rans64.hpp:262-278 verbatim (64x64 high product).
+__global__ __launch_bounds__(64) void k_rans_gen(EncodeJob j, int nstreams) {
+  const int sid = blockIdx.x * 64 + threadIdx.x;
+  if (sid >= nstreams) return;
+  StreamInfo st = j.streams[sid];
+  if (st.fast || st.mode != SM_RANS || st.err || st.n == 0) return;
+  const uint16_t* sp = j.sym + st.sym_off;
+  const EncGen* tab = j.tab_gen + (size_t)sid * j.gen_stride;
+  uint32_t* slab = j.slabs + st.slab_off;
+  Checkpoint* ck = j.ckpt + st.ckpt_off;
+  uint32_t widx = st.slab_cap;
+  const uint32_t pb = st.pb;
+  uint64_t x = 1ull << 31;
+  for (uint32_t i = st.n; i > 0; i--) {
+    const EncGen g = tab[sp[i - 1]];
+    const uint64_t x_max = (((1ull << 31) >> pb) << 32) * g.freq;
+    if (x >= x_max) {
+      slab[--widx] = (uint32_t)x;
+      x >>= 32;
+    }
+    const uint64_t q = __umul64hi(x, g.rcp) >> g.shift;
+    x = x + g.bias + q * g.cmpl;
+    if (((i - 1) % HOH_SEG) == 0) {
+      Checkpoint p;
+      p.xl = (uint32_t)x; p.xh = (uint32_t)(x >> 32); p.widx = widx; p.pad = 0;
+      ck[(i - 1) / HOH_SEG] = p;
+    }
+  }
+  slab[--widx] = (uint32_t)(x >> 32);
+  slab[--widx] = (uint32_t)x;
+  j.streams[sid].words = st.slab_cap - widx;
+  j.streams[sid].widx_end = widx;
+}
+
+void launch_rans_fast(const EncodeJob& j, const uint32_t*, int nplane, hipStream_t s) {
+  const int grid = (nplane + LANES - 1) / LANES;
+  hipLaunchKernelGGL(k_rans_fast, dim3(grid), dim3(64), TAB_BYTES + 16 * WIN * 4, s, j, nplane);
+}
+
+void launch_rans_gen(const EncodeJob& j, int nstreams, hipStream_t s) {
+  hipLaunchKernelGGL(k_rans_gen, dim3((nstreams + 63) / 64), dim3(64), 0, s, j, nstreams);
+}

@@ -1,0 +1,243 @@
+// Per-stream table construction, one wave per stream (entropy_encoding.hpp:19-216):
+//  histogram -> normalize_freqs (stattools.hpp:13-70, wave-parallel steal search with the
+//  reference's "first strictly smallest freq > 1" rule) -> clamp scan and expected sizes
+//  (entropy_encoding.hpp:45-122, with the reference's 32-bit / size_t wrap arithmetic) ->
+//  serialised header + frequency table (MSB-first stuffer with the reference's unmasked
+//  overflow, varint.hpp:47-77) -> encoder symbol tables for the rANS kernels.
+#include "hoh_internal.h"
+
+#define MAXR 4096
+
+struct Sink { uint8_t* b; uint32_t loc; uint32_t rem; uint32_t br; };
+
+// stuffer (varint.hpp:47-77) without recursion: a field wider than the free bits and than 8
+// is split into a top part and 8-bit bottoms exactly as the recursive calls do
+__device__ void stuff_base(Sink& s, uint32_t v, uint32_t bits) {
+  if (bits < s.br) {
+    s.rem = (uint8_t)(s.rem + (uint8_t)(v << (s.br - bits)));
+    s.br -= bits;
+  } else if (bits == s.br) {
+    s.b[s.loc++] = (uint8_t)(s.rem + (uint8_t)v);
+    s.rem = 0;
+    s.br = 8;
+  } else {
+    s.b[s.loc++] = (uint8_t)(s.rem + (uint8_t)(v >> (bits - s.br)));
+    s.br = 8 - (bits - s.br);
+    s.rem = (uint8_t)((v << s.br) % 256);
+  }
+}
+
+__device__ void stuff(Sink& s, uint32_t v, uint32_t bits) {
+  uint32_t pend[4];
+  int np = 0;
+  while (bits > s.br && bits > 8 && np < 4) {
+    pend[np++] = v % 256;
+    v >>= 8;
+    bits -= 8;
+  }
+  stuff_base(s, v, bits);
+  while (np > 0) stuff_base(s, pend[--np], 8);
+}
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    uint64_t u = __shfl_xor(v, o);
+    v = u < v ? u : v;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(64) void k_tables(EncodeJob j) {
+  __shared__ uint32_t fr[MAXR];
+  __shared__ uint32_t cum[MAXR + 1];
+  __shared__ uint32_t s_err;
+  const int s = blockIdx.x, lane = threadIdx.x;
+  StreamInfo st = j.streams[s];
+  uint8_t* hd = j.hdr + (size_t)s * j.hdr_cap;
+  if (st.range == 0) {                     // absent stream (bitimage tile)
+    if (lane == 0) { st.size = 0; st.hdr_len = 0; st.mode = SM_EMPTY; j.streams[s] = st; }
+    return;
+  }
+  const uint32_t range = st.range, n = st.n, pb = st.pb;
+  uint32_t vlen = hoh_write_varint(hd, 0, range - 1);
+  vlen = hoh_write_varint(hd, vlen, n);
+  if (n == 0) {                            // entropy_encoding.hpp:19-23
+    if (lane == 0) { st.vlen = st.hdr_len = st.size = vlen; st.mode = SM_EMPTY; st.fast = 0; j.streams[s] = st; }
+    return;
+  }
+  if (pb == 0 || pb > 31 || range > MAXR || range > j.gen_stride || ((uint64_t)1 << pb) < range) {
+    if (lane == 0) { st.err = 1; j.streams[s] = st; atomicOr(j.gerr, 1u); }
+    return;
+  }
+  if (lane == 0) s_err = 0;
+  for (uint32_t i = lane; i < range; i += 64) fr[i] = 0;
+  __syncthreads();
+  const uint16_t* sy = j.sym + st.sym_off;
+  const int kind = s % SK_PER_TILE;
+  if (j.hist && kind >= SK_G && j.tiles) {
+    for (uint32_t i = lane; i < range; i += 64) fr[i] = j.hist[(size_t)s * 512 + i];
+  } else {
+    for (uint32_t i = lane; i < n; i += 64) {
+      uint32_t v = sy[i];
+      if (v < range) atomicAdd(&fr[v], 1u); else s_err = 1;
+    }
+  }
+  __syncthreads();
+  if (s_err) {
+    if (lane == 0) { st.err = 2; j.streams[s] = st; atomicOr(j.gerr, 2u); }
+    return;
+  }
+  // ---- normalize_freqs: cumulative (wave scan over contiguous chunks)
+  const uint32_t chunk = (range + 63) / 64;
+  const uint32_t c0 = lane * chunk, c1 = min(range, c0 + chunk);
+  uint32_t local = 0;
+  for (uint32_t i = c0; i < c1; i++) local += fr[i];
+  uint32_t incl = local;
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t u = __shfl_up(incl, o);
+    if (lane >= o) incl += u;
+  }
+  uint32_t run = incl - local;
+  for (uint32_t i = c0; i < c1; i++) { run += fr[i]; cum[i + 1] = run; }
+  if (lane == 0) cum[0] = 0;
+  __syncthreads();
+  const uint32_t total = cum[range];
+  const uint32_t target = 1u << pb;
+  for (uint32_t i = 1 + lane; i <= range; i += 64) cum[i] = (uint32_t)(((uint64_t)target * cum[i]) / total);
+  __syncthreads();
+  for (uint32_t base = 0; base < range; base += 64) {
+    const uint32_t i0 = base + lane;
+    uint64_t zm = __ballot(i0 < range && fr[i0] && cum[i0 + 1] == cum[i0]);
+    while (zm) {
+      const uint32_t i = base + (__ffsll((unsigned long long)zm) - 1);
+      zm &= zm - 1;
+      uint64_t key = ~0ull;
+      for (uint32_t jj = lane; jj < range; jj += 64) {
+        uint32_t f = cum[jj + 1] - cum[jj];
+        if (f > 1) { uint64_t k = ((uint64_t)f << 32) | jj; key = k < key ? k : key; }
+      }
+      key = wave_min_u64(key);
+      if (key == ~0ull) { if (lane == 0) s_err = 3; break; }
+      const uint32_t best = (uint32_t)key;
+      if (best < i) {
+        for (uint32_t jj = best + 1 + lane; jj <= i; jj += 64) cum[jj]--;
+      } else {
+        for (uint32_t jj = i + 1 + lane; jj <= best; jj += 64) cum[jj]++;
+      }
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+  if (s_err) {
+    if (lane == 0) { st.err = 3; j.streams[s] = st; atomicOr(j.gerr, 4u); }
+    return;
+  }
+  for (uint32_t i = lane; i < range; i += 64) fr[i] = cum[i + 1] - cum[i];
+  __syncthreads();
+  // ---- encoder symbol tables
+  const bool fast = (pb == 15 && range <= HOH_FAST_RANGE && st.fast);
+  for (uint32_t i = lane; i < (fast ? (uint32_t)HOH_FAST_RANGE : range); i += 64) {
+    const uint32_t f = i < range ? fr[i] : 0, c = i < range ? cum[i] : 0;
+    if (fast) {
+      EncFast e;
+      if (f) {
+        double inv = 1.0 / (double)f;
+        unsigned long long b = __double_as_longlong(inv);
+        e.inv = __longlong_as_double((long long)(b + 2));   // round up by two ulps
+      } else {
+        e.inv = 1.0;
+      }
+      e.f = f ? f : 1;
+      e.c = c;
+      j.tab_fast[(size_t)s * HOH_FAST_RANGE + i] = e;
+    } else {
+      EncGen g;                                           // rans64.hpp:167-247
+      g.freq = f;
+      g.cmpl = (1u << pb) - f;
+      if (f < 2) {
+        g.rcp = ~0ull; g.shift = 0; g.bias = c + (1u << pb) - 1;
+      } else {
+        uint32_t shift = 0;
+        while (f > (1u << shift)) shift++;
+        uint64_t x0 = f - 1, x1 = 1ull << (shift + 31);
+        uint64_t t1 = x1 / f;
+        x0 += (x1 % f) << 32;
+        uint64_t t0 = x0 / f;
+        g.rcp = t0 + (t1 << 32); g.shift = shift - 1; g.bias = c;
+      }
+      j.tab_gen[(size_t)s * j.gen_stride + i] = g;
+    }
+  }
+  if (lane != 0) return;
+  // ---- header + table bytes (entropy_encoding.hpp:43-200), lane 0
+  const uint32_t maxbits = hoh_bitlen(range - 1);
+  const uint64_t expected_stored = vlen + 1 + ((uint64_t)maxbits * n + 8 - 1) / 8;
+  const uint64_t expected_raw = ((uint64_t)pb * range + 8 - 1) / 8;
+  const uint32_t cn32 = (pb - 1) / 4 + 2;
+  uint64_t exp_cl = (uint64_t)(uint32_t)((uint32_t)(2 * ((int)maxbits - 1)) * cn32);
+  exp_cl += (uint64_t)(uint32_t)(pb * 2);
+  const uint32_t cn = (uint8_t)cn32;
+  uint16_t lower[16], upper[16];
+  uint64_t size_bits = 0, climb = 0, lci = 0;
+  for (; climb < range; climb++) {
+    while ((uint64_t)fr[climb] >= (uint64_t)(1u << size_bits)) {
+      uint64_t idx;
+      if (size_bits == 0) { size_bits = 1; idx = 0; lci = 1; }
+      else if (size_bits == 1) { size_bits = 4; idx = 1; lci = 2; }
+      else { idx = size_bits / 4 + 1; size_bits += 4; lci++; }
+      if (idx < cn && idx < 16) lower[idx] = (uint16_t)climb;    // overrun write dropped (see oracle)
+    }
+    if (size_bits >= pb) { size_bits = pb; exp_cl += size_bits; break; }
+    exp_cl += size_bits;
+  }
+  while (lci < cn && lci < 16) lower[lci++] = (uint16_t)(range - 1);
+  size_bits = 0;
+  uint64_t climb2 = range - 1, uci = 0;
+  for (;; climb2--) {
+    while ((uint64_t)fr[climb2] >= (uint64_t)(1u << size_bits)) {
+      uint64_t idx;
+      if (size_bits == 0) { size_bits = 1; idx = 0; uci = 1; }
+      else if (size_bits == 1) { size_bits = 4; idx = 1; uci = 2; }
+      else { idx = size_bits / 4 + 1; size_bits += 4; uci++; }
+      if (idx < cn && idx < 16) upper[idx] = (uint16_t)climb2;
+    }
+    if (size_bits >= pb) { size_bits = pb; exp_cl += size_bits; break; }
+    exp_cl += size_bits;
+    if (climb2 == 0) break;
+  }
+  while (uci < cn && uci < 16) upper[uci++] = 0;
+  exp_cl += size_bits * (climb2 - climb - 1);                          // size_t wrap (Q5)
+  exp_cl = (exp_cl + 8 - 1) / 8;
+  Sink sk{hd, vlen, 0, 8};
+  if (expected_raw < exp_cl) {
+    hd[sk.loc++] = (uint8_t)((1u << 7) + (pb << 2) + 1);
+    for (uint32_t i = 0; i < range; i++) stuff(sk, fr[i], maxbits);
+  } else {
+    hd[sk.loc++] = (uint8_t)((1u << 7) + (pb << 2) + 2);
+    for (uint32_t i = 0; i < cn; i++) {
+      stuff(sk, lower[i], maxbits);
+      stuff(sk, upper[i], maxbits);
+    }
+    for (uint32_t i = 0; i < range; i++) {
+      uint32_t sb = 0;
+      if (lower[0] <= i && upper[0] >= i) sb = 1;
+      if (lower[1] <= i && upper[1] >= i) sb = 4;
+      for (uint32_t jj = 2; jj < cn; jj++)
+        if (lower[jj] <= i && upper[jj] >= i) sb = 4 * jj;
+      if (sb > pb) sb = pb;
+      stuff(sk, fr[i], sb);
+    }
+  }
+  if (sk.br != 8) hd[sk.loc++] = (uint8_t)sk.rem;
+  st.vlen = vlen;
+  st.hdr_len = sk.loc;
+  st.maxbits = maxbits;
+  st.expected_stored = expected_stored;
+  st.fast = fast ? 1 : 0;
+  st.mode = SM_RANS;
+  j.streams[s] = st;
+}
+
+void launch_tables(const EncodeJob& j, int nstreams, hipStream_t s) {
+  hipLaunchKernelGGL(k_tables, dim3(nstreams), dim3(64), 0, s, j);
+}

@@ -1,0 +1,320 @@
+"""hoh_ans -- Python mirror of the hoh-ANS hot-path API on the MI355X library (libhohgpu.so).
+
+The reference's interface is a set of C++ free functions (entropy_encoding.hpp:8,
+entropy_decoding.hpp:134, layer_encode.hpp:11, layer_decode.hpp:128, prediction.hpp:6,
+unprediction.hpp:6, channel.hpp:73) driven by the choh / dhoh CLIs.  This module exposes the
+same operations, same names and argument meaning, over the C ABI in include/hoh_ans.h:
+
+    encode_entropy(symbols, range, prob_bits)   -> bytes             (entropy_encoding.hpp:8)
+    decode_entropy(data, byte_pointer=0)        -> (symbols, bp)     (entropy_decoding.hpp:134)
+    layer_encode(plane, depth, nuke=None)       -> bytes             (layer_encode.hpp:11, -s0)
+    channelpredict_fastpath(plane, depth)       -> residuals         (prediction.hpp:6)
+    unpredict_fastpath(res, w, h, depth, backref=None) -> plane      (unprediction.hpp:6)
+    subtract_green(rgb)                         -> (G, R-G+256, B-G+256)   (channel.hpp:73)
+    choh(rgb)                                   -> (bytes, printed)  (choh.cpp:394, -s0)
+    dhoh(data)                                  -> rgb               (dhoh.cpp:297, fixed)
+
+Device-resident variants (encode_image / decode_image) take torch tensors already in HBM; they
+are what bench.py times.  Errors raise HohError carrying the C status code.  There is no CPU
+fallback: a missing library or GPU raises.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIBPATH = os.path.join(os.path.dirname(HERE), "lib", "libhohgpu.so")
+
+HOH_OK = 0
+ERRNAMES = {1: "E_ARG", 2: "E_CAP", 3: "E_HIP", 4: "E_RANGE", 5: "E_UNREPRODUCIBLE", 6: "E_UNSUPPORTED",
+            7: "E_CORRUPT", 8: "E_NODEV"}
+
+_L = None
+vp = C.c_void_p
+sz = C.c_size_t
+szp = C.POINTER(C.c_size_t)
+ip = C.POINTER(C.c_int)
+
+
+class HohError(RuntimeError):
+    def __init__(self, code, what=""):
+        self.code = code
+        super().__init__("%s: %s (%d)" % (what, ERRNAMES.get(code, "?"), code))
+
+
+def lib():
+    """Load libhohgpu.so (built in-tree by `make` / __graft_entry__.build())."""
+    global _L
+    if _L is None:
+        if not os.path.exists(LIBPATH):
+            raise RuntimeError("libhohgpu.so not built: run `make` (or __graft_entry__.build())")
+        L = C.CDLL(LIBPATH)
+        L.hoh_ctx_create.argtypes = [C.POINTER(vp), C.c_int]
+        L.hoh_ctx_destroy.argtypes = [vp]
+        L.hoh_strerror.restype = C.c_char_p
+        L.hoh_version.restype = C.c_char_p
+        L.hoh_set_profiling.argtypes = [vp, C.c_int]
+        L.hoh_get_kernel_ms.argtypes = [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.c_int]
+        L.hoh_encode_bound.restype = sz
+        L.hoh_encode_bound.argtypes = [C.c_int, C.c_int]
+        L.hoh_encode_image.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, vp, sz, szp, szp, vp]
+        L.hoh_encode_image_ix.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, vp, sz, szp, szp, vp, vp]
+        L.hoh_index_create.argtypes = [C.POINTER(vp)]
+        L.hoh_index_destroy.argtypes = [vp]
+        L.hoh_index_bytes.restype = sz
+        L.hoh_index_bytes.argtypes = [vp]
+        L.hoh_encode_tiles.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, sz, vp, szp, vp]
+        L.hoh_file_prefix.restype = sz
+        L.hoh_file_prefix.argtypes = [C.c_int, C.c_int, vp, C.c_int, vp, sz]
+        L.hoh_tiling.argtypes = [C.c_int, C.c_int, ip, ip, ip, ip]
+        L.hoh_peek_header.argtypes = [vp, sz, ip, ip, ip, ip]
+        L.hoh_synth_rgb.argtypes = [vp, vp, C.c_int, C.c_int, C.c_uint64, C.c_int, vp]
+        for name, args in (
+            ("hoh_decode_image", [vp, vp, sz, vp, sz, ip, ip, vp]),
+            ("hoh_decode_image_ix", [vp, vp, sz, vp, sz, ip, ip, vp, vp]),
+            ("hoh_encode_entropy", [vp, vp, sz, sz, C.c_uint32, vp, sz, szp]),
+            ("hoh_decode_entropy", [vp, vp, sz, szp, vp, sz, szp]),
+            ("hoh_entropy_count", [vp, sz, sz, szp]),
+            ("hoh_layer_encode", [vp, vp, sz, C.c_int, C.c_int, C.c_int, sz, vp, vp, sz, szp]),
+            ("hoh_layer_decode", [vp, vp, sz, sz, C.c_int, C.c_int, C.c_int, vp, vp]),
+            ("hoh_predict_fastpath", [vp, vp, C.c_int, C.c_int, C.c_int, vp]),
+            ("hoh_unpredict_fastpath", [vp, vp, sz, vp, C.c_int, C.c_int, C.c_int, vp]),
+            ("hoh_subtract_green", [vp, vp, sz, vp, vp, vp]),
+            ("hoh_add_green", [vp, vp, vp, vp, sz, vp]),
+        ):
+            if hasattr(L, name):
+                getattr(L, name).argtypes = args
+        if hasattr(L, "hoh_entropy_bound"):
+            L.hoh_entropy_bound.restype = sz
+            L.hoh_entropy_bound.argtypes = [sz, sz, C.c_uint32]
+        _L = L
+    return _L
+
+
+def check(code, what):
+    if code != HOH_OK:
+        raise HohError(code, what)
+
+
+def _p(a):
+    return a.ctypes.data_as(vp)
+
+
+class Context:
+    """One HIP device context (workspaces + stream).  Use one per thread per GPU."""
+
+    def __init__(self, device=0):
+        self.h = vp()
+        check(lib().hoh_ctx_create(C.byref(self.h), device), "hoh_ctx_create")
+        self.device = device
+
+    def close(self):
+        if self.h:
+            lib().hoh_ctx_destroy(self.h)
+            self.h = vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def profiling(self, on=True):
+        lib().hoh_set_profiling(self.h, 1 if on else 0)
+
+    def kernel_ms(self):
+        names = (C.c_char_p * 64)()
+        ms = (C.c_float * 64)()
+        n = lib().hoh_get_kernel_ms(self.h, names, ms, 64)
+        return [(names[i].decode(), ms[i]) for i in range(n)]
+
+
+_CTX = None
+
+
+def default_ctx():
+    global _CTX
+    if _CTX is None:
+        _CTX = Context(0)
+    return _CTX
+
+
+def tiling(W, H):
+    xt, yt, tw, th = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+    tiled = lib().hoh_tiling(W, H, C.byref(xt), C.byref(yt), C.byref(tw), C.byref(th))
+    return bool(tiled), xt.value, yt.value, tw.value, th.value
+
+
+# ------------------------------------------------------------------ device-resident (torch) API
+
+def _stream_ptr(torch):
+    return vp(torch.cuda.current_stream().cuda_stream)
+
+
+class Index:
+    """Decode side index (encoder checkpoints), kept beside the .hoh bytes."""
+
+    def __init__(self):
+        self.h = vp()
+        check(lib().hoh_index_create(C.byref(self.h)), "hoh_index_create")
+
+    def nbytes(self):
+        return lib().hoh_index_bytes(self.h)
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().hoh_index_destroy(self.h)
+        except Exception:
+            pass
+
+
+def encode_image(rgb_dev, W, H, out_dev=None, ctx=None, index=None):
+    """rgb_dev: uint8 torch tensor (W*H*3) in HBM.  Returns (out tensor, size, printed)."""
+    import torch
+    ctx = ctx or default_ctx()
+    if out_dev is None:
+        out_dev = torch.empty(lib().hoh_encode_bound(W, H), dtype=torch.uint8, device=rgb_dev.device)
+    n, printed = C.c_size_t(0), C.c_size_t(0)
+    r = lib().hoh_encode_image_ix(ctx.h, vp(rgb_dev.data_ptr()), W, H, 0, vp(out_dev.data_ptr()),
+                                  out_dev.numel(), C.byref(n), C.byref(printed),
+                                  index.h if index is not None else None, _stream_ptr(torch))
+    check(r, "hoh_encode_image")
+    return out_dev, n.value, printed.value
+
+
+def decode_image(hoh_dev, size, out_dev=None, ctx=None, index=None):
+    """hoh_dev: uint8 torch tensor holding `size` bytes of a .hoh.  Returns (rgb tensor, W, H)."""
+    import torch
+    ctx = ctx or default_ctx()
+    head = hoh_dev[:min(size, 16)].cpu().numpy()
+    W, H = peek_header(head.tobytes())[:2]
+    if out_dev is None:
+        out_dev = torch.empty(W * H * 3, dtype=torch.uint8, device=hoh_dev.device)
+    w, h = C.c_int(), C.c_int()
+    r = lib().hoh_decode_image_ix(ctx.h, vp(hoh_dev.data_ptr()), size, vp(out_dev.data_ptr()),
+                                  out_dev.numel(), C.byref(w), C.byref(h),
+                                  index.h if index is not None else None, _stream_ptr(torch))
+    check(r, "hoh_decode_image")
+    return out_dev, w.value, h.value
+
+
+def encode_tiles(rgb_dev, W, H, t0, ntiles, out_dev, sizes_dev, ctx=None):
+    import torch
+    ctx = ctx or default_ctx()
+    n = C.c_size_t(0)
+    r = lib().hoh_encode_tiles(ctx.h, vp(rgb_dev.data_ptr()), W, H, t0, ntiles, vp(out_dev.data_ptr()),
+                               out_dev.numel(), vp(sizes_dev.data_ptr()), C.byref(n), _stream_ptr(torch))
+    check(r, "hoh_encode_tiles")
+    return n.value
+
+
+def file_prefix(W, H, tile_sizes):
+    ts = np.ascontiguousarray(tile_sizes, dtype=np.uint32)
+    buf = np.empty(64 + 3 * ts.size, np.uint8)
+    n = lib().hoh_file_prefix(W, H, _p(ts), ts.size, _p(buf), buf.size)
+    if n == 0:
+        raise HohError(1, "hoh_file_prefix")
+    return buf[:n].tobytes()
+
+
+def peek_header(data):
+    b = np.frombuffer(bytes(data[:64]), np.uint8).copy()
+    W, H, xt, yt = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+    check(lib().hoh_peek_header(_p(b), b.size, C.byref(W), C.byref(H), C.byref(xt), C.byref(yt)), "hoh_peek_header")
+    return W.value, H.value, xt.value, yt.value
+
+
+def synth_rgb_dev(W, H, seed=1, noise=4, ctx=None, device="cuda"):
+    """Synthetic image generated in HBM (same bytes as hoh_ans.synth.synth_rgb)."""
+    import torch
+    ctx = ctx or default_ctx()
+    t = torch.empty(W * H * 3, dtype=torch.uint8, device=device)
+    check(lib().hoh_synth_rgb(ctx.h, vp(t.data_ptr()), W, H, seed, noise, _stream_ptr(torch)), "hoh_synth_rgb")
+    return t
+
+
+# ------------------------------------------------------------------ host-buffer API (reference names)
+
+def choh(rgb, ctx=None):
+    """`choh in out W H -s0` on an (H, W, 3) uint8 array -> (file bytes, printed size)."""
+    import torch
+    rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
+    H, W, _ = rgb.shape
+    d = torch.from_numpy(rgb.reshape(-1)).cuda()
+    out, n, printed = encode_image(d, W, H, ctx=ctx)
+    torch.cuda.synchronize()
+    return out[:n].cpu().numpy().tobytes(), printed
+
+
+def dhoh(data, ctx=None, index=None):
+    import torch
+    b = torch.from_numpy(np.frombuffer(bytes(data), np.uint8).copy()).cuda()
+    rgb, W, H = decode_image(b, len(data), ctx=ctx, index=index)
+    torch.cuda.synchronize()
+    return rgb.cpu().numpy().reshape(H, W, 3)
+
+
+def encode_entropy(symbols, range_, prob_bits, ctx=None):
+    ctx = ctx or default_ctx()
+    s = np.ascontiguousarray(symbols, dtype=np.uint16)
+    cap = lib().hoh_entropy_bound(s.size, range_, prob_bits)
+    out = np.empty(cap, np.uint8)
+    n = C.c_size_t(0)
+    check(lib().hoh_encode_entropy(ctx.h, _p(s), s.size, range_, prob_bits, _p(out), cap, C.byref(n)),
+          "hoh_encode_entropy")
+    return out[:n.value].tobytes()
+
+
+def decode_entropy(data, byte_pointer=0, ctx=None):
+    ctx = ctx or default_ctx()
+    b = np.frombuffer(bytes(data), np.uint8).copy()
+    cnt = C.c_size_t(0)
+    check(lib().hoh_entropy_count(_p(b), b.size, byte_pointer, C.byref(cnt)), "hoh_entropy_count")
+    out = np.empty(max(cnt.value, 1), np.uint16)
+    bp, n = C.c_size_t(byte_pointer), C.c_size_t(0)
+    check(lib().hoh_decode_entropy(ctx.h, _p(b), b.size, C.byref(bp), _p(out), out.size, C.byref(n)),
+          "hoh_decode_entropy")
+    return out[:n.value], bp.value
+
+
+def layer_encode(plane, depth, nuke=None, ctx=None):
+    ctx = ctx or default_ctx()
+    p = np.ascontiguousarray(plane, dtype=np.uint16)
+    h, w = p.shape
+    nk = None if nuke is None else np.ascontiguousarray(nuke, dtype=np.uint8)
+    cap = lib().hoh_entropy_bound(p.size, 1 << depth, 15) + 16
+    out = np.empty(cap, np.uint8)
+    n = C.c_size_t(0)
+    check(lib().hoh_layer_encode(ctx.h, _p(p), p.size, w, h, depth, 0, None if nk is None else _p(nk),
+                                 _p(out), cap, C.byref(n)), "hoh_layer_encode")
+    return out[:n.value].tobytes()
+
+
+def channelpredict_fastpath(plane, depth, ctx=None):
+    ctx = ctx or default_ctx()
+    p = np.ascontiguousarray(plane, dtype=np.uint16)
+    h, w = p.shape
+    out = np.empty_like(p)
+    check(lib().hoh_predict_fastpath(ctx.h, _p(p), w, h, depth, _p(out)), "hoh_predict_fastpath")
+    return out
+
+
+def unpredict_fastpath(res, w, h, depth, backref=None, ctx=None):
+    ctx = ctx or default_ctx()
+    r = np.ascontiguousarray(res, dtype=np.uint16)
+    br = None if backref is None else np.ascontiguousarray(backref, dtype=np.uint16)
+    out = np.empty((h, w), np.uint16)
+    check(lib().hoh_unpredict_fastpath(ctx.h, _p(r), r.size, None if br is None else _p(br), w, h, depth, _p(out)),
+          "hoh_unpredict_fastpath")
+    return out
+
+
+def subtract_green(rgb, ctx=None):
+    ctx = ctx or default_ctx()
+    a = np.ascontiguousarray(rgb, dtype=np.uint8)
+    n = a.size // 3
+    G, R, B = (np.empty(n, np.uint16) for _ in range(3))
+    check(lib().hoh_subtract_green(ctx.h, _p(a), n, _p(G), _p(R), _p(B)), "hoh_subtract_green")
+    return G, R, B

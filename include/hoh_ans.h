@@ -1,0 +1,158 @@
+/*
+ * hoh_ans.h -- C ABI of libhohgpu.so, the MI355X (gfx950) implementation of the hoh-ANS hot path:
+ * subtract-green colour transform, MED predictor / unpredictor, greedy RGB LZ, rans64 entropy
+ * stream coding and the .hoh tile container of `choh -s0` / `dhoh`.
+ *
+ * Conventions: plain pointers and sizes, integer status codes (HOH_OK == 0), no exceptions or
+ * C++ types across the boundary.  "d_" pointers are device (HBM) buffers; the others are host
+ * buffers.  `stream` is a hipStream_t passed as void* (NULL = the context's own stream).
+ * One context per host thread per device; contexts own grow-only device workspaces.
+ *
+ * Each entry point names the reference interface it replaces (hohMiyazawa/hoh-ANS @ v1,
+ * file:line).  The reference has no FFI of its own: its API is the set of free functions in
+ * the headers below, compiled into the choh / dhoh drivers.  include/hoh/ headers re-expose those
+ * exact C++ signatures on top of this ABI.
+ */
+#ifndef HOH_ANS_H
+#define HOH_ANS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---------------------------------------------------------------------- */
+#define HOH_OK 0
+#define HOH_E_ARG 1             /* invalid argument                                            */
+#define HOH_E_CAP 2             /* output capacity too small (*written / *out_size = needed)   */
+#define HOH_E_HIP 3             /* a HIP runtime call failed                                   */
+#define HOH_E_RANGE 4           /* symbol >= range, or range / prob_bits outside the supported
+                                   set (normalize_freqs assert, stattools.hpp:14)               */
+#define HOH_E_UNREPRODUCIBLE 5  /* the reference writes uninitialised bytes for this input
+                                   (grey non-binary tiles, choh.cpp:196-205; palette prefix
+                                   longer than the indexed layer, choh.cpp:301-308)             */
+#define HOH_E_UNSUPPORTED 6     /* valid but not implemented on this path (palette tiles,
+                                   -s1..-s4 predictor search, 4-channel formats)                */
+#define HOH_E_CORRUPT 7         /* decoder: malformed or undecodable bitstream (incl. the
+                                   reference's lossy raw tables)                     */
+#define HOH_E_NODEV 8           /* no GPU / HIP device unavailable                              */
+
+typedef struct hoh_ctx hoh_ctx;
+
+int hoh_ctx_create(hoh_ctx** ctx, int device);
+void hoh_ctx_destroy(hoh_ctx* ctx);
+const char* hoh_strerror(int code);
+const char* hoh_version(void);
+/* per-kernel device time of the last call, for measurement (ms); enable with hoh_set_profiling */
+void hoh_set_profiling(hoh_ctx* ctx, int on);
+int hoh_get_kernel_ms(hoh_ctx* ctx, const char** names, float* ms, int max);
+
+/* ---- image level: `choh in out W H -s0` / `dhoh in out` -------------------------------- */
+
+/* Worst-case .hoh size for a W x H image (stored planes + LZ streams + framing). */
+size_t hoh_encode_bound(int W, int H);
+
+/* Replaces choh.cpp:394-527 at cruncher_mode 0 (-s0).  Reads W*H*3 interleaved RGB bytes from
+ * d_rgb, writes the exact bytes choh writes (header-only for untiled images) to
+ * d_out.  *out_size = bytes written; *printed (optional) = the number choh prints
+ * (choh.cpp:522).  speed must be 0. */
+int hoh_encode_image(hoh_ctx* ctx, const uint8_t* d_rgb, int W, int H, int speed,
+                     uint8_t* d_out, size_t cap, size_t* out_size, size_t* printed, void* stream);
+
+/* Decode side index: the encoder's coder state every 1024 symbols of each plane stream (a
+ * Recoil-style checkpoint list kept BESIDE the .hoh, never inside it -- the file bytes are
+ * identical with or without it).  With an index the decoder splits every stream into
+ * independent segments; without one (any foreign .hoh) it decodes each stream serially.  A
+ * segment whose end state disagrees with the next checkpoint fails the decode (HOH_E_CORRUPT). */
+typedef struct hoh_index hoh_index;
+int hoh_index_create(hoh_index** idx);
+void hoh_index_destroy(hoh_index* idx);
+size_t hoh_index_bytes(const hoh_index* idx);
+int hoh_encode_image_ix(hoh_ctx* ctx, const uint8_t* d_rgb, int W, int H, int speed,
+                        uint8_t* d_out, size_t cap, size_t* out_size, size_t* printed,
+                        hoh_index* idx, void* stream);
+
+/* Replaces dhoh.cpp:297-396 (with the decoder defects of SURVEY Q1, Q9-Q12 fixed).  d_hoh holds
+ * `size` bytes of a .hoh file (as written by choh -s0); writes W*H*3 RGB bytes to d_rgb. */
+int hoh_decode_image(hoh_ctx* ctx, const uint8_t* d_hoh, size_t size, uint8_t* d_rgb, size_t cap,
+                     int* W, int* H, void* stream);
+int hoh_decode_image_ix(hoh_ctx* ctx, const uint8_t* d_hoh, size_t size, uint8_t* d_rgb, size_t cap,
+                        int* W, int* H, const hoh_index* idx, void* stream);
+
+/* Host-side header parse: W, H and tiling of a .hoh (dhoh.cpp:320-366). */
+int hoh_peek_header(const uint8_t* hoh, size_t size, int* W, int* H, int* x_tiles, int* y_tiles);
+
+/* ---- sharded image encode (multi-GPU: one process per GPU) ------------------------------ */
+
+/* Encodes tiles [t0, t0+ntiles) (row-major tile index, choh.cpp:464-500) of the W x H image into
+ * a blob of concatenated tile byte strings at d_out; d_tile_sizes (device, ntiles u32) receives
+ * each tile's size.  A rank's blob plus everyone's sizes are what the gather exchanges. */
+int hoh_encode_tiles(hoh_ctx* ctx, const uint8_t* d_rgb, int W, int H, int t0, int ntiles,
+                     uint8_t* d_out, size_t cap, uint32_t* d_tile_sizes, size_t* out_size,
+                     void* stream);
+/* Host: the .hoh prefix for a tiled image given every tile's size (choh.cpp:437-498):
+ * magic, format, depth, varint W-1, H-1, x_tiles-1, y_tiles-1, n-1 varint sizes.  Returns the
+ * prefix length, or 0 if cap is too small. */
+size_t hoh_file_prefix(int W, int H, const uint32_t* tile_sizes, int ntiles, uint8_t* out, size_t cap);
+/* tiling of choh.cpp:454-461: returns 1 if tiled */
+int hoh_tiling(int W, int H, int* x_tiles, int* y_tiles, int* tile_w, int* tile_h);
+
+/* ---- entropy stream level (host buffers; one call = one stream, batched inside) --------- */
+
+/* Replaces encode_entropy(uint16_t*, size_t, size_t, uint8_t*, uint32_t, uint8_t)
+ * (entropy_encoding.hpp:8-15; u8 overload :283-290).  Same bytes; *written = stream bytes. */
+int hoh_encode_entropy(hoh_ctx* ctx, const uint16_t* symbols, size_t n, size_t range,
+                       uint32_t prob_bits, uint8_t* out, size_t cap, size_t* written);
+size_t hoh_entropy_bound(size_t n, size_t range, uint32_t prob_bits);
+
+/* Replaces decode_entropy(uint8_t*, size_t, size_t*, size_t*, uint8_t)
+ * (entropy_decoding.hpp:134-140).  Advances *byte_pointer past the whole stream (Q1 fix);
+ * *n = symbol count; out must hold cap symbols (hoh_entropy_count tells the count). */
+int hoh_decode_entropy(hoh_ctx* ctx, const uint8_t* in, size_t in_size, size_t* byte_pointer,
+                       uint16_t* out, size_t cap, size_t* n);
+int hoh_entropy_count(const uint8_t* in, size_t in_size, size_t byte_pointer, size_t* n);
+
+/* Batched device form: nstreams streams, stream i = d_syms[h_offsets[i] .. + h_counts[i]]
+ * (h_offsets multiples of 8), all with the same range and prob_bits; stream i is written to
+ * d_out + h_out_offsets[i] (caller-chosen, each with hoh_entropy_bound room); h_sizes[i]
+ * receives its size. */
+int hoh_encode_entropy_batch(hoh_ctx* ctx, const uint16_t* d_syms, const uint64_t* h_offsets,
+                             const uint32_t* h_counts, int nstreams, uint32_t range,
+                             uint32_t prob_bits, uint8_t* d_out, const uint64_t* h_out_offsets,
+                             uint32_t* h_sizes, void* stream);
+
+/* ---- plane level ------------------------------------------------------------------------ */
+
+/* Replaces layer_encode(uint16_t*, size_t, int, int, int, size_t, uint8_t*, uint8_t*)
+ * (layer_encode.hpp:11-20) for cruncher_mode 0.  nuke may be NULL (no LZ). */
+int hoh_layer_encode(hoh_ctx* ctx, const uint16_t* data, size_t size, int width, int height,
+                     int depth, size_t cruncher_mode, const uint8_t* nuke, uint8_t* out,
+                     size_t cap, size_t* written);
+/* Replaces decode_layer (layer_decode.hpp:128-136), returning the full-depth plane (u16: the
+ * reference truncates 9-bit planes to u8).  backref may be NULL. */
+int hoh_layer_decode(hoh_ctx* ctx, const uint8_t* in, size_t in_size, size_t byte_pointer,
+                     int width, int height, int depth, const uint16_t* backref, uint16_t* out);
+/* Replaces channelpredict_fastpath (prediction.hpp:6-13; reached via channelpredict_section
+ * :59-68): MED residuals. */
+int hoh_predict_fastpath(hoh_ctx* ctx, const uint16_t* data, int width, int height, int depth,
+                         uint16_t* out);
+/* Replaces unpredict_all (unprediction.hpp:6-16) for the fast-path predictor (tile_map =
+ * {0x0010}) with MED on every row (SURVEY Q9 fixed).  res holds nres residuals; backref may be
+ * NULL. */
+int hoh_unpredict_fastpath(hoh_ctx* ctx, const uint16_t* res, size_t nres, const uint16_t* backref,
+                           int width, int height, int depth, uint16_t* out);
+/* Replaces subtract_green (channel.hpp:73-79) and provides its inverse. */
+int hoh_subtract_green(hoh_ctx* ctx, const uint8_t* rgb, size_t npix, uint16_t* G, uint16_t* R, uint16_t* B);
+int hoh_add_green(hoh_ctx* ctx, const uint16_t* G, const uint16_t* R, const uint16_t* B, size_t npix, uint8_t* rgb);
+
+/* ---- utilities ---------------------------------------------------------------------------- */
+
+/* Deterministic synthetic RGB (hoh_ans/synth.py formula) written to d_rgb. */
+int hoh_synth_rgb(hoh_ctx* ctx, uint8_t* d_rgb, int W, int H, uint64_t seed, int noise, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
