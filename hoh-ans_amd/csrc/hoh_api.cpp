@@ -356,6 +356,113 @@ int hoh_synth_rgb(hoh_ctx* c, uint8_t* d_rgb, int W, int H, uint64_t seed, int n
   return hipStreamSynchronize(s) == hipSuccess ? HOH_OK : HOH_E_HIP;
 }
 
+}  // extern "C"
+
+// ---------------------------------------------------------------- entropy streams (batched)
+
+// nstreams streams of d_syms (device), all with one range / prob_bits, written at
+// d_out + out_off[i] (device).  Host arrays: off (symbol offsets, multiples of 8), cnt, out_off.
+int encode_streams_impl(hoh_ctx* c, const uint16_t* d_syms, const uint64_t* off, const uint32_t* cnt, int nstreams,
+                        uint32_t range, uint32_t pb, uint8_t* d_out, const uint64_t* out_off, uint32_t* sizes,
+                        hipStream_t s) {
+  if (range == 0 || range > 4096 || pb == 0 || pb > 31) return HOH_E_RANGE;
+  if (nstreams <= 0) return HOH_E_ARG;
+  uint32_t nmax = 0;
+  for (int i = 0; i < nstreams; i++) { if (off[i] % 8) return HOH_E_ARG; nmax = cnt[i] > nmax ? cnt[i] : nmax; }
+  const size_t per_ck = nmax / HOH_SEG + 2;
+  const size_t slab = (size_t)nmax + 8;
+  const uint32_t hcap = (uint32_t)rup(64 + (2 * 8 * 16 + (size_t)range * (pb > 16 ? pb : 16)) / 8 + 16, 16);
+  int e;
+  if ((e = ensure(c->streams, (size_t)nstreams * sizeof(StreamInfo)))) return e;
+  if ((e = ensure(c->hdr, (size_t)nstreams * hcap))) return e;
+  if ((e = ensure(c->tab_gen, (size_t)nstreams * range * sizeof(EncGen)))) return e;
+  if ((e = ensure(c->slabs, (size_t)nstreams * slab * 4))) return e;
+  if ((e = ensure(c->ckpt, (size_t)nstreams * per_ck * sizeof(Checkpoint)))) return e;
+  if ((e = ensure(c->misc, 64))) return e;
+  std::vector<StreamInfo> st((size_t)nstreams);
+  for (int i = 0; i < nstreams; i++) {
+    memset(&st[i], 0, sizeof(StreamInfo));
+    st[i].sym_off = off[i];
+    st[i].slab_off = (uint64_t)i * slab;
+    st[i].slab_cap = (uint32_t)slab;
+    st[i].out_off = out_off[i];
+    st[i].n = cnt[i];
+    st[i].range = range;
+    st[i].pb = pb;
+    st[i].ckpt_off = (uint32_t)((size_t)i * per_ck);
+    st[i].mode = SM_EMPTY;
+  }
+  EncodeJob j;
+  memset(&j, 0, sizeof(j));
+  j.sym = (uint16_t*)d_syms;
+  j.streams = (StreamInfo*)c->streams.p;
+  j.hdr = (uint8_t*)c->hdr.p;
+  j.hdr_cap = hcap;
+  j.tab_gen = (EncGen*)c->tab_gen.p;
+  j.gen_stride = range;
+  j.slabs = (uint32_t*)c->slabs.p;
+  j.ckpt = (Checkpoint*)c->ckpt.p;
+  j.gerr = (uint32_t*)c->misc.p;
+  j.total = (uint64_t*)((uint8_t*)c->misc.p + 8);
+  j.out = d_out;
+  j.cap = ~0ull;
+  if (hipMemcpyAsync(c->streams.p, st.data(), st.size() * sizeof(StreamInfo), hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;
+  if (hipMemsetAsync(c->misc.p, 0, 64, s) != hipSuccess) return HOH_E_HIP;
+  launch_tables(j, nstreams, s);
+  launch_rans_gen(j, nstreams, s);
+  launch_finalize(j, nstreams, s);
+  launch_streambytes(j, nstreams, s);
+  if (hipGetLastError() != hipSuccess) return HOH_E_HIP;
+  if (hipMemcpyAsync(st.data(), c->streams.p, st.size() * sizeof(StreamInfo), hipMemcpyDeviceToHost, s) != hipSuccess) return HOH_E_HIP;
+  if (hipMemcpyAsync(c->pinned, c->misc.p, 8, hipMemcpyDeviceToHost, s) != hipSuccess) return HOH_E_HIP;
+  if (hipStreamSynchronize(s) != hipSuccess) return HOH_E_HIP;
+  if (c->pinned[0] & 2) return HOH_E_RANGE;
+  if (c->pinned[0]) return HOH_E_RANGE;
+  for (int i = 0; i < nstreams; i++) {
+    if (st[i].err) return HOH_E_RANGE;
+    sizes[i] = st[i].size;
+  }
+  return HOH_OK;
+}
+
+extern "C" {
+
+size_t hoh_entropy_bound(size_t n, size_t range, uint32_t pb) {
+  return 64 + (2 * 8 * 17 + range * (pb > 16 ? pb : 16) + 7) / 8 + 4 * (n + 2) + (hoh_bitlen(range) * n + 7) / 8;
+}
+
+int hoh_encode_entropy_batch(hoh_ctx* c, const uint16_t* d_syms, const uint64_t* h_off, const uint32_t* h_cnt,
+                             int nstreams, uint32_t range, uint32_t pb, uint8_t* d_out, const uint64_t* h_out_off,
+                             uint32_t* h_sizes, void* stream) {
+  if (!c || !d_syms || !h_off || !h_cnt || !d_out || !h_out_off || !h_sizes) return HOH_E_ARG;
+  (void)hipSetDevice(c->device);
+  return encode_streams_impl(c, d_syms, h_off, h_cnt, nstreams, range, pb, d_out, h_out_off, h_sizes, pick(c, stream));
+}
+
+int hoh_encode_entropy(hoh_ctx* c, const uint16_t* symbols, size_t n, size_t range, uint32_t pb, uint8_t* out,
+                       size_t cap, size_t* written) {
+  if (!c || (!symbols && n) || !out || !written) return HOH_E_ARG;
+  if (n >= (1u << 31)) return HOH_E_ARG;
+  (void)hipSetDevice(c->device);
+  hipStream_t s = c->own;
+  const size_t bound = hoh_entropy_bound(n, range, pb);
+  Buf ds, dout;
+  int r;
+  if ((r = ensure(ds, n * 2 + 16)) || (r = ensure(dout, bound))) { freebuf(ds); freebuf(dout); return r; }
+  if (n && hipMemcpyAsync(ds.p, symbols, n * 2, hipMemcpyHostToDevice, s) != hipSuccess) r = HOH_E_HIP;
+  uint64_t off = 0, oo = 0;
+  uint32_t cnt = (uint32_t)n, size = 0;
+  if (!r) r = encode_streams_impl(c, (const uint16_t*)ds.p, &off, &cnt, 1, (uint32_t)range, pb, (uint8_t*)dout.p, &oo, &size, s);
+  if (!r) {
+    *written = size;
+    if (size > cap) r = HOH_E_CAP;
+    else if (hipMemcpy(out, dout.p, size, hipMemcpyDeviceToHost) != hipSuccess) r = HOH_E_HIP;
+  }
+  freebuf(ds);
+  freebuf(dout);
+  return r;
+}
+
 // ---------------------------------------------------------------- decode side index
 
 int hoh_index_create(hoh_index** idx) {

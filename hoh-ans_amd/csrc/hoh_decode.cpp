@@ -1,0 +1,199 @@
+// C ABI: decoders and the plane-level entry points (include/hoh_ans.h).  Compute runs in
+// k_decode.hip / k_plane.hip; host code here only moves caller buffers and checks framing bytes.
+#include "hoh_dec.h"
+#include "../../include/hoh_ans.h"
+
+#include <string.h>
+#include <vector>
+
+int decode_image_impl(hoh_ctx* c, const uint8_t* d_in, size_t size, uint8_t* d_rgb, size_t cap, int* Wp, int* Hp,
+                      const hoh_index* idx, hipStream_t s);
+int decode_stream_impl(hoh_ctx* c, const uint8_t* d_in, size_t size, size_t* bp, uint16_t* d_out, size_t cap,
+                       size_t* n, hipStream_t s);
+int encode_streams_impl(hoh_ctx* c, const uint16_t* d_syms, const uint64_t* off, const uint32_t* cnt, int nstreams,
+                        uint32_t range, uint32_t pb, uint8_t* d_out, const uint64_t* out_off, uint32_t* sizes,
+                        hipStream_t s);
+void launch_predict(const uint16_t* d, int w, int h, int depth, uint16_t* out, hipStream_t s);
+void launch_unpredict_serial(const uint16_t* res, size_t nres, const uint16_t* br, int w, int h, int depth,
+                             uint16_t* o, uint32_t* err, hipStream_t s);
+void launch_green(const uint8_t* rgb, size_t n, uint16_t* G, uint16_t* R, uint16_t* B, hipStream_t s);
+void launch_addgreen(const uint16_t* G, const uint16_t* R, const uint16_t* B, size_t n, uint8_t* o, hipStream_t s);
+void launch_compact(const uint16_t* in, const uint8_t* nuke, size_t n, uint16_t* out, uint64_t* count, hipStream_t s);
+
+namespace {
+
+// scoped device allocation for the host-buffer entry points
+struct DevMem {
+  void* p = nullptr;
+  explicit DevMem(size_t n) { if (hipMalloc(&p, n ? n : 16) != hipSuccess) p = nullptr; }
+  ~DevMem() { if (p) (void)hipFree(p); }
+  template <class T> T* as() { return (T*)p; }
+};
+
+uint64_t rdv(const uint8_t* b, size_t size, size_t& p, bool& ok) {   // varint.hpp:6-27
+  if (p >= size) { ok = false; return 0; }
+  uint64_t b0 = b[p++];
+  if (!(b0 & 0x80)) return b0;
+  if (p >= size) { ok = false; return 0; }
+  uint64_t b1 = b[p++];
+  if (!(b1 & 0x80)) return ((b0 & 0x7f) << 7) + b1;
+  if (p >= size) { ok = false; return 0; }
+  uint64_t b2 = b[p++];
+  return ((b0 & 0x7f) << 14) + ((b1 & 0x7f) << 7) + b2;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hoh_decode_image_ix(hoh_ctx* c, const uint8_t* d_hoh, size_t size, uint8_t* d_rgb, size_t cap, int* W, int* H,
+                        const hoh_index* idx, void* stream) {
+  if (!c || !d_hoh || !d_rgb || !W || !H) return HOH_E_ARG;
+  (void)hipSetDevice(ctx_device(c));
+  return decode_image_impl(c, d_hoh, size, d_rgb, cap, W, H, idx, ctx_stream(c, stream));
+}
+
+int hoh_decode_image(hoh_ctx* c, const uint8_t* d_hoh, size_t size, uint8_t* d_rgb, size_t cap, int* W, int* H,
+                     void* stream) {
+  return hoh_decode_image_ix(c, d_hoh, size, d_rgb, cap, W, H, nullptr, stream);
+}
+
+int hoh_entropy_count(const uint8_t* in, size_t in_size, size_t bp, size_t* n) {
+  if (!in || !n) return HOH_E_ARG;
+  bool ok = true;
+  (void)rdv(in, in_size, bp, ok);
+  *n = (size_t)rdv(in, in_size, bp, ok);
+  return ok ? HOH_OK : HOH_E_CORRUPT;
+}
+
+int hoh_decode_entropy(hoh_ctx* c, const uint8_t* in, size_t in_size, size_t* bp, uint16_t* out, size_t cap,
+                       size_t* n) {
+  if (!c || !in || !bp || !n || *bp >= in_size) return HOH_E_ARG;
+  (void)hipSetDevice(ctx_device(c));
+  hipStream_t s = ctx_stream(c, nullptr);
+  size_t cnt = 0;
+  int r = hoh_entropy_count(in, in_size, *bp, &cnt);
+  if (r) return r;
+  if (cnt > cap) return HOH_E_CAP;
+  DevMem din(in_size + 8), dout(cnt * 2 + 16);
+  if (!din.p || !dout.p) return HOH_E_HIP;
+  if (hipMemcpy(din.p, in, in_size, hipMemcpyHostToDevice) != hipSuccess) return HOH_E_HIP;
+  if (hipMemset((uint8_t*)din.p + in_size, 0, 8) != hipSuccess) return HOH_E_HIP;
+  size_t p = *bp, m = 0;
+  r = decode_stream_impl(c, din.as<uint8_t>(), in_size, &p, dout.as<uint16_t>(), cnt, &m, s);
+  if (r) return r;
+  if (m && hipMemcpy(out, dout.p, m * 2, hipMemcpyDeviceToHost) != hipSuccess) return HOH_E_HIP;
+  *n = m;
+  *bp = p;
+  return HOH_OK;
+}
+
+int hoh_predict_fastpath(hoh_ctx* c, const uint16_t* data, int w, int h, int depth, uint16_t* out) {
+  if (!c || !data || !out || w <= 0 || h <= 0 || depth < 1 || depth > 15) return HOH_E_ARG;
+  (void)hipSetDevice(ctx_device(c));
+  hipStream_t s = ctx_stream(c, nullptr);
+  const size_t n = (size_t)w * h;
+  DevMem a(n * 2), b(n * 2);
+  if (!a.p || !b.p) return HOH_E_HIP;
+  if (hipMemcpyAsync(a.p, data, n * 2, hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;
+  launch_predict(a.as<uint16_t>(), w, h, depth, b.as<uint16_t>(), s);
+  if (hipMemcpyAsync(out, b.p, n * 2, hipMemcpyDeviceToHost, s) != hipSuccess) return HOH_E_HIP;
+  return hipStreamSynchronize(s) == hipSuccess ? HOH_OK : HOH_E_HIP;
+}
+
+int hoh_unpredict_fastpath(hoh_ctx* c, const uint16_t* res, size_t nres, const uint16_t* backref, int w, int h,
+                           int depth, uint16_t* out) {
+  if (!c || (!res && nres) || !out || w <= 0 || h <= 0 || depth < 1 || depth > 15) return HOH_E_ARG;
+  (void)hipSetDevice(ctx_device(c));
+  hipStream_t s = ctx_stream(c, nullptr);
+  const size_t n = (size_t)w * h;
+  DevMem dr(nres * 2), db(backref ? n * 2 : 16), dout(n * 2), de(16);
+  if (!dr.p || !db.p || !dout.p || !de.p) return HOH_E_HIP;
+  if (nres && hipMemcpyAsync(dr.p, res, nres * 2, hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;
+  if (backref && hipMemcpyAsync(db.p, backref, n * 2, hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;
+  launch_unpredict_serial(dr.as<uint16_t>(), nres, backref ? db.as<uint16_t>() : nullptr, w, h, depth,
+                          dout.as<uint16_t>(), de.as<uint32_t>(), s);
+  uint32_t err = 1;
+  if (hipMemcpyAsync(&err, de.p, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return HOH_E_HIP;
+  if (hipMemcpyAsync(out, dout.p, n * 2, hipMemcpyDeviceToHost, s) != hipSuccess) return HOH_E_HIP;
+  if (hipStreamSynchronize(s) != hipSuccess) return HOH_E_HIP;
+  return err ? HOH_E_CORRUPT : HOH_OK;
+}
+
+int hoh_subtract_green(hoh_ctx* c, const uint8_t* rgb, size_t npix, uint16_t* G, uint16_t* R, uint16_t* B) {
+  if (!c || !rgb || !G || !R || !B) return HOH_E_ARG;
+  (void)hipSetDevice(ctx_device(c));
+  hipStream_t s = ctx_stream(c, nullptr);
+  DevMem a(npix * 3), g(npix * 2), r(npix * 2), b(npix * 2);
+  if (!a.p || !g.p || !r.p || !b.p) return HOH_E_HIP;
+  if (hipMemcpyAsync(a.p, rgb, npix * 3, hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;
+  launch_green(a.as<uint8_t>(), npix, g.as<uint16_t>(), r.as<uint16_t>(), b.as<uint16_t>(), s);
+  if (hipMemcpyAsync(G, g.p, npix * 2, hipMemcpyDeviceToHost, s) != hipSuccess) return HOH_E_HIP;
+  if (hipMemcpyAsync(R, r.p, npix * 2, hipMemcpyDeviceToHost, s) != hipSuccess) return HOH_E_HIP;
+  if (hipMemcpyAsync(B, b.p, npix * 2, hipMemcpyDeviceToHost, s) != hipSuccess) return HOH_E_HIP;
+  return hipStreamSynchronize(s) == hipSuccess ? HOH_OK : HOH_E_HIP;
+}
+
+int hoh_add_green(hoh_ctx* c, const uint16_t* G, const uint16_t* R, const uint16_t* B, size_t npix, uint8_t* rgb) {
+  if (!c || !rgb || !G || !R || !B) return HOH_E_ARG;
+  (void)hipSetDevice(ctx_device(c));
+  hipStream_t s = ctx_stream(c, nullptr);
+  DevMem a(npix * 3), g(npix * 2), r(npix * 2), b(npix * 2);
+  if (!a.p || !g.p || !r.p || !b.p) return HOH_E_HIP;
+  if (hipMemcpyAsync(g.p, G, npix * 2, hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;
+  if (hipMemcpyAsync(r.p, R, npix * 2, hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;
+  if (hipMemcpyAsync(b.p, B, npix * 2, hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;
+  launch_addgreen(g.as<uint16_t>(), r.as<uint16_t>(), b.as<uint16_t>(), npix, a.as<uint8_t>(), s);
+  if (hipMemcpyAsync(rgb, a.p, npix * 3, hipMemcpyDeviceToHost, s) != hipSuccess) return HOH_E_HIP;
+  return hipStreamSynchronize(s) == hipSuccess ? HOH_OK : HOH_E_HIP;
+}
+
+// layer_encode.hpp:11-412 at cruncher_mode 0: 0x10, 00 00 00 10, entropy(cleaned MED residuals)
+int hoh_layer_encode(hoh_ctx* c, const uint16_t* data, size_t size, int w, int h, int depth, size_t cruncher,
+                     const uint8_t* nuke, uint8_t* out, size_t cap, size_t* written) {
+  if (!c || !data || !out || !written || w <= 0 || h <= 0 || (size_t)w * h != size || depth < 1 || depth > 12)
+    return HOH_E_ARG;
+  if (cruncher != 0) return HOH_E_UNSUPPORTED;                          // -s>=1 predictor search
+  (void)hipSetDevice(ctx_device(c));
+  hipStream_t s = ctx_stream(c, nullptr);
+  const size_t bound = hoh_entropy_bound(size, (size_t)1 << depth, 15);
+  DevMem a(size * 2), res(size * 2 + 16), cl(size * 2 + 16), nk(nuke ? size : 16), cnt(16), eout(bound);
+  if (!a.p || !res.p || !cl.p || !nk.p || !cnt.p || !eout.p) return HOH_E_HIP;
+  if (hipMemcpyAsync(a.p, data, size * 2, hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;
+  if (nuke && hipMemcpyAsync(nk.p, nuke, size, hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;
+  launch_predict(a.as<uint16_t>(), w, h, depth, res.as<uint16_t>(), s);
+  launch_compact(res.as<uint16_t>(), nuke ? nk.as<uint8_t>() : nullptr, size, cl.as<uint16_t>(), cnt.as<uint64_t>(), s);
+  uint64_t nc = 0;
+  if (hipMemcpyAsync(&nc, cnt.p, 8, hipMemcpyDeviceToHost, s) != hipSuccess) return HOH_E_HIP;
+  if (hipStreamSynchronize(s) != hipSuccess) return HOH_E_HIP;
+  uint64_t off = 0, oo = 0;
+  uint32_t n32 = (uint32_t)nc, sz = 0;
+  int r = encode_streams_impl(c, cl.as<uint16_t>(), &off, &n32, 1, 1u << depth, 15, eout.as<uint8_t>(), &oo, &sz, s);
+  if (r) return r;
+  const size_t possible = ((size_t)depth * size + ((size_t)depth * size) % 8 + 1024) / 8;   // :22
+  if (sz >= possible) return HOH_E_UNREPRODUCIBLE;                     // :115-120 keeps garbage
+  *written = 5 + (size_t)sz;
+  if (*written > cap) return HOH_E_CAP;
+  const uint8_t hdr[5] = {0x10, 0, 0, 0x00, 0x10};                    // :57, :320-325
+  memcpy(out, hdr, 5);
+  if (hipMemcpy(out + 5, eout.p, sz, hipMemcpyDeviceToHost) != hipSuccess) return HOH_E_HIP;
+  return HOH_OK;
+}
+
+// layer_decode.hpp:128-278 for -s0 layers; returns the full-depth plane (no u8 truncation, Q10)
+int hoh_layer_decode(hoh_ctx* c, const uint8_t* in, size_t in_size, size_t bp, int w, int h, int depth,
+                     const uint16_t* backref, uint16_t* out) {
+  if (!c || !in || !out || w <= 0 || h <= 0 || bp + 5 > in_size) return HOH_E_ARG;
+  if (in[bp] != 0x10) return HOH_E_UNSUPPORTED;                        // compaction / no prediction
+  if (in[bp + 1] != 0 || in[bp + 2] != 0) return HOH_E_UNSUPPORTED;    // predictor tiles (-s>=1)
+  if (in[bp + 3] != 0x00 || in[bp + 4] != 0x10) return HOH_E_UNSUPPORTED;
+  size_t cnt = 0;
+  int r = hoh_entropy_count(in, in_size, bp + 5, &cnt);
+  if (r) return r;
+  std::vector<uint16_t> res(cnt + 1);
+  size_t p = bp + 5, n = 0;
+  if ((r = hoh_decode_entropy(c, in, in_size, &p, res.data(), cnt, &n))) return r;
+  return hoh_unpredict_fastpath(c, res.data(), n, backref, w, h, depth, out);
+}
+
+}  // extern "C"

@@ -144,3 +144,4 @@ void launch_rans_gen(const EncodeJob& j, int nstreams, hipStream_t s);
 void launch_finalize(const EncodeJob& j, int nstreams, hipStream_t s);
 void launch_layout(const EncodeJob& j, hipStream_t s);
 void launch_assemble(const EncodeJob& j, int nstreams, hipStream_t s);
+void launch_streambytes(const EncodeJob& j, int nstreams, hipStream_t s);

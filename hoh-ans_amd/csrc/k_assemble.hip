@@ -194,3 +194,7 @@ void launch_assemble(const EncodeJob& j, int nstreams, hipStream_t s) {
   hipLaunchKernelGGL(k_tilebytes, dim3((j.ntiles + 63) / 64), dim3(64), 0, s, j);
   hipLaunchKernelGGL(k_streambytes, dim3(nstreams), dim3(256), 0, s, j);
 }
+
+void launch_streambytes(const EncodeJob& j, int nstreams, hipStream_t s) {
+  hipLaunchKernelGGL(k_streambytes, dim3(nstreams), dim3(256), 0, s, j);
+}
