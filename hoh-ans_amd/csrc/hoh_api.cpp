@@ -11,7 +11,7 @@
 #include <vector>
 #include <string>
 
-void launch_synth(uint8_t* rgb, int W, int H, uint64_t seed, int noise, hipStream_t s);
+void launch_synth(uint8_t* rgb, int W, int H, int y0, uint64_t seed, int noise, hipStream_t s);
 
 namespace {
 
@@ -49,8 +49,12 @@ struct hoh_ctx {
   DecWork dec;                  // decoder workspaces (k_decode.hip)
   uint64_t* pinned = nullptr;   // small host staging (status words, sizes)
   int profiling = 0;
-  std::vector<std::string> knames;
-  std::vector<hipEvent_t> kev;
+  std::vector<std::string> knames;      // names of the marks recorded by the current call
+  std::vector<hipEvent_t> kev;          // event pool, kev[0..nmark) recorded by the current call
+  size_t nmark = 0;
+  std::vector<std::string> snames;      // accumulated per-kernel totals since the last reset
+  std::vector<double> sms;
+  std::vector<uint64_t> scount;
   std::vector<float> kms;
 };
 
@@ -58,24 +62,43 @@ static hipStream_t pick(hoh_ctx* c, void* s) { return s ? (hipStream_t)s : c->ow
 
 // ---------------------------------------------------------------- profiling helpers
 
+// Events are recorded between consecutive launches on the call's stream (no host sync); at the
+// start of the next call, or when stats are read, the previous call's intervals are folded into
+// per-name totals.  Every API call ends with a stream sync, so the fold never waits.
+static void prof_fold(hoh_ctx* c) {
+  if (c->nmark >= 2) {
+    (void)hipEventSynchronize(c->kev[c->nmark - 1]);
+    for (size_t i = 1; i < c->nmark; i++) {
+      float v = 0;
+      (void)hipEventElapsedTime(&v, c->kev[i - 1], c->kev[i]);
+      size_t k = 0;
+      while (k < c->snames.size() && c->snames[k] != c->knames[i]) k++;
+      if (k == c->snames.size()) { c->snames.push_back(c->knames[i]); c->sms.push_back(0); c->scount.push_back(0); }
+      c->sms[k] += v;
+      c->scount[k] += 1;
+    }
+  }
+  c->nmark = 0;
+  c->knames.clear();
+}
+
+static void prof_mark(hoh_ctx* c, hipStream_t s, const char* name, bool reset) {
+  if (!c->profiling) return;
+  if (reset) prof_fold(c);
+  if (c->nmark == c->kev.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return;
+    c->kev.push_back(e);
+  }
+  (void)hipEventRecord(c->kev[c->nmark++], s);
+  c->knames.push_back(name);
+}
+
 struct Prof {
   hoh_ctx* c;
   hipStream_t s;
-  explicit Prof(hoh_ctx* c_, hipStream_t s_) : c(c_), s(s_) {
-    if (!c->profiling) return;
-    for (auto e : c->kev) (void)hipEventDestroy(e);
-    c->kev.clear();
-    c->knames.clear();
-    mark("start");
-  }
-  void mark(const char* name) {
-    if (!c->profiling) return;
-    hipEvent_t e;
-    (void)hipEventCreate(&e);
-    (void)hipEventRecord(e, s);
-    c->kev.push_back(e);
-    c->knames.push_back(name);
-  }
+  explicit Prof(hoh_ctx* c_, hipStream_t s_) : c(c_), s(s_) { prof_mark(c, s, "start", true); }
+  void mark(const char* name) { prof_mark(c, s, name, false); }
 };
 
 extern "C" {
@@ -129,16 +152,36 @@ void hoh_ctx_destroy(hoh_ctx* c) {
 void hoh_set_profiling(hoh_ctx* c, int on) { if (c) c->profiling = on; }
 
 int hoh_get_kernel_ms(hoh_ctx* c, const char** names, float* ms, int max) {
-  if (!c || c->kev.size() < 2) return 0;
+  if (!c || c->nmark < 2) return 0;
   int k = 0;
-  (void)hipEventSynchronize(c->kev.back());
-  for (size_t i = 1; i < c->kev.size() && k < max; i++, k++) {
+  (void)hipEventSynchronize(c->kev[c->nmark - 1]);
+  for (size_t i = 1; i < c->nmark && k < max; i++, k++) {
     float v = 0;
     (void)hipEventElapsedTime(&v, c->kev[i - 1], c->kev[i]);
     if (names) names[k] = c->knames[i].c_str();
     if (ms) ms[k] = v;
   }
   return k;
+}
+
+int hoh_get_kernel_stats(hoh_ctx* c, const char** names, double* total_ms, uint64_t* count, int max) {
+  if (!c) return 0;
+  prof_fold(c);
+  int k = 0;
+  for (; k < (int)c->snames.size() && k < max; k++) {
+    if (names) names[k] = c->snames[k].c_str();
+    if (total_ms) total_ms[k] = c->sms[k];
+    if (count) count[k] = c->scount[k];
+  }
+  return k;
+}
+
+void hoh_reset_kernel_stats(hoh_ctx* c) {
+  if (!c) return;
+  prof_fold(c);
+  c->snames.clear();
+  c->sms.clear();
+  c->scount.clear();
 }
 
 int hoh_tiling(int W, int H, int* xt, int* yt, int* tw, int* th) {
@@ -295,12 +338,17 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
 
 int hoh_encode_tiles(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int t0, int ntiles, uint8_t* d_out,
                      size_t cap, uint32_t* d_tile_sizes, size_t* out_size, void* stream) {
+  return hoh_encode_tiles_ix(c, d_rgb, W, H, t0, ntiles, d_out, cap, d_tile_sizes, out_size, nullptr, stream);
+}
+
+int hoh_encode_tiles_ix(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int t0, int ntiles, uint8_t* d_out,
+                        size_t cap, uint32_t* d_tile_sizes, size_t* out_size, hoh_index* idx, void* stream) {
   if (!c || !d_rgb || !d_out || !out_size || W <= 0 || H <= 0) return HOH_E_ARG;
   (void)hipSetDevice(c->device);
   int xt, yt, tw, th;
   if (!hoh_tiling(W, H, &xt, &yt, &tw, &th)) return HOH_E_ARG;
   uint64_t total = 0;
-  int r = encode_tiles_impl(c, d_rgb, W, H, t0, ntiles, d_out, cap, 0, 0, d_tile_sizes, &total, nullptr,
+  int r = encode_tiles_impl(c, d_rgb, W, H, t0, ntiles, d_out, cap, 0, 0, d_tile_sizes, &total, idx,
                             pick(c, stream));
   *out_size = (size_t)total;
   return r;
@@ -348,10 +396,14 @@ int hoh_encode_image(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int speed, 
 }
 
 int hoh_synth_rgb(hoh_ctx* c, uint8_t* d_rgb, int W, int H, uint64_t seed, int noise, void* stream) {
-  if (!c || !d_rgb || W <= 0 || H <= 0 || noise < 0) return HOH_E_ARG;
+  return hoh_synth_rgb_rows(c, d_rgb, W, 0, H, seed, noise, stream);
+}
+
+int hoh_synth_rgb_rows(hoh_ctx* c, uint8_t* d_rgb, int W, int y0, int rows, uint64_t seed, int noise, void* stream) {
+  if (!c || !d_rgb || W <= 0 || rows <= 0 || y0 < 0 || noise < 0) return HOH_E_ARG;
   (void)hipSetDevice(c->device);
   hipStream_t s = pick(c, stream);
-  launch_synth(d_rgb, W, H, seed, noise, s);
+  launch_synth(d_rgb, W, rows, y0, seed, noise, s);
   if (hipGetLastError() != hipSuccess) return HOH_E_HIP;
   return hipStreamSynchronize(s) == hipSuccess ? HOH_OK : HOH_E_HIP;
 }
@@ -504,16 +556,4 @@ DecWork& ctx_dec(hoh_ctx* c) { return c->dec; }
 hipStream_t ctx_stream(hoh_ctx* c, void* s) { return pick(c, s); }
 uint64_t* ctx_pinned(hoh_ctx* c) { return c->pinned; }
 int ctx_device(hoh_ctx* c) { return c->device; }
-void ctx_mark(hoh_ctx* c, hipStream_t s, const char* name, bool reset) {
-  if (!c->profiling) return;
-  if (reset) {
-    for (auto e : c->kev) (void)hipEventDestroy(e);
-    c->kev.clear();
-    c->knames.clear();
-  }
-  hipEvent_t e;
-  (void)hipEventCreate(&e);
-  (void)hipEventRecord(e, s);
-  c->kev.push_back(e);
-  c->knames.push_back(name);
-}
+void ctx_mark(hoh_ctx* c, hipStream_t s, const char* name, bool reset) { prof_mark(c, s, name, reset); }

@@ -36,6 +36,8 @@ struct DecJob {
   const IndexStream* ix;        // optional side index
   const Checkpoint* ck;
   int nix;
+  int t0;                       // global index of the first tile (shard decode)
+  const uint32_t* tsizes;       // shard decode: tile byte sizes instead of the file's table
 };
 
 __device__ __forceinline__ uint64_t rd_varint(const uint8_t* b, uint64_t& p) {
@@ -63,13 +65,15 @@ __global__ void k_dtable(DecJob j) {
   uint64_t off = 0;
   for (int i = 0; i < j.ntiles; i++) {
     DecTile t;
-    const int xo = (i % j.xt) * j.tw, yo = (i / j.xt) * j.th;
+    const int g = j.t0 + i;
+    const int xo = (g % j.xt) * j.tw, yo = (g / j.xt) * j.th;
     t.x0 = xo; t.y0 = yo;
     t.w = min(j.tw, j.W - xo); t.h = min(j.th, j.H - yo);
     t.off = off;               // relative to the first tile, fixed below
     t.mode = 0; t.nmatch = 0; t.err = 0; t.pad = 0;
     j.tiles[i] = t;
     if (i + 1 < j.ntiles) {
+      if (j.tsizes) { off += j.tsizes[i]; continue; }
       if (p + 3 > j.size) { atomicOr(j.gerr, 1u); return; }
       off += rd_varint(j.in, p);
     }
@@ -497,6 +501,8 @@ static int dbuf(DecWork& w, int k, size_t bytes, void** p) {
   return 0;
 }
 
+static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s);
+
 int decode_image_impl(hoh_ctx* c, const uint8_t* d_in, size_t size, uint8_t* d_rgb, size_t cap, int* Wp, int* Hp,
                       const hoh_index* idx, hipStream_t s) {
   // header (host copy of the first bytes: W, H decide every launch size)
@@ -532,6 +538,38 @@ int decode_image_impl(hoh_ctx* c, const uint8_t* d_in, size_t size, uint8_t* d_r
   j.in = d_in;
   j.size = size;
   j.rgb = d_rgb;
+  return decode_run(c, j, idx, s);
+}
+
+// shard decode: tiles [t0, t0+ntiles) of a W x H image, their bytes concatenated in d_blob
+int decode_tiles_impl(hoh_ctx* c, const uint8_t* d_blob, size_t size, int W, int H, int t0, int ntiles,
+                      const uint32_t* h_sizes, uint8_t* d_rgb, const hoh_index* idx, hipStream_t s) {
+  DecJob j;
+  memset(&j, 0, sizeof(j));
+  j.W = W; j.H = H;
+  if (!((W >= 512 || H >= 512) && W >= 256 && H >= 256)) return 6;
+  j.xt = W / 256; j.yt = H / 256;
+  j.tw = (W + j.xt - 1) / j.xt; j.th = (H + j.yt - 1) / j.yt;
+  if (t0 < 0 || ntiles <= 0 || t0 + ntiles > j.xt * j.yt) return 1;
+  j.t0 = t0;
+  j.ntiles = ntiles;
+  j.prefix = 0;
+  j.in = d_blob;
+  j.size = size;
+  j.rgb = d_rgb;
+  uint64_t tot = 0;
+  for (int i = 0; i < ntiles; i++) tot += h_sizes[i];
+  if (tot > size) return 7;
+  DecWork& w = ctx_dec(c);
+  void* q;
+  int e;
+  if ((e = dbuf(w, 12, (size_t)ntiles * 4, &q))) return e;
+  if (hipMemcpyAsync(q, h_sizes, (size_t)ntiles * 4, hipMemcpyHostToDevice, s) != hipSuccess) return 3;
+  j.tsizes = (const uint32_t*)q;
+  return decode_run(c, j, idx, s);
+}
+
+static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s) {
   j.npix_cap = (uint32_t)(((size_t)j.tw * j.th + 63) / 64 * 64);
   j.lz_cap = (uint32_t)((j.npix_cap / 4 + j.npix_cap / 255 + 16 + 7) / 8 * 8);
   const int S = j.ntiles * SK_PER_TILE;

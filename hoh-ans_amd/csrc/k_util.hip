@@ -8,16 +8,17 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
-__global__ void k_synth(uint8_t* rgb, int W, int H, uint64_t salt, int noise) {
+__global__ void k_synth(uint8_t* rgb, int W, int H, int y0, uint64_t salt, int noise) {
   const size_t total = (size_t)W * H * 3;
   const int A[3] = {37, 53, 29}, B[3] = {23, 31, 47}, O[3] = {10, 80, 160};
   const uint64_t k = (uint64_t)noise + 1;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
     const int c = (int)(i % 3);
     const size_t px = i / 3;
-    const long long x = (long long)(px % W), y = (long long)(px / W);
+    const long long x = (long long)(px % W), y = (long long)(px / W) + y0;
+    const uint64_t gi = ((uint64_t)y * W + (uint64_t)x) * 3 + c;
     const long long base = (((A[c] * x + B[c] * y) >> 8) + O[c]) & 255;
-    const uint64_t h = splitmix64(salt + (uint64_t)i);
+    const uint64_t h = splitmix64(salt + gi);
     const long long nz = (long long)(h % k) + (long long)((h >> 16) % k) - noise;
     long long v = base + nz;
     v = v < 0 ? 0 : v > 255 ? 255 : v;
@@ -25,7 +26,8 @@ __global__ void k_synth(uint8_t* rgb, int W, int H, uint64_t salt, int noise) {
   }
 }
 
-void launch_synth(uint8_t* rgb, int W, int H, uint64_t seed, int noise, hipStream_t s) {
+// rows [y0, y0 + H) of the global synthetic image of width W
+void launch_synth(uint8_t* rgb, int W, int H, int y0, uint64_t seed, int noise, hipStream_t s) {
   const uint64_t salt = seed * 0x100000001B3ull;
-  hipLaunchKernelGGL(k_synth, dim3(4096), dim3(256), 0, s, rgb, W, H, salt, noise);
+  hipLaunchKernelGGL(k_synth, dim3(4096), dim3(256), 0, s, rgb, W, H, y0, salt, noise);
 }

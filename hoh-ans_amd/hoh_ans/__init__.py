@@ -56,6 +56,10 @@ def lib():
         L.hoh_version.restype = C.c_char_p
         L.hoh_set_profiling.argtypes = [vp, C.c_int]
         L.hoh_get_kernel_ms.argtypes = [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.c_int]
+        L.hoh_get_kernel_stats.argtypes = [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_double),
+                                           C.POINTER(C.c_uint64), C.c_int]
+        L.hoh_reset_kernel_stats.argtypes = [vp]
+        L.hoh_reset_kernel_stats.restype = None
         L.hoh_encode_bound.restype = sz
         L.hoh_encode_bound.argtypes = [C.c_int, C.c_int]
         L.hoh_encode_image.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, vp, sz, szp, szp, vp]
@@ -70,6 +74,9 @@ def lib():
         L.hoh_tiling.argtypes = [C.c_int, C.c_int, ip, ip, ip, ip]
         L.hoh_peek_header.argtypes = [vp, sz, ip, ip, ip, ip]
         L.hoh_synth_rgb.argtypes = [vp, vp, C.c_int, C.c_int, C.c_uint64, C.c_int, vp]
+        L.hoh_synth_rgb_rows.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int, vp]
+        L.hoh_encode_tiles_ix.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, sz, vp, szp, vp, vp]
+        L.hoh_decode_tiles.argtypes = [vp, vp, sz, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp]
         for name, args in (
             ("hoh_decode_image", [vp, vp, sz, vp, sz, ip, ip, vp]),
             ("hoh_decode_image_ix", [vp, vp, sz, vp, sz, ip, ip, vp, vp]),
@@ -128,6 +135,17 @@ class Context:
         ms = (C.c_float * 64)()
         n = lib().hoh_get_kernel_ms(self.h, names, ms, 64)
         return [(names[i].decode(), ms[i]) for i in range(n)]
+
+    def kernel_stats(self):
+        """{stage: (total_ms, launches)} accumulated over profiled calls since reset_stats()."""
+        names = (C.c_char_p * 64)()
+        tot = (C.c_double * 64)()
+        cnt = (C.c_uint64 * 64)()
+        n = lib().hoh_get_kernel_stats(self.h, names, tot, cnt, 64)
+        return {names[i].decode(): (tot[i], cnt[i]) for i in range(n)}
+
+    def reset_stats(self):
+        lib().hoh_reset_kernel_stats(self.h)
 
 
 _CTX = None
@@ -200,14 +218,30 @@ def decode_image(hoh_dev, size, out_dev=None, ctx=None, index=None):
     return out_dev, w.value, h.value
 
 
-def encode_tiles(rgb_dev, W, H, t0, ntiles, out_dev, sizes_dev, ctx=None):
+def encode_tiles(rgb_dev, W, H, t0, ntiles, out_dev, sizes_dev, ctx=None, index=None, row0=0):
+    """Encode tiles [t0, t0+ntiles) of a W x H image into a blob (concatenated tile byte strings).
+    rgb_dev holds image rows from row0 on (a shard); only the named tiles' pixels are read.
+    Returns the blob size; sizes_dev (uint32, device) receives each tile's size."""
     import torch
     ctx = ctx or default_ctx()
     n = C.c_size_t(0)
-    r = lib().hoh_encode_tiles(ctx.h, vp(rgb_dev.data_ptr()), W, H, t0, ntiles, vp(out_dev.data_ptr()),
-                               out_dev.numel(), vp(sizes_dev.data_ptr()), C.byref(n), _stream_ptr(torch))
+    base = rgb_dev.data_ptr() - row0 * W * 3
+    r = lib().hoh_encode_tiles_ix(ctx.h, vp(base), W, H, t0, ntiles, vp(out_dev.data_ptr()),
+                                  out_dev.numel(), vp(sizes_dev.data_ptr()), C.byref(n),
+                                  index.h if index is not None else None, _stream_ptr(torch))
     check(r, "hoh_encode_tiles")
     return n.value
+
+
+def decode_tiles(blob_dev, size, W, H, t0, tile_sizes, out_dev, ctx=None, index=None, row0=0):
+    """Inverse of encode_tiles: decodes the blob's tiles into out_dev (image rows from row0 on)."""
+    import torch
+    ctx = ctx or default_ctx()
+    ts = np.ascontiguousarray(tile_sizes, dtype=np.uint32)
+    base = out_dev.data_ptr() - row0 * W * 3
+    r = lib().hoh_decode_tiles(ctx.h, vp(blob_dev.data_ptr()), size, W, H, t0, ts.size, _p(ts), vp(base),
+                               index.h if index is not None else None, _stream_ptr(torch))
+    check(r, "hoh_decode_tiles")
 
 
 def file_prefix(W, H, tile_sizes):
@@ -226,12 +260,14 @@ def peek_header(data):
     return W.value, H.value, xt.value, yt.value
 
 
-def synth_rgb_dev(W, H, seed=1, noise=4, ctx=None, device="cuda"):
-    """Synthetic image generated in HBM (same bytes as hoh_ans.synth.synth_rgb)."""
+def synth_rgb_dev(W, H, seed=1, noise=4, ctx=None, device="cuda", row0=0):
+    """Synthetic image generated in HBM (same bytes as hoh_ans.synth.synth_rgb); with row0, rows
+    [row0, row0+H) of the width-W global image (a shard)."""
     import torch
     ctx = ctx or default_ctx()
     t = torch.empty(W * H * 3, dtype=torch.uint8, device=device)
-    check(lib().hoh_synth_rgb(ctx.h, vp(t.data_ptr()), W, H, seed, noise, _stream_ptr(torch)), "hoh_synth_rgb")
+    check(lib().hoh_synth_rgb_rows(ctx.h, vp(t.data_ptr()), W, row0, H, seed, noise, _stream_ptr(torch)),
+          "hoh_synth_rgb_rows")
     return t
 
 

@@ -1,6 +1,6 @@
 """Deterministic synthetic 8-bit RGB input.
 
-Integer-only, so the numpy path here, the HIP generator in libhohgpu (hoh_gpu_synth_rgb) and
+Integer-only, so the numpy path here, the HIP generator in libhohgpu (hoh_synth_rgb) and
 the committed fixtures all agree byte for byte:
 
     h     = splitmix64(seed * 0x100000001B3 + (y*W + x)*3 + c)

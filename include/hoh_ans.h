@@ -48,6 +48,10 @@ const char* hoh_version(void);
 /* per-kernel device time of the last call, for measurement (ms); enable with hoh_set_profiling */
 void hoh_set_profiling(hoh_ctx* ctx, int on);
 int hoh_get_kernel_ms(hoh_ctx* ctx, const char** names, float* ms, int max);
+/* Per-kernel totals accumulated over every profiled call since the last reset (names are the
+ * kernel stages; total_ms / count give the average launch duration on the call's stream). */
+int hoh_get_kernel_stats(hoh_ctx* ctx, const char** names, double* total_ms, uint64_t* count, int max);
+void hoh_reset_kernel_stats(hoh_ctx* ctx);
 
 /* ---- image level: `choh in out W H -s0` / `dhoh in out` -------------------------------- */
 
@@ -88,10 +92,20 @@ int hoh_peek_header(const uint8_t* hoh, size_t size, int* W, int* H, int* x_tile
 
 /* Encodes tiles [t0, t0+ntiles) (row-major tile index, choh.cpp:464-500) of the W x H image into
  * a blob of concatenated tile byte strings at d_out; d_tile_sizes (device, ntiles u32) receives
- * each tile's size.  A rank's blob plus everyone's sizes are what the gather exchanges. */
+ * each tile's size.  A rank's blob plus everyone's sizes are what the gather exchanges.
+ * d_rgb is the base of the whole image: a rank holding only rows [y0, y1) passes
+ * (its buffer - y0*W*3); only the pixels of the named tiles are read. */
 int hoh_encode_tiles(hoh_ctx* ctx, const uint8_t* d_rgb, int W, int H, int t0, int ntiles,
                      uint8_t* d_out, size_t cap, uint32_t* d_tile_sizes, size_t* out_size,
                      void* stream);
+int hoh_encode_tiles_ix(hoh_ctx* ctx, const uint8_t* d_rgb, int W, int H, int t0, int ntiles,
+                        uint8_t* d_out, size_t cap, uint32_t* d_tile_sizes, size_t* out_size,
+                        hoh_index* idx, void* stream);
+/* Decodes tiles [t0, t0+ntiles) from d_blob (their byte strings concatenated, sizes in
+ * h_tile_sizes) into the W x H image at d_rgb (only those tiles' pixels are written; d_rgb is
+ * the base of the whole image).  idx may be the index hoh_encode_tiles_ix recorded. */
+int hoh_decode_tiles(hoh_ctx* ctx, const uint8_t* d_blob, size_t size, int W, int H, int t0, int ntiles,
+                     const uint32_t* h_tile_sizes, uint8_t* d_rgb, const hoh_index* idx, void* stream);
 /* Host: the .hoh prefix for a tiled image given every tile's size (choh.cpp:437-498):
  * magic, format, depth, varint W-1, H-1, x_tiles-1, y_tiles-1, n-1 varint sizes.  Returns the
  * prefix length, or 0 if cap is too small. */
@@ -149,8 +163,11 @@ int hoh_add_green(hoh_ctx* ctx, const uint16_t* G, const uint16_t* R, const uint
 
 /* ---- utilities ---------------------------------------------------------------------------- */
 
-/* Deterministic synthetic RGB (hoh_ans/synth.py formula) written to d_rgb. */
+/* Deterministic synthetic RGB (hoh_ans/synth.py formula) written to d_rgb; _rows writes only
+ * rows [y0, y0+rows) of a width-W image (a shard). */
 int hoh_synth_rgb(hoh_ctx* ctx, uint8_t* d_rgb, int W, int H, uint64_t seed, int noise, void* stream);
+int hoh_synth_rgb_rows(hoh_ctx* ctx, uint8_t* d_rgb, int W, int y0, int rows, uint64_t seed, int noise,
+                       void* stream);
 
 #ifdef __cplusplus
 }
