@@ -1,18 +1,21 @@
 // Decoder kernels (dhoh.cpp:22-283 semantics with SURVEY Q1, Q9-Q12 fixed).
-//  k_dtable: the .hoh tile table (n-1 varints after the header) -> tile offsets.
-//  k_dparse: one wave per tile walks the tile framing and its 6 entropy streams
-//            (entropy_decoding.hpp:134-257): header varints, meta byte, frequency table
-//            (clamped tables parsed in parallel: per-symbol field widths -> prefix sum ->
-//            MSB-first field extraction), payload location; writes DecStream records, the
-//            per-stream cumulative table and a 64-slot bucket table for symbol lookup.
-//  k_drans:  rANS decode (rans64.hpp:107-142).  With a side index: one lane per 1024-symbol
-//            segment starting from the encoder's checkpoint; without: one lane per stream.
-//  k_dlz:    LZ streams -> match list (un_lz.hpp:150-170, Q11/Q12 handled).
-//  k_dunpred: MED inverse (prediction.hpp:26-41 inverted, every row, Q9 fixed), LZ copies and
-//            inverse subtract-green, one workgroup per tile, three waves (one per plane) running
-//            an anti-diagonal wavefront over 64-row bands.
+//  k_dtable:  the .hoh tile table (n-1 varints after the header) -> tile offsets, parsed in
+//             parallel (terminator bytes + block prefix sums).
+//  k_dparse:  one wave per tile walks the tile framing and its 6 entropy streams
+//             (entropy_decoding.hpp:134-257): header varints, meta byte, frequency table
+//             (clamped tables parsed in parallel: per-symbol field widths -> prefix sum ->
+//             MSB-first field extraction), payload location; writes DecStream records, the
+//             per-stream cumulative table and a 512-bucket slot->symbol table.
+//  k_drans:   rANS decode (rans64.hpp:107-142).  With a side index: one workgroup per stream,
+//             lane = 1024-symbol segment from the encoder's checkpoint, tables and payload in
+//             LDS.  k_drans_serial: one lane per stream (no index).
+//  k_dlz:     LZ streams -> match list (un_lz.hpp:150-170, Q11/Q12 handled).
+//  k_dunpred_fast: MED inverse (prediction.hpp:26-41 inverted, every row, Q9 fixed) + inverse
+//             subtract-green, one wave per tile, anti-diagonal wavefront over 64-row bands.
+//  k_dunpred_lz: tiles with LZ copies, serial raster walk.
 #include "hoh_dec.h"
 #include <string.h>
+#include <algorithm>
 
 #define DSEG HOH_SEG
 
@@ -21,16 +24,17 @@ struct DecJob {
   uint64_t size;
   int W, H, xt, yt, tw, th, ntiles;
   uint32_t npix_cap, lz_cap;
+  uint32_t plane_cap;           // arena elements per tile-plane (flat or skewed layout + slack)
   uint64_t prefix;              // bytes before the tile table
   DecTile* tiles;
   DecStream* streams;
   uint32_t* cum;                // [stream][513]
   uint16_t* bsym;               // [stream][512] symbol at slot bucket*64 (prob_bits 15) / generic
-  uint16_t* dsym;               // decoded symbols: planes [tile][3][npix_cap], LZ [tile][3][lz_cap]
+  uint16_t* dsym;               // decoded symbols: planes [tile][3][plane_cap], LZ [tile][3][lz_cap]
   uint16_t* dplane;             // decoded planes of tiles with LZ matches [tile][3][npix_cap]
   uint32_t cum_stride;          // entries per stream in cum (>= range + 1)
-  int band;                     // rows per wavefront band (<= 64, LDS-bound)
-  uint32_t* matches;            // [tile][lz_cap][3]
+  uint32_t* matches;            // [tile][lz_cap+1][4]: pixel index, length, back, nuked before
+  int lzband;                   // rows per band of k_dunpred_lz (LDS-bound)
   uint8_t* rgb;                 // output image
   uint32_t* gerr;
   const IndexStream* ix;        // optional side index
@@ -59,27 +63,100 @@ __device__ __forceinline__ uint32_t get_bits(const uint8_t* b, uint64_t pos, uin
   return v;
 }
 
-__global__ void k_dtable(DecJob j) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  uint64_t p = j.prefix;
-  uint64_t off = 0;
-  for (int i = 0; i < j.ntiles; i++) {
+// inclusive block-wide prefix sum (1024 threads); returns the block total through *total
+__device__ uint64_t block_scan_1024(uint64_t v, uint64_t* wsum, uint64_t* total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t u = __shfl_up(v, o);
+    if (lane >= o) v += u;
+  }
+  if (lane == 63) wsum[wv] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t run = 0;
+    for (int i = 0; i < 16; i++) { const uint64_t x = wsum[i]; wsum[i] = run; run += x; }
+    wsum[16] = run;
+  }
+  __syncthreads();
+  v += wsum[wv];
+  *total = wsum[16];
+  __syncthreads();
+  return v;
+}
+
+// Tile table (dhoh.cpp:42-65): n-1 varints after the header give tile sizes.  Parallel parse:
+// a varint ends at a byte < 0x80, unless a run of >= 3 bytes >= 0x80 occurs (varint.hpp reads a
+// third byte whole), in which case thread 0 re-parses serially.  Shard decode (tsizes set)
+// takes the sizes from the caller instead.  Sizes are parked in tiles[i+1].off, then scanned.
+__global__ __launch_bounds__(1024) void k_dtable(DecJob j) {
+  __shared__ uint64_t wsum[17];
+  __shared__ uint64_t tend;
+  __shared__ int serial;
+  const int tid = threadIdx.x;
+  const int nt = j.ntiles, nv = nt - 1;
+  for (int i = tid; i < nt; i += 1024) {
     DecTile t;
     const int g = j.t0 + i;
     const int xo = (g % j.xt) * j.tw, yo = (g / j.xt) * j.th;
     t.x0 = xo; t.y0 = yo;
     t.w = min(j.tw, j.W - xo); t.h = min(j.th, j.H - yo);
-    t.off = off;               // relative to the first tile, fixed below
+    t.off = i == 0 ? 0 : (j.tsizes ? j.tsizes[i - 1] : 0);
     t.mode = 0; t.nmatch = 0; t.err = 0; t.pad = 0;
     j.tiles[i] = t;
-    if (i + 1 < j.ntiles) {
-      if (j.tsizes) { off += j.tsizes[i]; continue; }
-      if (p + 3 > j.size) { atomicOr(j.gerr, 1u); return; }
-      off += rd_varint(j.in, p);
+  }
+  if (tid == 0) { tend = j.prefix; serial = 0; }
+  __syncthreads();
+  if (!j.tsizes && nv > 0) {
+    const uint64_t p0 = j.prefix;
+    const uint64_t end = min((uint64_t)j.size, p0 + 3ull * nv);
+    uint64_t cnt = 0;
+    for (uint64_t base = p0; base < end && cnt < (uint64_t)nv; base += 1024) {
+      const uint64_t pos = base + tid;
+      const uint32_t b = pos < end ? j.in[pos] : 0xffu;
+      const bool term = pos < end && b < 0x80;
+      uint64_t tot;
+      const uint64_t incl = block_scan_1024(term ? 1 : 0, wsum, &tot);
+      const uint64_t idx = cnt + incl - 1;
+      if (term && idx < (uint64_t)nv) {
+        const bool b1 = pos >= p0 + 1 && j.in[pos - 1] >= 0x80;
+        const bool b2 = b1 && pos >= p0 + 2 && j.in[pos - 2] >= 0x80;
+        const bool b3 = b2 && pos >= p0 + 3 && j.in[pos - 3] >= 0x80;
+        if (b3) serial = 1;
+        uint64_t v = b;
+        if (b2) v = ((uint64_t)(j.in[pos - 2] & 0x7f) << 14) + ((uint64_t)(j.in[pos - 1] & 0x7f) << 7) + b;
+        else if (b1) v = ((uint64_t)(j.in[pos - 1] & 0x7f) << 7) + b;
+        j.tiles[idx + 1].off = v;
+        if (idx == (uint64_t)nv - 1) tend = pos + 1;
+      }
+      cnt += tot;
+    }
+    __syncthreads();
+    if (cnt < (uint64_t)nv) serial = 1;
+    __syncthreads();
+    if (serial && tid == 0) {                       // exact varint.hpp:6-27 walk
+      uint64_t p = p0;
+      bool ok = true;
+      for (int i = 0; i < nv; i++) {
+        if (p + 3 > j.size) { ok = false; break; }
+        j.tiles[i + 1].off = rd_varint(j.in, p);
+      }
+      tend = p;
+      if (!ok) atomicOr(j.gerr, 1u);
     }
   }
-  for (int i = 0; i < j.ntiles; i++) j.tiles[i].off += p;   // tiles follow the table (dhoh.cpp:42-65)
-  if (j.tiles[j.ntiles - 1].off >= j.size) atomicOr(j.gerr, 1u);
+  __syncthreads();
+  // exclusive offsets: tiles follow the table
+  uint64_t carry = tend;
+  for (int i0 = 0; i0 < nt; i0 += 1024) {
+    const int i = i0 + tid;
+    const uint64_t v = i < nt ? j.tiles[i].off : 0;
+    uint64_t tot;
+    const uint64_t incl = block_scan_1024(v, wsum, &tot);
+    if (i < nt) j.tiles[i].off = carry + incl;     // tiles[0].off holds 0
+    carry += tot;
+  }
+  __syncthreads();
+  if (tid == 0 && j.tiles[nt - 1].off >= j.size) atomicOr(j.gerr, 1u);
 }
 
 // parse one entropy stream starting at byte p (all lanes, uniform control flow)
@@ -216,7 +293,7 @@ __global__ __launch_bounds__(64) void k_dparse(DecJob j) {
   }
   if (ok) {
     const uint8_t lzt = j.in[p++];
-    const size_t lzbase = (size_t)j.ntiles * 3 * j.npix_cap + (size_t)t * 3 * j.lz_cap;
+    const size_t lzbase = (size_t)j.ntiles * 3 * j.plane_cap + (size_t)t * 3 * j.lz_cap;
     if (lzt != 0x03) { ok = false; err = 2; }
     for (int k = 0; k < 3 && ok; k++) ok = parse_stream(j, p, t * SK_PER_TILE + k, lzbase + (size_t)k * j.lz_cap, lane);
     if (ok && p + 1 < j.size && j.in[p] == 0x81 && j.in[p + 1] == 0x7f) { ok = false; err = 2; }  // 4th LZ stream (-s>=1)
@@ -235,7 +312,7 @@ __global__ __launch_bounds__(64) void k_dparse(DecJob j) {
         break;
       }
       q += 5;
-      ok = parse_stream(j, q, t * SK_PER_TILE + 3 + k, (size_t)(t * 3 + k) * j.npix_cap, lane);
+      ok = parse_stream(j, q, t * SK_PER_TILE + 3 + k, (size_t)(t * 3 + k) * j.plane_cap, lane);
       const uint32_t depth = k ? 9 : 8;
       if (ok && j.streams[t * SK_PER_TILE + 3 + k].range != (1u << depth)) ok = false;
     }
@@ -269,77 +346,244 @@ __device__ __forceinline__ uint32_t ld_u32_unaligned(const uint8_t* base, uint64
   return __builtin_amdgcn_alignbyte(hi, lo, sh);
 }
 
-// rANS decode of [s0, s1) of stream d from state x, word cursor wp (byte offset of next word)
+// Plane residuals of tiles without LZ matches are stored "skewed" for the wavefront unpredict:
+// band b (rows 64b..64b+63), step st, lane r hold the residual of (x = st - r, y = 64b + r), so
+// the 64 lanes of k_dunpred_fast read 128 contiguous bytes per plane per step.
+__device__ __forceinline__ uint32_t skew_pos(uint32_t x, uint32_t y, uint32_t w) {
+  const uint32_t r = y & 63;
+  return ((y >> 6) * (w + 63) + x + r) * 64 + r;
+}
+
+// skewed-layout width of stream sid (0: flat).  Only complete planes (n == w*h, i.e. no LZ
+// nukes) are skewed; the single-stream decoder has no tiles.
+__device__ __forceinline__ uint32_t skew_w(const DecJob& j, int sid, uint32_t n) {
+  if (!j.tiles || sid % SK_PER_TILE < 3) return 0;
+  const DecTile& t = j.tiles[sid / SK_PER_TILE];
+  return n == (uint32_t)(t.w * t.h) ? (uint32_t)t.w : 0u;
+}
+
+struct OutCursor {
+  uint16_t* out;
+  uint32_t w, x, y;
+  __device__ OutCursor(uint16_t* o, uint32_t w_, uint32_t i) : out(o), w(w_), x(w_ ? i % w_ : 0), y(w_ ? i / w_ : 0) {}
+  __device__ __forceinline__ void put(uint32_t i, uint16_t v) {
+    if (w) {
+      out[skew_pos(x, y, w)] = v;
+      if (++x == w) { x = 0; y++; }
+    } else {
+      out[i] = v;
+    }
+  }
+};
+
+// rANS decode (rans64.hpp:107-142) of symbols [s0, s1) of stream d from state x.  Payload words
+// come from `words` (LDS-staged, word index wi) when non-null, else from the file (byte wp).
+template <bool LDSW>
 __device__ bool dec_run(const DecJob& j, const DecStream& d, const uint32_t* cum, const uint16_t* bs,
-                        uint64_t x, uint64_t wp, uint64_t wend, uint32_t s0, uint32_t s1, uint16_t* out,
-                        uint64_t* xend) {
-  const uint32_t pb = d.pb, mask = (1u << pb) - 1;
-  const uint32_t bshift = pb > 9 ? pb - 9 : 0;
+                        uint32_t bshift, const uint32_t* words, uint64_t x, uint64_t wp, uint64_t wend,
+                        uint32_t s0, uint32_t s1, OutCursor oc, uint64_t* xend) {
+  const uint32_t pb = d.pb, mask = (1u << pb) - 1, range = d.range;
   for (uint32_t i = s0; i < s1; i++) {
     const uint32_t slot = (uint32_t)x & mask;
     uint32_t s = bs[slot >> bshift];
-    while (cum[s + 1] <= slot) s++;
-    out[i] = (uint16_t)s;
+    while (cum[s + 1] <= slot && s + 1 < range) s++;
+    oc.put(i, (uint16_t)s);
     const uint32_t c = cum[s], f = cum[s + 1] - c;
     x = (uint64_t)f * (x >> pb) + (slot - c);                // Rans64DecAdvance
     if (x < (1ull << 31)) {
-      if (wp + 4 > wend) return false;
-      x = (x << 32) | ld_u32_unaligned(j.in, wp);
-      wp += 4;
+      if (wp >= wend) return false;
+      x = (x << 32) | (LDSW ? words[wp] : ld_u32_unaligned(j.in, wp));
+      wp += LDSW ? 1 : 4;
     }
   }
   *xend = x;
   return true;
 }
 
-// grid: with index -> one workgroup (64 lanes) per stream, lane = segment (strided);
-//       without    -> 64 streams per workgroup, one lane each.
-__global__ __launch_bounds__(64) void k_drans(DecJob j, int nstreams, int indexed) {
-  __shared__ uint32_t cum_s[513];
-  __shared__ uint16_t bs_s[512];
-  const int lane = threadIdx.x;
-  if (indexed) {
-    const int sid = blockIdx.x;
-    const DecStream d = j.streams[sid];
-    if (d.mode != SM_RANS || d.range > 512) return;
-    for (uint32_t i = lane; i <= d.range; i += 64) cum_s[i] = j.cum[(size_t)sid * j.cum_stride + i];
-    for (uint32_t i = lane; i < 512; i += 64) bs_s[i] = j.bsym[(size_t)sid * 512 + i];
-    __syncthreads();
-    const uint64_t wend = d.payload_off + (uint64_t)d.words * 4;
-    uint16_t* out = j.dsym + d.out_off;
-    if (d.ix < 0) {
-      // no index for this stream: serial on lane 0
-      if (lane == 0) {
-        uint64_t x = (uint64_t)ld_u32_unaligned(j.in, d.payload_off) | ((uint64_t)ld_u32_unaligned(j.in, d.payload_off + 4) << 32);
-        uint64_t xe;
-        if (!dec_run(j, d, cum_s, bs_s, x, d.payload_off + 8, wend, 0, d.n, out, &xe) || xe != (1ull << 31)) atomicOr(j.gerr, 4u);
-      }
-      return;
+#define DR_BK 1024   // slot buckets per stream table
+#define DR_DB 16     // symbols per block (<= 8 payload words at pb <= 15)
+#define DR_RP 33     // LDS word-ring pitch per lane (32 words + 1 pad)
+
+// Payload words [k, k+8) of a stream whose word 0 is at byte `pay` (any alignment), in two
+// halves so the loads can be awaited a block later: issue() loads the 9 aligned dwords covering
+// them (addresses clamped to the last whole dword of the file, so no branch), finish() swaps in
+// the file's partial tail dword where the clamp applied and realigns.
+struct WordFetch {
+  uint64_t last;    // byte offset of the last whole dword of the file
+  uint32_t tail;    // bytes [size & ~3, size) as a dword (0 if none)
+  __device__ void init(const DecJob& j) {
+    last = j.size >= 4 ? (j.size & ~3ull) - 4 : 0;
+    tail = 0;
+    for (uint64_t q = j.size & ~3ull; q < j.size; q++) tail |= (uint32_t)j.in[q] << (8 * (q & 3));
+  }
+  __device__ __forceinline__ void issue(const DecJob& j, uint64_t pay, uint32_t k, uint32_t* raw) const {
+    const uint64_t base = (pay & ~3ull) + (uint64_t)k * 4;
+#pragma unroll
+    for (int q = 0; q < 9; q++) raw[q] = *(const uint32_t*)(j.in + min(base + (uint64_t)q * 4, last));
+  }
+  __device__ __forceinline__ void finish(uint64_t pay, uint32_t k, const uint32_t* raw, uint32_t* wv) const {
+    const uint32_t al = (uint32_t)(pay & 3);
+    const uint64_t base = (pay & ~3ull) + (uint64_t)k * 4;
+    uint32_t a[9];
+#pragma unroll
+    for (int q = 0; q < 9; q++) {
+      const uint64_t ad = base + (uint64_t)q * 4;
+      a[q] = ad <= last ? raw[q] : (ad == last + 4 ? tail : 0u);
     }
-    const IndexStream xs = j.ix[d.ix];
-    const uint32_t nseg = (d.n + DSEG - 1) / DSEG;
-    for (uint32_t sg = lane; sg < nseg; sg += 64) {
-      const Checkpoint c = j.ck[xs.ckpt_off + sg];
-      const uint64_t x = (uint64_t)c.xl | ((uint64_t)c.xh << 32);
-      const uint64_t wp = d.payload_off + (uint64_t)(c.widx - xs.widx_end) * 4;
-      const uint32_t s0 = sg * DSEG, s1 = min(d.n, s0 + DSEG);
+#pragma unroll
+    for (int q = 0; q < 8; q++) wv[q] = __builtin_amdgcn_alignbyte(a[q + 1], a[q], al);   // al = 0: a[q]
+  }
+};
+
+// Indexed decode: one workgroup (64 lanes) per stream, lane = 1024-symbol segment starting from
+// the encoder's checkpoint.  LDS holds the stream's cumulative table, a 1024-bucket table
+// (first symbol of each bucket + its packed start/frequency) and a 32-word payload ring per
+// lane.  Work proceeds in 16-symbol blocks: at a block boundary the lane lands the 8 words it
+// prefetched one block earlier, issues the stores of the previous block's symbols and the next
+// prefetch; inside a block the dependent chain touches LDS only.  (gfx9 counts loads and stores
+// on one vmcnt, so a load awaited right after a store would wait for the store: every global
+// access here is awaited one block after issue.)
+__global__ __launch_bounds__(64) void k_drans(DecJob j, int nstreams) {
+  __shared__ uint32_t cum_s[514];
+  __shared__ uint32_t cf_s[DR_BK];
+  __shared__ uint16_t sy_s[DR_BK];
+  __shared__ uint32_t ring[64 * DR_RP];
+  const int lane = threadIdx.x;
+  const int sid = blockIdx.x;
+  const DecStream d = j.streams[sid];
+  if (d.mode != SM_RANS || d.range > 512) return;
+  for (uint32_t i = lane; i <= d.range; i += 64) cum_s[i] = j.cum[(size_t)sid * j.cum_stride + i];
+  const uint32_t bshift = d.pb > 10 ? d.pb - 10 : 0;
+  const uint32_t nbk = 1u << (d.pb - bshift);
+  __syncthreads();
+  for (uint32_t s = lane; s < d.range; s += 64) {          // bucket b starts inside symbol s's slots
+    const uint32_t c0 = cum_s[s], c1 = cum_s[s + 1];
+    if (c1 <= c0) continue;
+    const uint32_t b1 = (c1 - 1) >> bshift;
+    for (uint32_t b = (c0 + (1u << bshift) - 1) >> bshift; b <= b1 && b < nbk; b++) {
+      sy_s[b] = (uint16_t)s;
+      cf_s[b] = c0 | ((c1 - c0) << 16);
+    }
+  }
+  __syncthreads();
+  uint16_t* out = j.dsym + d.out_off;
+  const uint32_t sw = skew_w(j, sid, d.n);
+  const uint32_t pb = d.pb, mask = (1u << pb) - 1, range = d.range;
+  if (d.ix < 0) {
+    // no index for this stream: serial on lane 0 from the file
+    if (lane == 0) {
+      const uint64_t wend = d.payload_off + (uint64_t)d.words * 4;
+      uint64_t x = (uint64_t)ld_u32_unaligned(j.in, d.payload_off) | ((uint64_t)ld_u32_unaligned(j.in, d.payload_off + 4) << 32);
       uint64_t xe;
-      bool ok = dec_run(j, d, cum_s, bs_s, x, wp, wend, s0, s1, out, &xe);
-      uint64_t want = 1ull << 31;
-      if (sg + 1 < nseg) { const Checkpoint c2 = j.ck[xs.ckpt_off + sg + 1]; want = (uint64_t)c2.xl | ((uint64_t)c2.xh << 32); }
-      if (!ok || xe != want) atomicOr(j.gerr, 4u);
+      if (!dec_run<false>(j, d, cum_s, sy_s, bshift, nullptr, x, d.payload_off + 8, wend, 0, d.n,
+                          OutCursor(out, sw, 0), &xe) || xe != (1ull << 31))
+        atomicOr(j.gerr, 4u);
     }
     return;
   }
-  const int sid = blockIdx.x * 64 + lane;
+  const IndexStream xs = j.ix[d.ix];
+  const uint32_t nseg = (d.n + DSEG - 1) / DSEG;
+  uint32_t* myring = ring + lane * DR_RP;
+  WordFetch wf;
+  wf.init(j);
+  bool bad = false;
+  for (uint32_t sg0 = 0; sg0 < nseg; sg0 += 64) {
+    const uint32_t sg = sg0 + lane;
+    const bool act = sg < nseg;
+    uint64_t x = 0;
+    uint32_t wi = 0, s0 = 0, s1 = 0;
+    if (act) {
+      const Checkpoint c = j.ck[xs.ckpt_off + sg];
+      x = (uint64_t)c.xl | ((uint64_t)c.xh << 32);
+      wi = c.widx - xs.widx_end;
+      s0 = sg * DSEG;
+      s1 = min(d.n, s0 + DSEG);
+    }
+    // initial fill: words [wi, wi+24)
+    uint32_t lw = wi;
+    for (int g = 0; g < 3; g++) {
+      uint32_t raw[9], wv[8];
+      wf.issue(j, d.payload_off, lw, raw);
+      wf.finish(d.payload_off, lw, raw, wv);
+#pragma unroll
+      for (int q = 0; q < 8; q++) myring[(lw + q) & 31] = wv[q];
+      lw += 8;
+    }
+    OutCursor oc(out, sw, s0);
+    uint32_t pend[9];                                  // raw dwords of the in-flight prefetch
+    bool haspend = false;
+    uint32_t pk = lw;                                  // its first word
+    uint32_t sym[DR_DB];
+    wf.issue(j, d.payload_off, pk, pend);
+    for (uint32_t blk = 0; blk <= DSEG / DR_DB; blk++) {
+      const uint32_t i0 = s0 + blk * DR_DB;
+      {                                                // land the prefetch issued one block ago
+        uint32_t wv[8];
+#pragma unroll
+        for (int q = 0; q < 9; q++) asm volatile("" ::"v"(pend[q]));   // the vmcnt wait lands here
+        wf.finish(d.payload_off, pk, pend, wv);
+        if (haspend) {
+#pragma unroll
+          for (int q = 0; q < 8; q++) myring[(lw + q) & 31] = wv[q];
+          lw += 8;
+        }
+      }
+      if (blk > 0 && act) {                            // stores of the previous block's symbols
+#pragma unroll
+        for (int k = 0; k < DR_DB; k++)
+          if (i0 - DR_DB + k < s1) oc.put(i0 - DR_DB + k, (uint16_t)sym[k]);
+      }
+      if (blk == DSEG / DR_DB) break;
+      haspend = act && lw + 8 <= wi + 32 && lw < d.words;
+      pk = lw;
+      wf.issue(j, d.payload_off, pk, pend);
+#pragma unroll
+      for (int k = 0; k < DR_DB; k++) {
+        const uint32_t i = i0 + k;
+        if (act && i < s1) {
+          const uint32_t nw = myring[wi & 31];
+          const uint32_t slot = (uint32_t)x & mask;
+          const uint32_t bk = slot >> bshift;
+          uint32_t cf = cf_s[bk];
+          uint32_t s = sy_s[bk];
+          uint32_t c = cf & 0xffffu, f = cf >> 16;
+          if (slot - c >= f) {                        // slot past the bucket's first symbol
+            while (s + 1 < range && cum_s[s + 1] <= slot) s++;
+            c = cum_s[s];
+            f = cum_s[s + 1] - c;
+          }
+          sym[k] = s;
+          x = (uint64_t)f * (x >> pb) + (slot - c);   // Rans64DecAdvance
+          if (x < (1ull << 31)) {
+            if (wi >= lw) bad = true;
+            x = (x << 32) | nw;
+            wi++;
+          }
+        }
+      }
+    }
+    if (act) {
+      uint64_t want = 1ull << 31;
+      if (sg + 1 < nseg) { const Checkpoint c2 = j.ck[xs.ckpt_off + sg + 1]; want = (uint64_t)c2.xl | ((uint64_t)c2.xh << 32); }
+      if (x != want || wi > d.words) bad = true;
+    }
+  }
+  if (bad) atomicOr(j.gerr, 4u);
+}
+
+// Without an index: one lane per stream, tables from the parse kernel (512 buckets).
+__global__ __launch_bounds__(64) void k_drans_serial(DecJob j, int nstreams) {
+  const int sid = blockIdx.x * 64 + threadIdx.x;
   if (sid >= nstreams) return;
   const DecStream d = j.streams[sid];
   if (d.mode != SM_RANS) return;
   const uint64_t wend = d.payload_off + (uint64_t)d.words * 4;
   uint64_t x = (uint64_t)ld_u32_unaligned(j.in, d.payload_off) | ((uint64_t)ld_u32_unaligned(j.in, d.payload_off + 4) << 32);
   uint64_t xe;
-  if (!dec_run(j, d, j.cum + (size_t)sid * j.cum_stride, j.bsym + (size_t)sid * 512, x, d.payload_off + 8, wend, 0, d.n,
-               j.dsym + d.out_off, &xe) || xe != (1ull << 31))
+  const uint32_t bshift = d.pb > 9 ? d.pb - 9 : 0;
+  if (!dec_run<false>(j, d, j.cum + (size_t)sid * j.cum_stride, j.bsym + (size_t)sid * 512, bshift, nullptr, x,
+                      d.payload_off + 8, wend, 0, d.n, OutCursor(j.dsym + d.out_off, skew_w(j, sid, d.n), 0), &xe) ||
+      xe != (1ull << 31))
     atomicOr(j.gerr, 4u);
 }
 
@@ -349,8 +593,11 @@ __global__ void k_dstored(DecJob j, int nstreams) {
   const DecStream d = j.streams[sid];
   if (d.mode != SM_STORED) return;
   uint16_t* out = j.dsym + d.out_off;
-  for (uint32_t i = threadIdx.x; i < d.n; i += blockDim.x)
-    out[i] = (uint16_t)get_bits(j.in, d.payload_off * 8 + (uint64_t)i * d.maxbits, d.maxbits);
+  const uint32_t sw = skew_w(j, sid, d.n);
+  for (uint32_t i = threadIdx.x; i < d.n; i += blockDim.x) {
+    const uint16_t v = (uint16_t)get_bits(j.in, d.payload_off * 8 + (uint64_t)i * d.maxbits, d.maxbits);
+    out[sw ? skew_pos(i % sw, i / sw, sw) : i] = v;
+  }
 }
 
 // LZ streams -> matches (un_lz.hpp:150-170); one lane per tile
@@ -363,9 +610,9 @@ __global__ void k_dlz(DecJob j) {
   const uint16_t* fut = j.dsym + st[0].out_off;
   const uint16_t* len = j.dsym + st[1].out_off;
   const uint16_t* bb = j.dsym + st[2].out_off;
-  uint32_t* mt = j.matches + (size_t)t * 3 * (j.lz_cap + 1);
+  uint32_t* mt = j.matches + (size_t)t * 4 * (j.lz_cap + 1);
   const uint32_t npix = (uint32_t)ti.w * ti.h;
-  uint32_t idx = 0, g = 0, nm = 0;
+  uint32_t idx = 0, g = 0, nm = 0, nuked = 0;
   bool bad = false;
   for (uint32_t i = 0; i < st[0].n; i++) {
     const uint32_t v = fut[i];
@@ -375,9 +622,10 @@ __global__ void k_dlz(DecJob j) {
     const uint32_t L = len[g] + 4, back = bb[g];
     g++;
     if (back == 0 || back > idx || idx + L > npix) { bad = true; break; }
-    mt[3 * nm] = idx; mt[3 * nm + 1] = L; mt[3 * nm + 2] = back;
+    mt[4 * nm] = idx; mt[4 * nm + 1] = L; mt[4 * nm + 2] = back; mt[4 * nm + 3] = nuked;
     nm++;
     idx += L;
+    nuked += L;
   }
   if (idx > npix) bad = true;
   ti.nmatch = nm;
@@ -390,79 +638,263 @@ __device__ __forceinline__ uint16_t dmed16(uint16_t a, uint16_t b, uint16_t c) {
   return b < c ? b : (c > a ? c : a);
 }
 
-// Tiles without LZ matches: wavefront.  Each of 3 waves decodes one plane; a band of 64 rows is
-// swept along anti-diagonals (lane = row in band, step t decodes x = t - lane), T/TL come from
-// the lane above via DPP-free __shfl_up of the previous step, row -1 of a band from LDS.
-// Tiles with matches (rare) use a serial raster loop per plane (LZ copies can point up-right).
-#define BAND 64
-__global__ __launch_bounds__(192) void k_dunpred(DecJob j) {
+// fast-path eligibility: no LZ copies and three complete (skewed) planes
+__device__ __forceinline__ bool unpred_fast(const DecJob& j, int t, const DecTile& ti) {
+  const DecStream* st = j.streams + (size_t)t * SK_PER_TILE + 3;
+  const uint32_t np = (uint32_t)ti.w * ti.h;
+  return ti.nmatch == 0 && st[0].n == np && st[1].n == np && st[2].n == np;
+}
+
+// lane r gets v of lane r-1; lane 0 gets `old` (DPP wave_shr:1, bound_ctrl off)
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v, uint32_t old) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xf, 0xf, false);
+}
+
+__device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
+  return max(min(a, b), min(max(a, b), c));
+}
+
+#define UP_P 8   // residual prefetch depth (steps)
+
+// Wavefront MED inverse (prediction.hpp:26-41 inverted on every row, Q9 fixed) of the three
+// planes of one tile + inverse subtract-green (channel.hpp:73-79), one wave per tile.
+// Lane r owns row 64b + r of band b and decodes x = st - r at step st; T and TL come from lane
+// r-1 through DPP (its values at steps st-1 and st-2), row -1 of a band from LDS.  The three
+// planes are independent chains interleaved in one instruction stream.
+// LDS row pitch (bytes) of the output staging band: whole dwords, odd dword count (bank spread)
+__host__ __device__ __forceinline__ uint32_t ostage_pitch(uint32_t tw) {
+  uint32_t dw = (tw * 3 + 3) / 4;
+  return (dw | 1u) * 4;
+}
+
+__global__ __launch_bounds__(64) void k_dunpred_fast(DecJob j) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int t = blockIdx.x;
   const DecTile ti = j.tiles[t];
-  if (ti.err) return;
+  if (ti.err || !unpred_fast(j, t, ti)) return;
+  const uint32_t opitch = ostage_pitch(j.tw);
+  uint8_t* ob = lds;                                   // [64][opitch] RGB bytes of the band
+  uint16_t* lastG = (uint16_t*)(lds + 64 * opitch);
+  uint16_t* lastR = lastG + j.tw;
+  uint16_t* lastB = lastR + j.tw;
+  const int lane = threadIdx.x;
+  const int w = ti.w, h = ti.h, nst = w + 63;
+  const uint16_t* skG = j.dsym + (size_t)(t * 3) * j.plane_cap + lane;
+  const uint16_t* skR = skG + j.plane_cap;
+  const uint16_t* skB = skR + j.plane_cap;
+  const size_t pitch = (size_t)j.W * 3;
+  uint8_t* obase = j.rgb + ((size_t)ti.y0 * j.W + ti.x0) * 3;
+  const bool dw_ok = ((pitch | ((size_t)ti.x0 * 3) | (size_t)j.rgb) & 3) == 0;
+  for (int r0 = 0; r0 < h; r0 += 64) {
+    const int y = r0 + lane;
+    const int last = min(63, h - r0 - 1);
+    const bool rowok = y < h;
+    const size_t bo = (size_t)(r0 >> 6) * nst * 64;
+    uint32_t qG[UP_P], qR[UP_P], qB[UP_P];
+#pragma unroll
+    for (int u = 0; u < UP_P; u++) { qG[u] = skG[bo + u * 64]; qR[u] = skR[bo + u * 64]; qB[u] = skB[bo + u * 64]; }
+    uint32_t cG = 0, cR = 0, cB = 0;      // this lane's value at the previous step (L)
+    uint32_t pG = 128, pR = 256, pB = 256; // T of the previous step (TL)
+    uint8_t* orow = ob + (size_t)lane * opitch;
+    for (int s0 = 0; s0 < nst; s0 += UP_P) {
+#pragma unroll
+      for (int u = 0; u < UP_P; u++) {
+        const int st = s0 + u;
+        const int x = st - lane;
+        const uint32_t rG = qG[u], rR = qR[u], rB = qB[u];
+        const size_t nx = bo + (size_t)(st + UP_P) * 64;
+        qG[u] = skG[nx]; qR[u] = skR[nx]; qB[u] = skB[nx];
+        uint32_t oG = 128, oR = 256, oB = 256;        // lane 0: row above the band
+        if (r0 > 0 && lane == 0 && x < w) { oG = lastG[x]; oR = lastR[x]; oB = lastB[x]; }
+        const uint32_t TG = wave_shr1(cG, oG), TR = wave_shr1(cR, oR), TB = wave_shr1(cB, oB);
+        const bool xz = x <= 0;
+        const uint32_t LG = xz ? 128u : cG, LR = xz ? 256u : cR, LB = xz ? 256u : cB;
+        const uint32_t AG = xz ? 128u : pG, AR = xz ? 256u : pR, AB = xz ? 256u : pB;
+        const uint32_t vG = (rG + med3u(TG, LG, (TG + LG - AG) & 0xffffu) + 128u) & 255u;
+        const uint32_t vR = (rR + med3u(TR, LR, (TR + LR - AR) & 0xffffu) + 256u) & 511u;
+        const uint32_t vB = (rB + med3u(TB, LB, (TB + LB - AB) & 0xffffu) + 256u) & 511u;
+        pG = TG; pR = TR; pB = TB;
+        cG = vG; cR = vR; cB = vB;
+        if (rowok && x >= 0 && x < w) {
+          uint8_t* o = orow + x * 3;
+          o[0] = (uint8_t)(vR + vG); o[1] = (uint8_t)vG; o[2] = (uint8_t)(vB + vG);
+          if (lane == last) { lastG[x] = (uint16_t)vG; lastR[x] = (uint16_t)vR; lastB[x] = (uint16_t)vB; }
+        }
+      }
+    }
+    __syncthreads();
+    // coalesced flush of the band (rows r0 .. r0+last)
+    const int rows = last + 1, rb = w * 3;
+    if (dw_ok) {
+      const int dpr = rb >> 2;
+      for (int rr = 0; rr < rows; rr++) {
+        const uint32_t* src = (const uint32_t*)(ob + (size_t)rr * opitch);
+        uint32_t* dst = (uint32_t*)(obase + (size_t)(r0 + rr) * pitch);
+        for (int e = lane; e < dpr; e += 64) dst[e] = src[e];
+        for (int e = dpr * 4 + lane; e < rb; e += 64) ((uint8_t*)dst)[e] = ((const uint8_t*)src)[e];
+      }
+    } else {
+      for (int rr = 0; rr < rows; rr++) {
+        const uint8_t* src = ob + (size_t)rr * opitch;
+        uint8_t* dst = obase + (size_t)(r0 + rr) * pitch;
+        for (int e = lane; e < rb; e += 64) dst[e] = src[e];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// pixels of [0, i) covered by LZ copies (matches sorted by pixel index)
+__device__ __forceinline__ uint32_t nuked_before(const uint32_t* mt, uint32_t nm, uint32_t i) {
+  uint32_t lo = 0, hi = nm;                      // first match with idx >= i
+  while (lo < hi) { const uint32_t mid = (lo + hi) / 2; if (mt[4 * mid] < i) lo = mid + 1; else hi = mid; }
+  if (lo == 0) return 0;
+  const uint32_t m = lo - 1;
+  return mt[4 * m + 3] + min(mt[4 * m + 1], i - mt[4 * m]);
+}
+
+#define PK_HALF (128u | (256u << 8) | (256u << 17))
+
+// packed (G:8 | R':9 | B':9) MED inverse of one pixel
+__device__ __forceinline__ uint32_t unpred_px(uint32_t T, uint32_t L, uint32_t TL, uint32_t r) {
+  const uint32_t tg = T & 255, lg = L & 255, ag = TL & 255;
+  const uint32_t tr = (T >> 8) & 511, lr = (L >> 8) & 511, ar = (TL >> 8) & 511;
+  const uint32_t tb = T >> 17, lb = L >> 17, ab = TL >> 17;
+  const uint32_t g = ((r & 255) + med3u(tg, lg, (tg + lg - ag) & 0xffffu) + 128u) & 255u;
+  const uint32_t rr = (((r >> 8) & 511) + med3u(tr, lr, (tr + lr - ar) & 0xffffu) + 256u) & 511u;
+  const uint32_t bb = ((r >> 17) + med3u(tb, lb, (tb + lb - ab) & 0xffffu) + 256u) & 511u;
+  return g | (rr << 8) | (bb << 17);
+}
+
+// Tiles with LZ copies (lz.hpp at -s0: back distance 1..64 pixels in raster order, so a copy
+// at the start of a row can read the end of the row above, which a fixed-skew wavefront has not
+// produced yet).  Dynamic wavefront, one wave per tile: lane r owns row r0+r of a band and
+// advances its own column counter when (a) the lane above has passed the column (T, TL) and
+// (b) a copy's source pixel is done.  Decoded pixels (packed G/R'/B') live in LDS rows
+// [row above band | band rows]; the band's residuals (a contiguous range, residuals skip
+// copied pixels) are staged in LDS first.  Needs w >= 64 (copies reach at most one row up).
+__global__ __launch_bounds__(64) void k_dunpred_lz(DecJob j) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lz_lds[];
+  const int t = blockIdx.x;
+  const DecTile ti = j.tiles[t];
+  if (ti.err || unpred_fast(j, t, ti) || ti.w < 64) return;
+  const int lane = threadIdx.x;
+  const int w = ti.w, h = ti.h, BR = j.lzband;
+  uint32_t* band = lz_lds;                                   // (BR+1) rows x w
+  uint32_t* rs = lz_lds + (size_t)(BR + 1) * w;              // BR*w packed residuals
+  const DecStream* st = j.streams + (size_t)t * SK_PER_TILE + 3;
+  const uint32_t* mt = j.matches + (size_t)t * 4 * (j.lz_cap + 1);
+  const uint32_t nm = ti.nmatch, npix = (uint32_t)w * h;
+  const uint32_t n = st[0].n;
+  if (st[1].n != n || st[2].n != n || nuked_before(mt, nm, npix) + n != npix) {
+    if (lane == 0) atomicOr(j.gerr, 1u);
+    return;
+  }
+  const uint16_t* resG = j.dsym + (size_t)(t * 3) * j.plane_cap;
+  const uint16_t* resR = resG + j.plane_cap;
+  const uint16_t* resB = resR + j.plane_cap;
+  uint8_t* obase = j.rgb + ((size_t)ti.y0 * j.W + ti.x0) * 3;
+  bool bad = false;
+  for (int r0 = 0; r0 < h; r0 += BR) {
+    const int r1 = min(h, r0 + BR);
+    const uint32_t kb0 = (uint32_t)r0 * w - nuked_before(mt, nm, (uint32_t)r0 * w);
+    const uint32_t kb1 = (uint32_t)r1 * w - nuked_before(mt, nm, (uint32_t)r1 * w);
+    for (uint32_t e = lane; e < kb1 - kb0; e += 64)
+      rs[e] = resG[kb0 + e] | ((uint32_t)resR[kb0 + e] << 8) | ((uint32_t)resB[kb0 + e] << 17);
+    __syncthreads();
+    const int y = r0 + lane;
+    const bool act = lane < BR && y < h;
+    uint32_t prog = act ? 0u : (uint32_t)w;
+    uint32_t nuk = act ? nuked_before(mt, nm, (uint32_t)y * w) : 0u;
+    uint32_t m = 0;                                          // first match ending after row start
+    if (act) {
+      uint32_t lo = 0, hi = nm;
+      while (lo < hi) { const uint32_t mid = (lo + hi) / 2; if (mt[4 * mid] + mt[4 * mid + 1] <= (uint32_t)y * w) lo = mid + 1; else hi = mid; }
+      m = lo;
+    }
+    uint32_t midx = 0xffffffffu, mlen = 0, mback = 0;
+    if (m < nm) { midx = mt[4 * m]; mlen = mt[4 * m + 1]; mback = mt[4 * m + 2]; }
+    uint32_t left = PK_HALF;
+    const uint32_t rowbase = (uint32_t)y * w;
+    uint32_t* myrow = band + (size_t)(lane + 1) * w;
+    const uint32_t* uprow = band + (size_t)lane * w;
+    uint8_t* orow = obase + (size_t)y * j.W * 3;
+    while (__any(prog < (uint32_t)w)) {
+      const uint32_t above = wave_shr1(prog, (uint32_t)w);
+      if (prog < (uint32_t)w) {
+        const uint32_t x = prog, i = rowbase + x;
+        if (m < nm && midx + mlen <= i) {
+          m++;
+          while (m < nm && mt[4 * m] + mt[4 * m + 1] <= i) m++;
+          midx = 0xffffffffu;
+          if (m < nm) { midx = mt[4 * m]; mlen = mt[4 * m + 1]; mback = mt[4 * m + 2]; }
+        }
+        const bool copy = m < nm && midx <= i;
+        bool ready = above > x;
+        uint32_t src = 0;
+        if (copy) {
+          src = i - mback;
+          if (src < rowbase) {
+            if (src + (uint32_t)w < rowbase) { bad = true; src = rowbase; }   // two rows up: w < 64 only
+            else ready = above > src + (uint32_t)w - rowbase;
+          }
+        }
+        if (ready) {
+          uint32_t v;
+          if (copy) {
+            v = src >= rowbase ? myrow[src - rowbase] : uprow[src + w - rowbase];
+            nuk++;
+          } else {
+            const uint32_t T = y == 0 ? PK_HALF : uprow[x];
+            const uint32_t TL = (y == 0 || x == 0) ? PK_HALF : uprow[x - 1];
+            const uint32_t L = x == 0 ? PK_HALF : left;
+            const uint32_t k = i - nuk;
+            uint32_t r = 0;
+            if (k < kb0 || k >= kb1) bad = true; else r = rs[k - kb0];
+            v = unpred_px(T, L, TL, r);
+          }
+          myrow[x] = v;
+          left = v;
+          const uint32_t G = v & 255;
+          uint8_t* o = orow + (size_t)x * 3;
+          o[0] = (uint8_t)(((v >> 8) & 511) + G); o[1] = (uint8_t)G; o[2] = (uint8_t)((v >> 17) + G);
+          prog++;
+        }
+      }
+    }
+    __syncthreads();
+    const int lastrow = r1 - r0;                            // LDS row of the band's last image row
+    for (int x = lane; x < w; x += 64) band[x] = band[(size_t)lastrow * w + x];
+    __syncthreads();
+  }
+  if (bad) atomicOr(j.gerr, 1u);
+}
+
+// Tiles with LZ copies narrower than 64 pixels (copies may reach two rows up): serial raster
+// walk per plane, one lane per plane, into dplane.
+__global__ __launch_bounds__(192) void k_dunpred_serial(DecJob j) {
+  const int t = blockIdx.x;
+  const DecTile ti = j.tiles[t];
+  if (ti.err || unpred_fast(j, t, ti) || ti.w >= 64) return;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int w = ti.w, h = ti.h;
   const int depth = wv ? 9 : 8, c = 1 << depth, half = c / 2;
-  const int BR = j.band;
-  uint16_t* band = (uint16_t*)lds + (size_t)wv * BR * w;         // decoded band of this plane
-  uint16_t* prevrow = (uint16_t*)lds + (size_t)3 * BR * w + (size_t)wv * w;
-  const uint16_t* res = j.dsym + (size_t)(t * 3 + wv) * j.npix_cap;
+  const uint16_t* res = j.dsym + (size_t)(t * 3 + wv) * j.plane_cap;
   const DecStream d = j.streams[t * SK_PER_TILE + 3 + wv];
-  if (ti.nmatch == 0) {
-    if (d.n != (uint32_t)(w * h)) { if (threadIdx.x == 0) atomicOr(j.gerr, 1u); return; }
-    for (int r0 = 0; r0 < h; r0 += BR) {
-      const int y = r0 + lane;
-      const bool act = y < h && lane < BR;
-      uint32_t cur = 0, prev = 0;        // this lane's value at steps t-1 and t-2
-      for (int st = 0; st < w + j.band - 1; st++) {
-        const int x = st - lane;
-        // values of the lane above at steps st-1 (x, y-1) and st-2 (x-1, y-1)
-        const uint32_t up1 = __shfl_up(cur, 1), up2 = __shfl_up(prev, 1);
-        if (act && x >= 0 && x < w) {
-          uint16_t T, TL;
-          if (y == 0) { T = half; TL = half; }
-          else if (lane == 0) { T = prevrow[x]; TL = x ? prevrow[x - 1] : (uint16_t)half; }
-          else { T = (uint16_t)up1; TL = x ? (uint16_t)up2 : (uint16_t)half; }
-          const uint16_t L = x ? (uint16_t)cur : (uint16_t)half;
-          const uint16_t p = dmed16(T, L, (uint16_t)(T + L - TL));
-          const uint16_t v = (uint16_t)((res[(size_t)y * w + x] + p - half + c) & (c - 1));
-          band[lane * w + x] = v;
-          prev = cur;
-          cur = v;
-        }
-      }
-      __syncthreads();
-      // row r0+63 (or the last row) becomes row -1 of the next band
-      const int last = min(BR, h - r0) - 1;
-      for (int x = lane; x < w; x += 64) prevrow[x] = band[last * w + x];
-      // inverse subtract-green for this band once all three planes are done
-      uint16_t* bG = (uint16_t*)lds;
-      uint16_t* bR = bG + BR * w;
-      uint16_t* bB = bR + BR * w;
-      const int rows = last + 1;
-      for (int i = threadIdx.x; i < rows * w; i += 192) {
-        const int yy = i / w, xx = i % w;
-        const uint16_t G = bG[i], R = bR[i], B = bB[i];
-        uint8_t* o = j.rgb + ((size_t)(ti.y0 + r0 + yy) * j.W + ti.x0 + xx) * 3;
-        o[0] = (uint8_t)(R + G - 256); o[1] = (uint8_t)G; o[2] = (uint8_t)(B + G - 256);
-      }
-      __syncthreads();
-    }
-    return;
-  }
-  // serial path (tiles with LZ matches): lane 0 of each wave walks its plane in raster order
-  const uint32_t* mt = j.matches + (size_t)t * 3 * (j.lz_cap + 1);
+  const uint32_t* mt = j.matches + (size_t)t * 4 * (j.lz_cap + 1);
   uint16_t* plane = j.dplane + (size_t)(t * 3 + wv) * j.npix_cap;
   if (lane == 0) {
     uint32_t k = 0, m = 0, nm = ti.nmatch;   // residuals are consumed by the non-matched pixels
-    for (int y = 0; y < h; y++) {
+    bool bad = false;
+    for (int y = 0; y < h && !bad; y++) {
       for (int x = 0; x < w; x++) {
         const uint32_t i = (uint32_t)y * w + x;
-        while (m < nm && mt[3 * m] + mt[3 * m + 1] <= i) m++;
+        while (m < nm && mt[4 * m] + mt[4 * m + 1] <= i) m++;
         uint16_t v;
-        if (m < nm && mt[3 * m] <= i) {
-          v = plane[i - mt[3 * m + 2]];
+        if (m < nm && mt[4 * m] <= i) {
+          v = plane[i - mt[4 * m + 2]];
         } else {
+          if (k >= d.n) { bad = true; break; }
           const uint16_t r = res[k++];
           const uint16_t L = x ? plane[i - 1] : (uint16_t)half;
           const uint16_t T = y ? plane[i - w] : (uint16_t)half;
@@ -473,7 +905,7 @@ __global__ __launch_bounds__(192) void k_dunpred(DecJob j) {
         plane[i] = v;
       }
     }
-    if (k != d.n) atomicOr(j.gerr, 1u);
+    if (bad || k != d.n) atomicOr(j.gerr, 1u);
   }
   __syncthreads();
   const uint16_t* G = j.dplane + (size_t)(t * 3) * j.npix_cap;
@@ -572,6 +1004,10 @@ int decode_tiles_impl(hoh_ctx* c, const uint8_t* d_blob, size_t size, int W, int
 static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s) {
   j.npix_cap = (uint32_t)(((size_t)j.tw * j.th + 63) / 64 * 64);
   j.lz_cap = (uint32_t)((j.npix_cap / 4 + j.npix_cap / 255 + 16 + 7) / 8 * 8);
+  {
+    const size_t skew = (size_t)((j.th + 63) / 64) * (j.tw + 63) * 64 + (size_t)UP_P * 64;
+    j.plane_cap = (uint32_t)((std::max((size_t)j.npix_cap, skew) + 63) / 64 * 64);
+  }
   const int S = j.ntiles * SK_PER_TILE;
   DecWork& w = ctx_dec(c);
   void* q;
@@ -581,8 +1017,8 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   j.cum_stride = 513;
   if ((e = dbuf(w, 2, (size_t)S * 513 * 4, &q))) return e; j.cum = (uint32_t*)q;
   if ((e = dbuf(w, 3, (size_t)S * 512 * 2, &q))) return e; j.bsym = (uint16_t*)q;
-  if ((e = dbuf(w, 4, ((size_t)j.ntiles * 3 * j.npix_cap + (size_t)j.ntiles * 3 * j.lz_cap) * 2, &q))) return e; j.dsym = (uint16_t*)q;
-  if ((e = dbuf(w, 5, (size_t)j.ntiles * 3 * (j.lz_cap + 1) * 4, &q))) return e; j.matches = (uint32_t*)q;
+  if ((e = dbuf(w, 4, ((size_t)j.ntiles * 3 * j.plane_cap + (size_t)j.ntiles * 3 * j.lz_cap) * 2, &q))) return e; j.dsym = (uint16_t*)q;
+  if ((e = dbuf(w, 5, (size_t)j.ntiles * 4 * (j.lz_cap + 1) * 4, &q))) return e; j.matches = (uint32_t*)q;
   if ((e = dbuf(w, 6, 64, &q))) return e; j.gerr = (uint32_t*)q;
   if ((e = dbuf(w, 7, (size_t)j.ntiles * 3 * j.npix_cap * 2, &q))) return e; j.dplane = (uint16_t*)q;
   j.ix = index_streams(idx);
@@ -592,24 +1028,24 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   if (hipMemsetAsync(j.gerr, 0, 64, s) != hipSuccess) return 3;
   if (hipMemsetAsync(j.streams, 0, (size_t)S * sizeof(DecStream), s) != hipSuccess) return 3;
   ctx_mark(c, s, "start", true);
-  hipLaunchKernelGGL(k_dtable, dim3(1), dim3(64), 0, s, j);
+  hipLaunchKernelGGL(k_dtable, dim3(1), dim3(1024), 0, s, j);
   ctx_mark(c, s, "dtable", false);
   hipLaunchKernelGGL(k_dparse, dim3(j.ntiles), dim3(64), 0, s, j);
   ctx_mark(c, s, "dparse", false);
   if (indexed) {
     hipLaunchKernelGGL(k_dmatch, dim3((S + 255) / 256), dim3(256), 0, s, j, S);
-    hipLaunchKernelGGL(k_drans, dim3(S), dim3(64), 0, s, j, S, 1);
+    hipLaunchKernelGGL(k_drans, dim3(S), dim3(64), 0, s, j, S);
   } else {
-    hipLaunchKernelGGL(k_drans, dim3((S + 63) / 64), dim3(64), 0, s, j, S, 0);
+    hipLaunchKernelGGL(k_drans_serial, dim3((S + 63) / 64), dim3(64), 0, s, j, S);
   }
   ctx_mark(c, s, "drans", false);
   hipLaunchKernelGGL(k_dstored, dim3(S), dim3(256), 0, s, j, S);
   hipLaunchKernelGGL(k_dlz, dim3((j.ntiles + 63) / 64), dim3(64), 0, s, j);
   ctx_mark(c, s, "dlz", false);
-  j.band = BAND;
-  while (j.band > 1 && (size_t)3 * j.band * j.tw * 2 + (size_t)3 * j.tw * 2 > 160 * 1024) j.band /= 2;
-  const size_t lds = (size_t)3 * j.band * j.tw * 2 + (size_t)3 * j.tw * 2;
-  hipLaunchKernelGGL(k_dunpred, dim3(j.ntiles), dim3(192), lds, s, j);
+  hipLaunchKernelGGL(k_dunpred_fast, dim3(j.ntiles), dim3(64), (size_t)64 * ostage_pitch(j.tw) + (size_t)3 * j.tw * 2, s, j);
+  j.lzband = (int)std::min<size_t>(64, (160 * 1024 - (size_t)j.tw * 4) / ((size_t)j.tw * 8));
+  hipLaunchKernelGGL(k_dunpred_lz, dim3(j.ntiles), dim3(64), (size_t)(2 * j.lzband + 1) * j.tw * 4, s, j);
+  hipLaunchKernelGGL(k_dunpred_serial, dim3(j.ntiles), dim3(192), 0, s, j);
   ctx_mark(c, s, "dunpred", false);
   if (hipGetLastError() != hipSuccess) return 3;
   uint64_t* pin = ctx_pinned(c);
@@ -636,7 +1072,8 @@ __global__ __launch_bounds__(64) void k_dstream(DecJob j, uint64_t bp, uint64_t*
     const uint64_t wend = d.payload_off + (uint64_t)d.words * 4;
     uint64_t x = (uint64_t)ld_u32_unaligned(j.in, d.payload_off) | ((uint64_t)ld_u32_unaligned(j.in, d.payload_off + 4) << 32);
     uint64_t xe;
-    if (!dec_run(j, d, j.cum, j.bsym, x, d.payload_off + 8, wend, 0, d.n, j.dsym, &xe) || xe != (1ull << 31)) {
+    if (!dec_run<false>(j, d, j.cum, j.bsym, d.pb > 9 ? d.pb - 9 : 0, nullptr, x, d.payload_off + 8, wend, 0, d.n,
+                        OutCursor(j.dsym, 0, 0), &xe) || xe != (1ull << 31)) {
       res[0] = 1;
       return;
     }
