@@ -8,7 +8,7 @@
 #define HOH_WAVE 64
 #define HOH_HDR_CAP 1600          // bytes reserved per stream for varints + meta + table
 #define HOH_FAST_RANGE 512        // LDS-table fast encoder handles range <= 512 at prob_bits 15
-#define HOH_SEG 1024              // decode checkpoint spacing (symbols)
+#define HOH_SEG 256               // decode checkpoint spacing (symbols)
 #define HOH_MAX_TILE_W 65535
 #define HOH_LZ_WINDOW 64          // -s0 seek distance 6 -> 1 << 6 pixels back (choh.cpp:125, lz.hpp:20)
 

@@ -15,7 +15,10 @@
 //  k_dunpred_lz: tiles with LZ copies, serial raster walk.
 #include "hoh_dec.h"
 #include <string.h>
+#include <stdlib.h>
 #include <algorithm>
+#include <vector>
+#include <stdio.h>
 
 #define DSEG HOH_SEG
 
@@ -35,6 +38,8 @@ struct DecJob {
   uint32_t cum_stride;          // entries per stream in cum (>= range + 1)
   uint32_t* matches;            // [tile][lz_cap+1][4]: pixel index, length, back, nuked before
   int lzband;                   // rows per band of k_dunpred_lz (LDS-bound)
+  uint32_t dbg;                 // measurement knobs (HOH_DEC_DBG), 0 in production
+  uint64_t* dbgbuf;             // per-workgroup s_memtime stamps when dbg & 16
   uint8_t* rgb;                 // output image
   uint32_t* gerr;
   const IndexStream* ix;        // optional side index
@@ -275,7 +280,10 @@ __device__ bool parse_stream(const DecJob& j, uint64_t& p, int sid, uint64_t out
   d.payload_off = p;
   d.words = (uint32_t)(data / 4);
   p += data;                                              // Q1 fix: skip the payload
-  if (lane == 0) j.streams[sid] = d;
+  if (lane == 0) {
+    j.streams[sid] = d;
+    if (j.gerr) atomicMax(j.gerr + 1, d.words);           // sizes the decoder's LDS payload stage
+  }
   return true;
 }
 
@@ -357,7 +365,7 @@ __device__ __forceinline__ uint32_t skew_pos(uint32_t x, uint32_t y, uint32_t w)
 // skewed-layout width of stream sid (0: flat).  Only complete planes (n == w*h, i.e. no LZ
 // nukes) are skewed; the single-stream decoder has no tiles.
 __device__ __forceinline__ uint32_t skew_w(const DecJob& j, int sid, uint32_t n) {
-  if (!j.tiles || sid % SK_PER_TILE < 3) return 0;
+  if (!j.tiles || sid % SK_PER_TILE < 3 || (j.dbg & 1)) return 0;
   const DecTile& t = j.tiles[sid / SK_PER_TILE];
   return n == (uint32_t)(t.w * t.h) ? (uint32_t)t.w : 0u;
 }
@@ -400,97 +408,110 @@ __device__ bool dec_run(const DecJob& j, const DecStream& d, const uint32_t* cum
   return true;
 }
 
-#define DR_BK 1024   // slot buckets per stream table
-#define DR_DB 16     // symbols per block (<= 8 payload words at pb <= 15)
-#define DR_RP 33     // LDS word-ring pitch per lane (32 words + 1 pad)
+#define DR_T 256      // threads per stream workgroup (lane = segment of HOH_SEG symbols)
+#define DR_BSH 5      // slot bucket = 32 slots
 
-// Payload words [k, k+8) of a stream whose word 0 is at byte `pay` (any alignment), in two
-// halves so the loads can be awaited a block later: issue() loads the 9 aligned dwords covering
-// them (addresses clamped to the last whole dword of the file, so no branch), finish() swaps in
-// the file's partial tail dword where the clamp applied and realigns.
-struct WordFetch {
-  uint64_t last;    // byte offset of the last whole dword of the file
-  uint32_t tail;    // bytes [size & ~3, size) as a dword (0 if none)
-  __device__ void init(const DecJob& j) {
-    last = j.size >= 4 ? (j.size & ~3ull) - 4 : 0;
-    tail = 0;
-    for (uint64_t q = j.size & ~3ull; q < j.size; q++) tail |= (uint32_t)j.in[q] << (8 * (q & 3));
-  }
-  __device__ __forceinline__ void issue(const DecJob& j, uint64_t pay, uint32_t k, uint32_t* raw) const {
-    const uint64_t base = (pay & ~3ull) + (uint64_t)k * 4;
-#pragma unroll
-    for (int q = 0; q < 9; q++) raw[q] = *(const uint32_t*)(j.in + min(base + (uint64_t)q * 4, last));
-  }
-  __device__ __forceinline__ void finish(uint64_t pay, uint32_t k, const uint32_t* raw, uint32_t* wv) const {
-    const uint32_t al = (uint32_t)(pay & 3);
-    const uint64_t base = (pay & ~3ull) + (uint64_t)k * 4;
-    uint32_t a[9];
-#pragma unroll
-    for (int q = 0; q < 9; q++) {
-      const uint64_t ad = base + (uint64_t)q * 4;
-      a[q] = ad <= last ? raw[q] : (ad == last + 4 ? tail : 0u);
-    }
-#pragma unroll
-    for (int q = 0; q < 8; q++) wv[q] = __builtin_amdgcn_alignbyte(a[q + 1], a[q], al);   // al = 0: a[q]
-  }
-};
-
-// Indexed decode: one workgroup (64 lanes) per stream, lane = 1024-symbol segment starting from
-// the encoder's checkpoint.  LDS holds the stream's cumulative table, a 1024-bucket table
-// (first symbol of each bucket + its packed start/frequency) and a 32-word payload ring per
-// lane.  Work proceeds in 16-symbol blocks: at a block boundary the lane lands the 8 words it
-// prefetched one block earlier, issues the stores of the previous block's symbols and the next
-// prefetch; inside a block the dependent chain touches LDS only.  (gfx9 counts loads and stores
-// on one vmcnt, so a load awaited right after a store would wait for the store: every global
-// access here is awaited one block after issue.)
-__global__ __launch_bounds__(64) void k_drans(DecJob j, int nstreams) {
-  __shared__ uint32_t cum_s[514];
-  __shared__ uint32_t cf_s[DR_BK];
-  __shared__ uint16_t sy_s[DR_BK];
-  __shared__ uint32_t ring[64 * DR_RP];
-  const int lane = threadIdx.x;
+// Indexed decode (rans64.hpp:107-142): one 256-thread workgroup per stream, thread = segment of
+// HOH_SEG symbols starting from the encoder's checkpoint.  LDS holds the cumulative table, an
+// exact slot -> symbol table (a byte per slot: the symbol's offset from the first symbol of its
+// 32-slot bucket, plus that first symbol per bucket) and the whole payload, so the per-symbol
+// chain is two LDS round trips and no global load; the symbol stores are never awaited.
+// Dynamic LDS: cum (514 u32) | bucket symbols (u16) | slot table (u8) | payload words | 4 rings.
+__global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams, uint32_t wcap) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t dr_lds[];
+  const int tid = threadIdx.x;
   const int sid = blockIdx.x;
   const DecStream d = j.streams[sid];
   if (d.mode != SM_RANS || d.range > 512) return;
-  for (uint32_t i = lane; i <= d.range; i += 64) cum_s[i] = j.cum[(size_t)sid * j.cum_stride + i];
-  const uint32_t bshift = d.pb > 10 ? d.pb - 10 : 0;
-  const uint32_t nbk = 1u << (d.pb - bshift);
+  uint64_t T0 = 0, T1 = 0;
+  if (j.dbg & 16) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(T0)::"memory");
+  const uint32_t pb = d.pb, M = 1u << pb, mask = M - 1, range = d.range;
+  const uint32_t bsh = pb < DR_BSH ? pb : DR_BSH;
+  uint32_t* cum_s = dr_lds;                                   // 514
+  uint16_t* sy_s = (uint16_t*)(dr_lds + 514);                 // nbk (<= 1024)
+  uint8_t* tb = (uint8_t*)(dr_lds + 514 + 512);               // M (<= 32768)
+  uint32_t* pw = dr_lds + 514 + 512 + 8192;                   // wcap words
+  __shared__ int wide;
+  if (tid == 0) wide = 0;
+  for (uint32_t i = tid; i <= range; i += DR_T) cum_s[i] = j.cum[(size_t)sid * j.cum_stride + i];
+  const bool staged = d.words <= wcap;
+  if (staged) {
+    const uint64_t last = j.size >= 4 ? (j.size & ~3ull) - 4 : 0;
+    uint32_t tail = 0;
+    for (uint64_t q = j.size & ~3ull; q < j.size; q++) tail |= (uint32_t)j.in[q] << (8 * (q & 3));
+    const uint32_t al = (uint32_t)(d.payload_off & 3);
+    const uint64_t base = d.payload_off & ~3ull;
+    // 8 words per thread in flight per round (the loads of a round are issued back to back)
+    for (uint32_t i0 = 0; i0 < d.words; i0 += DR_T * 8) {
+      uint32_t v0[8], v1[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint64_t a0 = min(base + (uint64_t)(i0 + k * DR_T + tid) * 4, last), a1 = min(a0 + 4, last);
+        v0[k] = *(const uint32_t*)(j.in + a0);
+        v1[k] = *(const uint32_t*)(j.in + a1);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint32_t i = i0 + k * DR_T + tid;
+        if (i < d.words) {
+          const uint64_t a0 = base + (uint64_t)i * 4, a1 = a0 + 4;
+          const uint32_t w0 = a0 <= last ? v0[k] : (a0 == last + 4 ? tail : 0u);
+          const uint32_t w1 = a1 <= last ? v1[k] : (a1 == last + 4 ? tail : 0u);
+          pw[i] = __builtin_amdgcn_alignbyte(w1, w0, al);
+        }
+      }
+    }
+  }
   __syncthreads();
-  for (uint32_t s = lane; s < d.range; s += 64) {          // bucket b starts inside symbol s's slots
-    const uint32_t c0 = cum_s[s], c1 = cum_s[s + 1];
-    if (c1 <= c0) continue;
-    const uint32_t b1 = (c1 - 1) >> bshift;
-    for (uint32_t b = (c0 + (1u << bshift) - 1) >> bshift; b <= b1 && b < nbk; b++) {
-      sy_s[b] = (uint16_t)s;
-      cf_s[b] = c0 | ((c1 - c0) << 16);
+  uint64_t Ta = 0;
+  if (j.dbg & 16) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(Ta)::"memory");
+  // slot table, one thread per 32-slot bucket: first symbol (binary search) then a walk
+  for (uint32_t b = tid; b < (M >> bsh); b += DR_T) {
+    const uint32_t slot0 = b << bsh;
+    uint32_t lo = 0, hi = range;                             // cum[lo] <= slot0 < cum[hi]
+    while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (cum_s[mid] <= slot0) lo = mid; else hi = mid; }
+    sy_s[b] = (uint16_t)lo;
+    uint32_t s = lo, cn = cum_s[lo + 1];
+    for (uint32_t k = 0; k < (1u << bsh); k++) {
+      while (cn <= slot0 + k && s + 1 < range) { s++; cn = cum_s[s + 1]; }
+      if (s - lo > 255) wide = 1;
+      tb[slot0 + k] = (uint8_t)(s - lo);
     }
   }
   __syncthreads();
   uint16_t* out = j.dsym + d.out_off;
   const uint32_t sw = skew_w(j, sid, d.n);
-  const uint32_t pb = d.pb, mask = (1u << pb) - 1, range = d.range;
-  if (d.ix < 0) {
-    // no index for this stream: serial on lane 0 from the file
-    if (lane == 0) {
+  if (d.ix < 0 || wide || !staged) {
+    // no index for this stream (or a table/payload that does not fit): serial on thread 0
+    if (tid == 0) {
       const uint64_t wend = d.payload_off + (uint64_t)d.words * 4;
       uint64_t x = (uint64_t)ld_u32_unaligned(j.in, d.payload_off) | ((uint64_t)ld_u32_unaligned(j.in, d.payload_off + 4) << 32);
       uint64_t xe;
-      if (!dec_run<false>(j, d, cum_s, sy_s, bshift, nullptr, x, d.payload_off + 8, wend, 0, d.n,
-                          OutCursor(out, sw, 0), &xe) || xe != (1ull << 31))
-        atomicOr(j.gerr, 4u);
+      bool ok;
+      if (d.ix < 0) {
+        ok = staged ? dec_run<true>(j, d, cum_s, sy_s, bsh, pw, x, 2, d.words, 0, d.n, OutCursor(out, sw, 0), &xe)
+                    : dec_run<false>(j, d, cum_s, sy_s, bsh, nullptr, x, d.payload_off + 8, wend, 0, d.n,
+                                     OutCursor(out, sw, 0), &xe);
+        if (!ok || xe != (1ull << 31)) atomicOr(j.gerr, 4u);
+        return;
+      }
     }
-    return;
+    if (d.ix < 0) return;
   }
+  if (j.dbg & 16) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(T1)::"memory");
+  if (j.dbg & 4) return;
   const IndexStream xs = j.ix[d.ix];
   const uint32_t nseg = (d.n + DSEG - 1) / DSEG;
-  uint32_t* myring = ring + lane * DR_RP;
-  WordFetch wf;
-  wf.init(j);
   bool bad = false;
-  for (uint32_t sg0 = 0; sg0 < nseg; sg0 += 64) {
-    const uint32_t sg = sg0 + lane;
+  const bool fast = staged && !wide;
+  // rows of HOH_SEG pixels: thread = row, wave = 64-row band, so the skewed layout's line
+  // (band, st) collects over 64 steps in an LDS ring and leaves as one coalesced 128-B store
+  const bool ringmode = fast && sw == DSEG;
+  uint16_t* ring = (uint16_t*)(pw + wcap) + (tid >> 6) * 4096;
+  for (uint32_t sg0 = 0; sg0 < nseg; sg0 += DR_T) {
+    const uint32_t sg = sg0 + tid;
     const bool act = sg < nseg;
-    uint64_t x = 0;
+    uint64_t x = 0, want = 1ull << 31;
     uint32_t wi = 0, s0 = 0, s1 = 0;
     if (act) {
       const Checkpoint c = j.ck[xs.ckpt_off + sg];
@@ -498,77 +519,60 @@ __global__ __launch_bounds__(64) void k_drans(DecJob j, int nstreams) {
       wi = c.widx - xs.widx_end;
       s0 = sg * DSEG;
       s1 = min(d.n, s0 + DSEG);
-    }
-    // initial fill: words [wi, wi+24)
-    uint32_t lw = wi;
-    for (int g = 0; g < 3; g++) {
-      uint32_t raw[9], wv[8];
-      wf.issue(j, d.payload_off, lw, raw);
-      wf.finish(d.payload_off, lw, raw, wv);
-#pragma unroll
-      for (int q = 0; q < 8; q++) myring[(lw + q) & 31] = wv[q];
-      lw += 8;
-    }
-    OutCursor oc(out, sw, s0);
-    uint32_t pend[9];                                  // raw dwords of the in-flight prefetch
-    bool haspend = false;
-    uint32_t pk = lw;                                  // its first word
-    uint32_t sym[DR_DB];
-    wf.issue(j, d.payload_off, pk, pend);
-    for (uint32_t blk = 0; blk <= DSEG / DR_DB; blk++) {
-      const uint32_t i0 = s0 + blk * DR_DB;
-      {                                                // land the prefetch issued one block ago
-        uint32_t wv[8];
-#pragma unroll
-        for (int q = 0; q < 9; q++) asm volatile("" ::"v"(pend[q]));   // the vmcnt wait lands here
-        wf.finish(d.payload_off, pk, pend, wv);
-        if (haspend) {
-#pragma unroll
-          for (int q = 0; q < 8; q++) myring[(lw + q) & 31] = wv[q];
-          lw += 8;
-        }
-      }
-      if (blk > 0 && act) {                            // stores of the previous block's symbols
-#pragma unroll
-        for (int k = 0; k < DR_DB; k++)
-          if (i0 - DR_DB + k < s1) oc.put(i0 - DR_DB + k, (uint16_t)sym[k]);
-      }
-      if (blk == DSEG / DR_DB) break;
-      haspend = act && lw + 8 <= wi + 32 && lw < d.words;
-      pk = lw;
-      wf.issue(j, d.payload_off, pk, pend);
-#pragma unroll
-      for (int k = 0; k < DR_DB; k++) {
-        const uint32_t i = i0 + k;
-        if (act && i < s1) {
-          const uint32_t nw = myring[wi & 31];
-          const uint32_t slot = (uint32_t)x & mask;
-          const uint32_t bk = slot >> bshift;
-          uint32_t cf = cf_s[bk];
-          uint32_t s = sy_s[bk];
-          uint32_t c = cf & 0xffffu, f = cf >> 16;
-          if (slot - c >= f) {                        // slot past the bucket's first symbol
-            while (s + 1 < range && cum_s[s + 1] <= slot) s++;
-            c = cum_s[s];
-            f = cum_s[s + 1] - c;
-          }
-          sym[k] = s;
-          x = (uint64_t)f * (x >> pb) + (slot - c);   // Rans64DecAdvance
-          if (x < (1ull << 31)) {
-            if (wi >= lw) bad = true;
-            x = (x << 32) | nw;
-            wi++;
-          }
-        }
-      }
-    }
-    if (act) {
-      uint64_t want = 1ull << 31;
       if (sg + 1 < nseg) { const Checkpoint c2 = j.ck[xs.ckpt_off + sg + 1]; want = (uint64_t)c2.xl | ((uint64_t)c2.xh << 32); }
+    }
+    if (ringmode) {
+      const uint32_t lane = tid & 63;
+      const uint32_t band = (sg0 >> 6) + (tid >> 6);
+      if (band * 64 >= nseg) continue;                      // whole wave past the last row
+      uint16_t* bo = out + (size_t)band * (DSEG + 63) * 64 + lane;
+      for (uint32_t xx = 0; xx < DSEG; xx++) {
+        if (act) {
+          const uint32_t nw = pw[min(wi, wcap - 1)];
+          const uint32_t slot = (uint32_t)x & mask;
+          const uint32_t sym = sy_s[slot >> bsh] + tb[slot];
+          const uint32_t cc = cum_s[sym], f = cum_s[sym + 1] - cc;
+          ring[((xx + lane) & 63) * 64 + lane] = (uint16_t)sym;
+          x = (uint64_t)f * (x >> pb) + (slot - cc);       // Rans64DecAdvance
+          if (x < (1ull << 31)) { x = (x << 32) | nw; wi++; }
+        }
+        bo[xx * 64] = ring[(xx & 63) * 64 + lane];          // line xx is complete (lane 0 wrote last)
+      }
+      for (uint32_t st = DSEG; st < DSEG + 63; st++) bo[st * 64] = ring[(st & 63) * 64 + lane];
+      if (act && (x != want || wi > d.words)) bad = true;
+      continue;
+    }
+    if (!act) continue;
+    if (fast) {
+      OutCursor oc(out, sw, s0);
+      for (uint32_t i = s0; i < s1; i++) {
+        const uint32_t nw = pw[min(wi, wcap - 1)];
+        const uint32_t slot = (uint32_t)x & mask;
+        const uint32_t sym = sy_s[slot >> bsh] + tb[slot];
+        const uint32_t cc = cum_s[sym], f = cum_s[sym + 1] - cc;
+        oc.put(i, (uint16_t)sym);
+        x = (uint64_t)f * (x >> pb) + (slot - cc);         // Rans64DecAdvance
+        if (x < (1ull << 31)) { x = (x << 32) | nw; wi++; }
+      }
       if (x != want || wi > d.words) bad = true;
+    } else {
+      const uint64_t wend = d.payload_off + (uint64_t)d.words * 4;
+      uint64_t xe;
+      const bool ok = staged ? dec_run<true>(j, d, cum_s, sy_s, bsh, pw, x, wi, d.words, s0, s1, OutCursor(out, sw, s0), &xe)
+                             : dec_run<false>(j, d, cum_s, sy_s, bsh, nullptr, x, d.payload_off + (uint64_t)wi * 4, wend,
+                                              s0, s1, OutCursor(out, sw, s0), &xe);
+      if (!ok || xe != want) bad = true;
     }
   }
   if (bad) atomicOr(j.gerr, 4u);
+  if ((j.dbg & 16) && tid == 0) {
+    uint64_t T2;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(T2)::"memory");
+    j.dbgbuf[sid * 4] = T1 - T0;
+    j.dbgbuf[sid * 4 + 1] = T2 - T1;
+    j.dbgbuf[sid * 4 + 2] = 1;
+    j.dbgbuf[sid * 4 + 3] = Ta - T0;
+  }
 }
 
 // Without an index: one lane per stream, tables from the parse kernel (512 buckets).
@@ -1002,6 +1006,17 @@ int decode_tiles_impl(hoh_ctx* c, const uint8_t* d_blob, size_t size, int W, int
 }
 
 static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s) {
+  {
+    const char* e = getenv("HOH_DEC_DBG");
+    j.dbg = e ? (uint32_t)atoi(e) : 0;
+  }
+  DecWork& w0 = ctx_dec(c);
+  if (j.dbg & 16) {
+    void* q;
+    if (dbuf(w0, 13, (size_t)j.ntiles * SK_PER_TILE * 32, &q)) return 3;
+    j.dbgbuf = (uint64_t*)q;
+    (void)hipMemsetAsync(q, 0, (size_t)j.ntiles * SK_PER_TILE * 32, s);
+  }
   j.npix_cap = (uint32_t)(((size_t)j.tw * j.th + 63) / 64 * 64);
   j.lz_cap = (uint32_t)((j.npix_cap / 4 + j.npix_cap / 255 + 16 + 7) / 8 * 8);
   {
@@ -1032,9 +1047,21 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   ctx_mark(c, s, "dtable", false);
   hipLaunchKernelGGL(k_dparse, dim3(j.ntiles), dim3(64), 0, s, j);
   ctx_mark(c, s, "dparse", false);
+  uint64_t* pin = ctx_pinned(c);
+  if (hipMemcpyAsync(pin, j.gerr, 8, hipMemcpyDeviceToHost, s) != hipSuccess) return 3;
+  if (hipStreamSynchronize(s) != hipSuccess) return 3;
+  {
+    const uint32_t ge = (uint32_t)pin[0];
+    if (ge & 2) return 6;
+    if (ge) return 7;
+  }
+  const uint32_t maxw = (uint32_t)(pin[0] >> 32);
   if (indexed) {
+    // payload stage sized to the largest stream when it fits next to the tables (<= 128 KB)
+    const size_t fixed = (514 + 512 + 8192) * 4 + 4 * 4096 * 2;   // tables + 4 output rings
+    const uint32_t wcap = (uint32_t)std::min<size_t>(std::max<uint32_t>(maxw, 1), (150 * 1024 - fixed) / 4);
     hipLaunchKernelGGL(k_dmatch, dim3((S + 255) / 256), dim3(256), 0, s, j, S);
-    hipLaunchKernelGGL(k_drans, dim3(S), dim3(64), 0, s, j, S);
+    hipLaunchKernelGGL(k_drans, dim3(S), dim3(DR_T), fixed + (size_t)wcap * 4, s, j, S, wcap);
   } else {
     hipLaunchKernelGGL(k_drans_serial, dim3((S + 63) / 64), dim3(64), 0, s, j, S);
   }
@@ -1048,7 +1075,15 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   hipLaunchKernelGGL(k_dunpred_serial, dim3(j.ntiles), dim3(192), 0, s, j);
   ctx_mark(c, s, "dunpred", false);
   if (hipGetLastError() != hipSuccess) return 3;
-  uint64_t* pin = ctx_pinned(c);
+  if (j.dbg & 16) {
+    std::vector<uint64_t> h((size_t)S * 4);
+    (void)hipMemcpyAsync(h.data(), j.dbgbuf, h.size() * 8, hipMemcpyDeviceToHost, s);
+    (void)hipStreamSynchronize(s);
+    double a = 0, b = 0, n = 0, st = 0;
+    for (int i = 0; i < S; i++) if (h[i * 4 + 2]) { a += h[i * 4]; b += h[i * 4 + 1]; st += h[i * 4 + 3]; n++; }
+    fprintf(stderr, "k_drans: %d rANS workgroups, avg setup %.0f (staging %.0f), decode %.0f s_memtime ticks\n", (int)n,
+            a / n, st / n, b / n);
+  }
   if (hipMemcpyAsync(pin, j.gerr, 8, hipMemcpyDeviceToHost, s) != hipSuccess) return 3;
   if (hipStreamSynchronize(s) != hipSuccess) return 3;
   const uint32_t ge = (uint32_t)pin[0];

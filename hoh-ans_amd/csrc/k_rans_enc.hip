@@ -123,22 +123,22 @@ __global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane) {
       if (b - 3 >= 0) s1 = sp4[b - 3];
 #pragma unroll
       for (int k = 7; k >= 0; --k) step15(c, eA[k]);
-      if ((b & 127) == 0) ckpt(c, ck, (uint32_t)b * 8 / HOH_SEG);
+      if ((b & (HOH_SEG / 8 - 1)) == 0) ckpt(c, ck, (uint32_t)b * 8 / HOH_SEG);
       lookup8(eA, s0, lds, lb);
       if (b - 4 >= 0) s0 = sp4[b - 4];
 #pragma unroll
       for (int k = 7; k >= 0; --k) step15(c, eB[k]);
-      if (((b - 1) & 127) == 0) ckpt(c, ck, (uint32_t)(b - 1) * 8 / HOH_SEG);
+      if (((b - 1) & (HOH_SEG / 8 - 1)) == 0) ckpt(c, ck, (uint32_t)(b - 1) * 8 / HOH_SEG);
       lookup8(eB, s1, lds, lb);
       if (b - 5 >= 0) s1 = sp4[b - 5];
 #pragma unroll
       for (int k = 7; k >= 0; --k) step15(c, eA[k]);
-      if (((b - 2) & 127) == 0) ckpt(c, ck, (uint32_t)(b - 2) * 8 / HOH_SEG);
+      if (((b - 2) & (HOH_SEG / 8 - 1)) == 0) ckpt(c, ck, (uint32_t)(b - 2) * 8 / HOH_SEG);
       if (b - 4 >= 0) lookup8(eA, s0, lds, lb);
       if (b - 6 >= 0) s0 = sp4[b - 6];
 #pragma unroll
       for (int k = 7; k >= 0; --k) step15(c, eB[k]);
-      if (((b - 3) & 127) == 0) ckpt(c, ck, (uint32_t)(b - 3) * 8 / HOH_SEG);
+      if (((b - 3) & (HOH_SEG / 8 - 1)) == 0) ckpt(c, ck, (uint32_t)(b - 3) * 8 / HOH_SEG);
       flush_win(c);
     }
   }
