@@ -262,6 +262,10 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   Prof prof(c, s);
   EncodeJob j;
   memset(&j, 0, sizeof(j));
+  {
+    const char* e = getenv("HOH_ENC_DBG");
+    j.dbg = e ? (uint32_t)atoi(e) : 0;
+  }
   j.rgb = d_rgb; j.W = W; j.H = H;
   j.xt = xt; j.yt = yt; j.tw = tw; j.th = th;
   j.t0 = t0; j.ntiles = ntiles;

@@ -113,6 +113,7 @@ struct EncodeJob {
   int t0, ntiles;         // tiles [t0, t0 + ntiles) of the image are coded
   uint32_t npix_cap;      // max pixels of one tile (per-plane stride of the residual arena)
   uint32_t lz_cap;        // symbols per LZ stream slot
+  uint32_t dbg;           // measurement knobs (HOH_ENC_DBG), 0 in production
   // arenas
   uint16_t* sym;          // residual planes + LZ symbols
   uint32_t* hist;         // [stream][512]

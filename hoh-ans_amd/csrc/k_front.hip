@@ -1,14 +1,23 @@
-// Encoder front end, one workgroup per 256x256 tile (choh.cpp:464-500 tiles are independent):
+// Encoder front end, one workgroup (4 waves) per 256x256 tile (choh.cpp:464-500 tiles are
+// independent), streaming the tile in raster blocks of 256 pixels:
 //  * subtract-green (channel.hpp:73-79) + MED fast-path residuals for the three planes
 //    (prediction.hpp:6-44), written to the residual arena, histograms in LDS;
 //  * grey test (channel.hpp:21-31) and distinct-colour count capped at 257 (choh.cpp:17-46);
-//  * LZ candidate detection for find_lz_rgb at -s0 (lz.hpp:32-53): a position is a candidate iff
-//    some back distance b in [1, 64] gives a run of >= 4 equal RGB pixels.  The greedy selection
-//    itself runs in k_lz.hip over the (sparse) candidate bitmap.
-// Rows stream through an LDS ring of packed pixels so that every pixel is read from HBM once.
+//  * LZ candidate detection for find_lz_rgb at -s0 (lz.hpp:32-53): a position q is a candidate
+//    iff some back distance b in [1, min(64, q)] gives 4 equal RGB pixels q..q+3 vs q-b..q-b+3.
+//    Every position gets a 32-bit fingerprint of its 4-pixel window.  Per block, an LDS hash
+//    table counts the fingerprints of positions [base - 64, base + 256); a position whose
+//    fingerprint occurs there more than once (its own occurrence) may have an equal window
+//    within 64 back, and only those positions are checked exactly (b = 1..64, first hit wins),
+//    so the candidate set is exact at one table probe per position.  The greedy selection runs
+//    in k_lz.hip over the (sparse) candidate bitmap.
+// Pixels live in an LDS ring (stored twice, so reads at q+k and q-d never wrap); every pixel is
+// read from HBM once, one block ahead of its use.
 #include "hoh_internal.h"
 
-#define RING 2048               // pixels; >= 4 rows of the widest tile (511) + 64
+#define RING 2048               // pixels: >= the 1024-pixel span [q - 512, q + 512) in use
+#define HRING 512               // fingerprints: >= the 320-position span [base - 64, base + 256)
+#define HTAB 1024               // fingerprint table slots (>= 3x the 320 keys of a block)
 #define NT 256
 
 __device__ __forceinline__ uint16_t med16(uint16_t a, uint16_t b, uint16_t c) {
@@ -22,42 +31,85 @@ __device__ __forceinline__ uint32_t plane_val(uint32_t px, int k) {
   return k == 0 ? g : k == 1 ? r - g + 256 : b - g + 256;
 }
 
+__device__ __forceinline__ uint32_t fp32(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  uint32_t h = a * 0x9E3779B1u;
+  h = (h ^ b) * 0x85EBCA77u;
+  h = (h ^ c) * 0xC2B2AE3Du;
+  h = (h ^ d) * 0x27D4EB2Fu;
+  return (h ^ (h >> 15)) | 1u;                     // never 0 (the empty-slot key)
+}
+
 __global__ __launch_bounds__(NT) void k_front(EncodeJob j) {
-  __shared__ uint32_t ring[RING];
-  __shared__ uint64_t mring[RING];
+  __shared__ uint32_t ring[2 * RING];
+  __shared__ uint32_t hring[HRING];
+  __shared__ uint32_t hkey[HTAB];
+  __shared__ uint32_t hcnt[HTAB];
   __shared__ uint32_t hist[3][512];
   __shared__ uint32_t hset[1024];
   __shared__ int s_ncol, s_notgrey, s_ncand;
 
-  const int t = blockIdx.x, tid = threadIdx.x;
+  const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const int gt = j.t0 + t;
   const int x0 = (gt % j.xt) * j.tw, y0 = (gt / j.xt) * j.th;
   const int w = min(j.tw, j.W - x0), h = min(j.th, j.H - y0);
+  const uint32_t npix = (uint32_t)w * h;
   for (int i = tid; i < 3 * 512; i += NT) (&hist[0][0])[i] = 0;
   for (int i = tid; i < 1024; i += NT) hset[i] = 0xffffffffu;
   if (tid == 0) { s_ncol = 0; s_notgrey = 0; s_ncand = 0; }
-  __syncthreads();
 
   uint16_t* res[3];
   for (int k = 0; k < 3; k++) res[k] = j.sym + (size_t)(t * 3 + k) * j.npix_cap;
   uint64_t* cand = j.candbits + (size_t)t * (j.npix_cap / 64);
-  uint32_t tested = 0;
-  int notgrey = 0, ncand = 0;
+  const uint8_t* img = j.rgb + ((size_t)y0 * j.W + x0) * 3;
+  const size_t pitch = (size_t)j.W * 3;
 
-  for (int y = 0; y < h; y++) {
-    const uint8_t* row = j.rgb + ((size_t)(y0 + y) * j.W + x0) * 3;
-    for (int x = tid; x < w; x += NT) {
-      uint32_t v = row[3 * x] | (row[3 * x + 1] << 8) | (row[3 * x + 2] << 16);
-      ring[(y * w + x) & (RING - 1)] = v;
+  // loader: this thread's pixel of block `blk` (raster position blk*256 + tid), (x, y) walked
+  // incrementally (w >= 256 for tiled images, so a block step wraps at most one row... or more
+  // for narrow edge tiles, hence the loop)
+  int lx = tid, ly = 0;
+  while (lx >= w) { lx -= w; ly++; }
+  auto load_px = [&](uint32_t q) -> uint32_t {
+    if (q >= npix) return 0;
+    const uint8_t* p = img + (size_t)ly * pitch + (size_t)lx * 3;
+    return p[0] | (p[1] << 8) | (p[2] << 16);
+  };
+  auto advance = [&]() { lx += NT; while (lx >= w) { lx -= w; ly++; } };
+  // block 0 into the ring, block 1 in flight
+  {
+    const uint32_t v0 = load_px(tid);
+    ring[tid & (RING - 1)] = v0;
+    ring[(tid & (RING - 1)) + RING] = v0;
+    advance();
+  }
+  uint32_t nextv = load_px(NT + tid);
+  advance();
+  __syncthreads();
+
+  int notgrey = 0, ncand = 0;
+  const uint32_t nblk = (npix + NT - 1) / NT;
+  for (uint32_t blk = 0; blk < nblk; blk++) {
+    const uint32_t base = blk * NT;
+    {   // land block blk+1, issue block blk+2
+      const uint32_t qn = base + NT + tid;
+      ring[qn & (RING - 1)] = nextv;
+      ring[(qn & (RING - 1)) + RING] = nextv;
+      nextv = load_px(base + 2 * NT + tid);
+      advance();
     }
     __syncthreads();
-    for (int x = tid; x < w; x += NT) {
-      const uint32_t q = (uint32_t)y * w + x;
-      const uint32_t v = ring[q & (RING - 1)];
+    const uint32_t q = base + tid;
+    const bool act = q < npix;
+    const uint32_t ri = q & (RING - 1);
+    const uint32_t* fwd = ring + ri;              // fwd[k] = pixel q + k
+    const uint32_t* bwd = ring + ri + RING;       // bwd[-d] = pixel q - d
+    const uint32_t v = fwd[0];
+    const bool win = q + 3 < npix;                 // a 4-pixel window starts here
+    uint32_t hq = 0;
+    if (act) {
+      const uint32_t x = q % (uint32_t)w, y = q / (uint32_t)w;
       const uint32_t pr = v & 255, pg = (v >> 8) & 255, pbb = v >> 16;
       notgrey |= (pr != pg) | (pr != pbb);
-      // distinct colours, stop inserting past 256
-      if (s_ncol <= 256) {
+      if (s_ncol <= 256 && !(j.dbg & 1)) {         // distinct colours, stop past 256
         uint32_t hsh = (v * 2654435761u) >> 22;
         for (int probe = 0; probe < 1024; probe++) {
           uint32_t old = atomicCAS(&hset[hsh], 0xffffffffu, v);
@@ -67,9 +119,9 @@ __global__ __launch_bounds__(NT) void k_front(EncodeJob j) {
         }
       }
       const bool hasL = x > 0, hasT = y > 0;
-      const uint32_t vL = hasL ? ring[(q - 1) & (RING - 1)] : 0;
-      const uint32_t vT = hasT ? ring[(q - w) & (RING - 1)] : 0;
-      const uint32_t vTL = (hasL && hasT) ? ring[(q - w - 1) & (RING - 1)] : 0;
+      const uint32_t vL = hasL ? bwd[-1] : 0;
+      const uint32_t vT = hasT ? bwd[-w] : 0;
+      const uint32_t vTL = (hasL && hasT) ? bwd[-w - 1] : 0;
 #pragma unroll
       for (int k = 0; k < 3; k++) {
         const int c = k ? 512 : 256, half = c / 2;
@@ -79,27 +131,53 @@ __global__ __launch_bounds__(NT) void k_front(EncodeJob j) {
         uint16_t p = med16(T, L, (uint16_t)(T + L - TL));
         uint32_t r = ((int)plane_val(v, k) - (int)p + half + c) & (c - 1);
         res[k][q] = (uint16_t)r;
-        atomicAdd(&hist[k][r], 1u);
+        if (!(j.dbg & 2)) atomicAdd(&hist[k][r], 1u);
       }
-      // LZ: bit b-1 set iff pixel q equals pixel q-b (lz.hpp:37-42)
-      uint64_t m = 0;
-      const uint32_t bmax = q < 64 ? q : 64;
-      for (uint32_t b = 1; b <= bmax; b++) m |= (uint64_t)(ring[(q - b) & (RING - 1)] == v) << (b - 1);
-      mring[q & (RING - 1)] = m;
+      if (win) hq = fp32(v, fwd[1], fwd[2], fwd[3]);
+    }
+    hring[q & (HRING - 1)] = hq;                    // 0: no window at q
+    for (int i = tid; i < HTAB; i += NT) { hkey[i] = 0; hcnt[i] = 0; }
+    __syncthreads();
+    // count the fingerprints of positions [base - 64, base + 256)
+    for (int i = tid; i < NT + 64; i += NT) {
+      const int p = (int)base - 64 + i;
+      if (p < 0) continue;
+      const uint32_t f = hring[p & (HRING - 1)];
+      if (!f) continue;
+      uint32_t sl = f & (HTAB - 1);
+      for (int probe = 0; probe < HTAB; probe++) {
+        const uint32_t old = atomicCAS(&hkey[sl], 0u, f);
+        if (old == 0u || old == f) { atomicAdd(&hcnt[sl], 1u); break; }
+        sl = (sl + 1) & (HTAB - 1);
+      }
     }
     __syncthreads();
-    // candidates: a run of 4 at one back distance starting at q (needs q + 3 < npix)
-    const uint32_t done = (uint32_t)(y + 1) * w;
-    const uint32_t hi = done >= 3 ? done - 3 : 0;
-    for (uint32_t q = tested + tid; q < hi; q += NT) {
-      uint64_t a = mring[q & (RING - 1)] & mring[(q + 1) & (RING - 1)] & mring[(q + 2) & (RING - 1)] &
-                   mring[(q + 3) & (RING - 1)];
-      if (a) {
-        atomicOr((unsigned long long*)&cand[q >> 6], 1ull << (q & 63));
-        ncand++;
+    bool hit = false;
+    if (win && !(j.dbg & 4)) {
+      uint32_t sl = hq & (HTAB - 1);
+      for (int probe = 0; probe < HTAB; probe++) {
+        const uint32_t k = hkey[sl];
+        if (k == hq) { hit = hcnt[sl] > 1; break; }
+        if (k == 0) break;
+        sl = (sl + 1) & (HTAB - 1);
       }
     }
-    if (hi > tested) tested = hi;
+    const uint64_t flag = __ballot(win && hit);
+    uint64_t word = 0;
+    if (flag) {
+      // exact check for the flagged lanes (lz.hpp:37-42 with offset < 4)
+      bool c = false;
+      if ((flag >> lane) & 1) {
+        const uint32_t bmax = q < 64 ? q : 64;
+        const uint32_t v1 = fwd[1], v2 = fwd[2], v3 = fwd[3];
+        for (uint32_t b = 1; b <= bmax && !c; b++)
+          if (hring[(q - b) & (HRING - 1)] == hq)
+            c = bwd[-(int)b] == v && bwd[1 - (int)b] == v1 && bwd[2 - (int)b] == v2 && bwd[3 - (int)b] == v3;
+      }
+      word = __ballot(c);
+    }
+    if (lane == 0 && (q >> 6) < (npix + 63) / 64) cand[q >> 6] = word;
+    ncand += lane == 0 ? __popcll(word) : 0;
   }
   if (notgrey) atomicOr(&s_notgrey, 1);
   if (ncand) atomicAdd(&s_ncand, ncand);

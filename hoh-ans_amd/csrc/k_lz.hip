@@ -98,33 +98,13 @@ __global__ __launch_bounds__(64) void k_lz(EncodeJob j) {
       prev_end = mpos + mt[3 * m + 1];
     }
   }
-  // --- nuke: compact the residual planes and fix their histograms
+  // --- nuked pixels (compaction of the residual planes runs in k_nuke)
   uint32_t nclean = npix;
   if (nmk && !overflow) {
-    for (uint32_t wi = lane; wi < nwords; wi += 64) bits[wi] = 0;
-    __syncthreads();
-    for (uint32_t m = 0; m < nmk; m++) {
-      const uint32_t a = mt[3 * m], e = a + mt[3 * m + 1];
-      for (uint32_t p = a + lane; p < e; p += 64) atomicOr((unsigned long long*)&bits[p >> 6], 1ull << (p & 63));
-    }
-    __syncthreads();
-    for (int k = 0; k < 3; k++) {
-      uint16_t* r = j.sym + (size_t)(t * 3 + k) * j.npix_cap;
-      uint32_t* hk = j.hist + (size_t)(t * SK_PER_TILE + SK_G + k) * 512;
-      uint32_t outc = 0;
-      for (uint32_t base = 0; base < npix; base += 64) {
-        const uint32_t p = base + lane;
-        const bool valid = p < npix;
-        const uint16_t v = valid ? r[p] : 0;
-        const bool nuked = valid && ((bits[base >> 6] >> lane) & 1);
-        if (nuked) atomicSub(&hk[v], 1u);
-        const uint64_t keep = __ballot(valid && !nuked);
-        const uint32_t dest = outc + __popcll(keep & ((1ull << lane) - 1));
-        if (valid && !nuked) r[dest] = v;
-        outc += __popcll(keep);
-      }
-      nclean = outc;
-    }
+    uint32_t nk = 0;
+    for (uint32_t m = lane; m < nmk; m += 64) nk += mt[3 * m + 1];
+    for (int o = 32; o > 0; o >>= 1) nk += __shfl_xor(nk, o);
+    nclean = npix - nk;
   }
   if (lane == 0) {
     if (overflow) ti.flags |= TF_OVERFLOW;
@@ -159,6 +139,56 @@ __global__ __launch_bounds__(64) void k_lz(EncodeJob j) {
   }
 }
 
+// Residual compaction of tiles with LZ copies (layer_encode.hpp:93-99): nuked pixels leave
+// the three residual planes (order kept) and their histograms.  One 256-thread workgroup per
+// tile; the nuke bitmap is built in LDS from the match list, then the plane is walked in
+// 256-pixel blocks with a block-wide rank of the kept pixels.
+__global__ __launch_bounds__(256) void k_nuke(EncodeJob j) {
+  extern __shared__ uint32_t nk_bits[];                  // npix_cap / 32 words
+  __shared__ uint32_t wsum[4];
+  const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const TileInfo ti = j.tiles[t];
+  const uint32_t nm = ti.nmatch;
+  if (nm == 0 || (ti.flags & TF_OVERFLOW) || nm > j.lz_cap) return;
+  const uint32_t npix = (uint32_t)ti.w * ti.h, nwords = (npix + 31) / 32;
+  const uint32_t* mt = j.matches + (size_t)t * 3 * (j.lz_cap + 1);
+  for (uint32_t i = tid; i < nwords; i += 256) nk_bits[i] = 0;
+  __syncthreads();
+  for (uint32_t m = 0; m < nm; m++) {
+    const uint32_t a = mt[3 * m], e = a + mt[3 * m + 1];
+    for (uint32_t p = a + tid; p < e; p += 256) atomicOr(&nk_bits[p >> 5], 1u << (p & 31));
+  }
+  __syncthreads();
+  for (int k = 0; k < 3; k++) {
+    uint16_t* r = j.sym + (size_t)(t * 3 + k) * j.npix_cap;
+    uint32_t* hk = j.hist + (size_t)(t * SK_PER_TILE + SK_G + k) * 512;
+    uint32_t outc = 0;
+    uint16_t vnext = tid < npix ? r[tid] : 0;
+    for (uint32_t base = 0; base < npix; base += 256) {
+      const uint32_t p = base + tid;
+      const bool valid = p < npix;
+      const uint16_t v = vnext;
+      if (base + 256 + tid < npix) vnext = r[base + 256 + tid];
+      const bool nuked = valid && ((nk_bits[p >> 5] >> (p & 31)) & 1);
+      if (nuked) atomicSub(&hk[v], 1u);
+      const bool keep = valid && !nuked;
+      const uint64_t bal = __ballot(keep);
+      if (lane == 0) wsum[wv] = (uint32_t)__popcll(bal);
+      __syncthreads();
+      uint32_t before = 0, tot = 0;
+      for (int q = 0; q < 4; q++) { const uint32_t c = wsum[q]; if (q < wv) before += c; tot += c; }
+      const uint32_t dest = outc + before + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+      __syncthreads();
+      // in place: dest <= p, and every block reads its values before any write of this pass
+      // reaches them (writes of block i land below block i's end)
+      if (keep) r[dest] = v;
+      outc += tot;
+    }
+    __syncthreads();
+  }
+}
+
 void launch_lz(const EncodeJob& j, hipStream_t s) {
   hipLaunchKernelGGL(k_lz, dim3(j.ntiles), dim3(64), 0, s, j);
+  hipLaunchKernelGGL(k_nuke, dim3(j.ntiles), dim3(256), (size_t)(j.npix_cap / 32 + 1) * 4, s, j);
 }

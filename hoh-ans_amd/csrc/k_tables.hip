@@ -48,8 +48,9 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 }
 
 __global__ __launch_bounds__(64) void k_tables(EncodeJob j) {
-  __shared__ uint32_t fr[MAXR];
-  __shared__ uint32_t cum[MAXR + 1];
+  extern __shared__ uint32_t tb_lds[];             // fr[gen_stride] | cum[gen_stride + 1]
+  uint32_t* fr = tb_lds;
+  uint32_t* cum = tb_lds + j.gen_stride;
   __shared__ uint32_t s_err;
   const int s = blockIdx.x, lane = threadIdx.x;
   StreamInfo st = j.streams[s];
@@ -239,5 +240,7 @@ __global__ __launch_bounds__(64) void k_tables(EncodeJob j) {
 }
 
 void launch_tables(const EncodeJob& j, int nstreams, hipStream_t s) {
-  hipLaunchKernelGGL(k_tables, dim3(nstreams), dim3(64), 0, s, j);
+  // LDS sized to the job's largest alphabet (512 for images): many streams per CU at once, so
+  // the serial header writer of each runs concurrently with the others
+  hipLaunchKernelGGL(k_tables, dim3(nstreams), dim3(64), (size_t)(2 * j.gen_stride + 1) * 4, s, j);
 }
