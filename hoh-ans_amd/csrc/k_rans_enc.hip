@@ -3,9 +3,10 @@
 // Bit-exactness forces one serial coder state per stream (the reference never interleaves), so
 // the encoder is a latency-bound chain of 65,536 dependent steps per 256x256 tile plane.  The
 // fast kernel therefore spends all its effort on the length of that chain:
-//  * 12 streams per wave, one wave per CU (256 CUs x 12 = 3,072 = the planes of an 8192^2 image);
-//  * per-stream symbol tables staged in LDS, interleaved (symbol*16 + lane)*16 B so that one
-//    v_perm_b32 turns a packed u16 symbol into its LDS address;
+//  * one stream per lane, RF_LANES streams per wave; the symbol tables (16-B entries: 1/f as
+//    f64, f, c) are gathered from global memory (L2-resident, ~8 KB per stream) one 8-symbol
+//    block ahead, so the kernel needs only its 8-KB output window in LDS and leaves the CUs
+//    free for concurrent work;
 //  * the quotient floor(x/f) of the reciprocal step is computed exactly with two f64
 //    multiplications by 1/f rounded up two ulps (the high word first, then remainder*2^32 +
 //    low word, both < 2^53: exact floors), which is mathematically identical to the Alverson
@@ -18,17 +19,14 @@
 // are unaffected).
 #include "hoh_internal.h"
 
-#define LANES 12
-#define TAB_BYTES (HOH_FAST_RANGE * 16 * 16)
 #define WIN 32
 
 __device__ __forceinline__ uint32_t plane_sid(int pi) { return (pi / 3) * SK_PER_TILE + SK_G + pi % 3; }
 
-__device__ __forceinline__ void lookup8(EncFast* e, uint4 sy, const unsigned char* lds, uint32_t lb) {
+__device__ __forceinline__ void lookup8(EncFast* e, uint4 sy, const EncFast* tab) {
   const uint32_t w[4] = {sy.x, sy.y, sy.z, sy.w};
 #pragma unroll
-  for (int k = 0; k < 8; ++k)
-    e[k] = *(const EncFast*)(lds + __builtin_amdgcn_perm(w[k >> 1], lb, (k & 1) ? 0x0C070600u : 0x0C050400u));
+  for (int k = 0; k < 8; ++k) e[k] = tab[(k & 1) ? (w[k >> 1] >> 16) : (w[k >> 1] & 0xffffu)];
 }
 
 struct Coder {
@@ -57,10 +55,14 @@ __device__ __forceinline__ void step15(Coder& c, const EncFast& e) {
   const bool emit = (c.xh >> 16) >= f;
   const uint32_t nh = emit ? 0u : c.xh;
   const uint32_t nl = emit ? c.xh : c.xl;
-  const uint32_t qh = (uint32_t)((double)nh * e.inv);
-  const uint32_t rh = nh - qh * f;
-  const double nd = fma((double)rh, 4294967296.0, (double)nl);
-  const uint32_t ql = (uint32_t)(nd * e.inv);
+  // all intermediate values are integers < 2^53, so every f64 operation below is exact; the
+  // remainder stays in f64 (no int round trip on the dependent chain)
+  const double nhd = (double)nh;
+  const double qhd = __builtin_trunc(nhd * e.inv);                 // floor(nh / f)
+  const double rhd = fma(-qhd, (double)f, nhd);                    // nh - qh*f
+  const double nd = fma(rhd, 4294967296.0, (double)nl);
+  const uint32_t ql = (uint32_t)(nd * e.inv);                      // floor(n / f)
+  const uint32_t qh = (uint32_t)qhd;
   c.xl = nl + e.c + ql * (32768u - f);
   c.xh = __builtin_amdgcn_alignbit(qh, ql, 17);
   c.mask = (c.mask << 1) | (emit ? 1u : 0u);
@@ -73,40 +75,29 @@ __device__ __forceinline__ void ckpt(const Coder& c, Checkpoint* ck, uint32_t k)
   ck[k] = p;
 }
 
+template <int LANES>
 __global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int lane = threadIdx.x;
-  const int pi0 = blockIdx.x * LANES;
-  for (int i = lane; i < HOH_FAST_RANGE * 16; i += 64) {
-    const int l = i & 15, sy = i >> 4;
-    EncFast v;
-    v.inv = 1.0; v.f = 1; v.c = 0;
-    if (l < LANES && pi0 + l < nplane) {
-      const uint32_t sid = plane_sid(pi0 + l);
-      if (j.streams[sid].fast) v = j.tab_fast[(size_t)sid * HOH_FAST_RANGE + sy];
-    }
-    ((EncFast*)lds)[i] = v;
-  }
-  __syncthreads();
-  const int pi = pi0 + lane;
+  const int pi = blockIdx.x * LANES + lane;
   if (lane >= LANES || pi >= nplane) return;
   const uint32_t sid = plane_sid(pi);
   StreamInfo st = j.streams[sid];
   if (!st.fast || st.mode != SM_RANS || st.err || st.n == 0) return;
   const uint32_t n = st.n;
+  const EncFast* tab = j.tab_fast + (size_t)sid * HOH_FAST_RANGE;
   Coder c;
   c.xh = 0; c.xl = 1u << 31; c.mask = 0; c.slot = 0;
   c.slab = j.slabs + st.slab_off;
   c.widx = st.slab_cap;
-  c.win = (uint32_t*)(lds + TAB_BYTES + lane * WIN * 4);
+  c.win = (uint32_t*)(lds + lane * WIN * 4);
   Checkpoint* ck = j.ckpt + st.ckpt_off;
-  const uint32_t lb = lane * 16;
   const uint16_t* sp = j.sym + st.sym_off;
   // prologue: the top n % 32 symbols one at a time (descending); the rest is whole windows
   const uint32_t r = n & 31, nb = (n - r) / 8;   // nb 8-symbol blocks, a multiple of 4
   for (uint32_t i = n; i > n - r; i--) {
     const uint32_t s = sp[i - 1];
-    const EncFast e = *(const EncFast*)(lds + ((s << 8) | lb));
+    const EncFast e = tab[s];
     step15(c, e);
   }
   flush_win(c);
@@ -116,25 +107,25 @@ __global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane) {
     EncFast eA[8], eB[8];
     uint4 s1 = sp4[nb - 2];
     uint4 s0 = sp4[nb - 3];
-    lookup8(eA, sp4[nb - 1], lds, lb);
+    lookup8(eA, sp4[nb - 1], tab);
     for (int b = (int)nb - 1; b >= 3; b -= 4) {
       // entering: eA = entries of block b, s1 = symbols of b-1, s0 = symbols of b-2
-      lookup8(eB, s1, lds, lb);
+      lookup8(eB, s1, tab);
       if (b - 3 >= 0) s1 = sp4[b - 3];
 #pragma unroll
       for (int k = 7; k >= 0; --k) step15(c, eA[k]);
       if ((b & (HOH_SEG / 8 - 1)) == 0) ckpt(c, ck, (uint32_t)b * 8 / HOH_SEG);
-      lookup8(eA, s0, lds, lb);
+      lookup8(eA, s0, tab);
       if (b - 4 >= 0) s0 = sp4[b - 4];
 #pragma unroll
       for (int k = 7; k >= 0; --k) step15(c, eB[k]);
       if (((b - 1) & (HOH_SEG / 8 - 1)) == 0) ckpt(c, ck, (uint32_t)(b - 1) * 8 / HOH_SEG);
-      lookup8(eB, s1, lds, lb);
+      lookup8(eB, s1, tab);
       if (b - 5 >= 0) s1 = sp4[b - 5];
 #pragma unroll
       for (int k = 7; k >= 0; --k) step15(c, eA[k]);
       if (((b - 2) & (HOH_SEG / 8 - 1)) == 0) ckpt(c, ck, (uint32_t)(b - 2) * 8 / HOH_SEG);
-      if (b - 4 >= 0) lookup8(eA, s0, lds, lb);
+      if (b - 4 >= 0) lookup8(eA, s0, tab);
       if (b - 6 >= 0) s0 = sp4[b - 6];
 #pragma unroll
       for (int k = 7; k >= 0; --k) step15(c, eB[k]);
@@ -186,8 +177,16 @@ __global__ __launch_bounds__(64) void k_rans_gen(EncodeJob j, int nstreams) {
 }
 
 void launch_rans_fast(const EncodeJob& j, const uint32_t*, int nplane, hipStream_t s) {
-  const int grid = (nplane + LANES - 1) / LANES;
-  hipLaunchKernelGGL(k_rans_fast, dim3(grid), dim3(64), TAB_BYTES + 16 * WIN * 4, s, j, nplane);
+  const int lanes = (j.dbg >> 8) & 127 ? (j.dbg >> 8) & 127 : 64;     // measurement knob
+  if (lanes == 16) {
+    hipLaunchKernelGGL(k_rans_fast<16>, dim3((nplane + 15) / 16), dim3(64), 16 * WIN * 4, s, j, nplane);
+  } else if (lanes == 32) {
+    hipLaunchKernelGGL(k_rans_fast<32>, dim3((nplane + 31) / 32), dim3(64), 32 * WIN * 4, s, j, nplane);
+  } else if (lanes == 8) {
+    hipLaunchKernelGGL(k_rans_fast<8>, dim3((nplane + 7) / 8), dim3(64), 8 * WIN * 4, s, j, nplane);
+  } else {
+    hipLaunchKernelGGL(k_rans_fast<64>, dim3((nplane + 63) / 64), dim3(64), 64 * WIN * 4, s, j, nplane);
+  }
 }
 
 void launch_rans_gen(const EncodeJob& j, int nstreams, hipStream_t s) {
