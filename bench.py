@@ -37,6 +37,7 @@ import os
 import subprocess
 import sys
 import tempfile
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -127,6 +128,8 @@ def main():
     ap.add_argument("--cpu-tiles", type=int, default=512)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-index", action="store_true", help="decode without the side index (serial rANS)")
+    ap.add_argument("--inflight", type=int, default=4,
+                    help="images in flight per GPU (each with its own context/stream); 1 = one at a time")
     args = ap.parse_args()
 
     import numpy as np
@@ -147,8 +150,6 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     L = hoh_ans.lib()
-    ctx = hoh_ans.Context(local)
-    index = None if args.no_index else hoh_ans.Index()
     W = args.size
     H = args.size * world
     if world == 1:
@@ -156,56 +157,94 @@ def main():
     else:
         t0, nt, y0, y1 = hd.shard(W, H, rank, world)
     rows = y1 - y0
-    rgb = hoh_ans.synth_rgb_dev(W, rows, args.seed, args.noise, ctx=ctx, row0=y0)
-    out = torch.empty(L.hoh_encode_bound(W, rows), dtype=torch.uint8, device=dev)
-    dec = torch.empty(W * rows * 3, dtype=torch.uint8, device=dev)
-    sizes_dev = torch.empty(max(nt, 1), dtype=torch.int32, device=dev)
-    gather = hd.FileGather(W, H, dev) if world > 1 else None
-    t_enc = t_dec = 0.0
-    state = {}
+    D = max(1, args.inflight)
+    rgb = hoh_ans.synth_rgb_dev(W, rows, args.seed, args.noise, row0=y0)
+    torch.cuda.synchronize()
 
-    def step():
-        nonlocal t_enc, t_dec
-        ta = time.perf_counter()
-        if world == 1:
-            _, n, _ = hoh_ans.encode_image(rgb, W, H, out_dev=out, ctx=ctx, index=index)
-            tb = time.perf_counter()
-            hoh_ans.decode_image(out, n, out_dev=dec, ctx=ctx, index=index)
-            state["n"] = n
-        else:
-            n = hoh_ans.encode_tiles(rgb, W, H, t0, nt, out, sizes_dev, ctx=ctx, index=index, row0=y0)
-            ts = sizes_dev[:nt].cpu().numpy().astype(np.uint32)
-            f, total = gather(out, n, ts)
-            tb = time.perf_counter()
-            hoh_ans.decode_tiles(out, n, W, H, t0, ts, dec, ctx=ctx, index=index, row0=y0)
-            state["n"] = n
-            state["total"] = total
-        torch.cuda.current_stream().synchronize()
-        tc = time.perf_counter()
-        t_enc += tb - ta
-        t_dec += tc - tb
+    class Lane:
+        """One in-flight image slot: its own library context (HIP stream + workspaces), torch
+        stream, buffers, side index and (N > 1) process group for the gather."""
 
-    ctx.profiling(True)
-    for _ in range(args.warmup):
-        step()
-    ctx.reset_stats()
-    t_enc = t_dec = 0.0
+        def __init__(self, k):
+            self.ctx = hoh_ans.Context(local)
+            self.stream = torch.cuda.Stream(device=dev)
+            self.index = None if args.no_index else hoh_ans.Index()
+            self.out = torch.empty(L.hoh_encode_bound(W, rows), dtype=torch.uint8, device=dev)
+            self.dec = torch.empty(W * rows * 3, dtype=torch.uint8, device=dev)
+            self.sizes = torch.empty(max(nt, 1), dtype=torch.int32, device=dev)
+            self.group = dist.new_group(list(range(world))) if world > 1 else None
+            self.gather = hd.FileGather(W, H, dev, group=self.group) if world > 1 else None
+            self.t_enc = self.t_dec = 0.0
+            self.n = 0
+
+        def step(self):
+            with torch.cuda.stream(self.stream):
+                ta = time.perf_counter()
+                if world == 1:
+                    _, n, _ = hoh_ans.encode_image(rgb, W, H, out_dev=self.out, ctx=self.ctx, index=self.index)
+                    tb = time.perf_counter()
+                    hoh_ans.decode_image(self.out, n, out_dev=self.dec, ctx=self.ctx, index=self.index)
+                else:
+                    n = hoh_ans.encode_tiles(rgb, W, H, t0, nt, self.out, self.sizes, ctx=self.ctx,
+                                             index=self.index, row0=y0)
+                    ts = self.sizes[:nt].cpu().numpy().astype(np.uint32)
+                    self.gather(self.out, n, ts)
+                    tb = time.perf_counter()
+                    hoh_ans.decode_tiles(self.out, n, W, H, t0, ts, self.dec, ctx=self.ctx, index=self.index,
+                                         row0=y0)
+                self.stream.synchronize()
+                tc = time.perf_counter()
+            self.n = n
+            self.t_enc += tb - ta
+            self.t_dec += tc - tb
+
+        def run(self, count):
+            for _ in range(count):
+                self.step()
+
+    lanes = [Lane(k) for k in range(D)]
+
+    def run_all(total):
+        # steps are dealt round-robin to the lanes; each lane runs its share back to back
+        shares = [total // D + (1 if k < total % D else 0) for k in range(D)]
+        if D == 1:
+            lanes[0].run(shares[0])
+            return
+        th = [threading.Thread(target=ln.run, args=(c,)) for ln, c in zip(lanes, shares)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+
+    for ln in lanes:
+        ln.ctx.profiling(True)
+    run_all(max(args.warmup, D))
+    for ln in lanes:
+        ln.ctx.reset_stats()
+        ln.t_enc = ln.t_dec = 0.0
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    run_all(args.steps)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t
-    stats = ctx.kernel_stats()
-    ctx.profiling(False)
+    stats = {}
+    for ln in lanes:
+        for k, (tot, cnt) in ln.ctx.kernel_stats().items():
+            a0, c0 = stats.get(k, (0.0, 0))
+            stats[k] = (a0 + tot, c0 + cnt)
+        ln.ctx.profiling(False)
+    t_enc = sum(ln.t_enc for ln in lanes)
+    t_dec = sum(ln.t_dec for ln in lanes)
 
     # checks outside the timed region
-    lossless = bool(torch.equal(dec, rgb))
-    n = state["n"]
+    lossless = all(bool(torch.equal(ln.dec, rgb)) for ln in lanes)
+    n = lanes[0].n
+    out = lanes[0].out
+    index = lanes[0].index
     sha = None
     if world == 1:
         sha = hashlib.sha256(out[:n].cpu().numpy().tobytes()).hexdigest()
@@ -254,16 +293,17 @@ def main():
             "data": "synthetic",
             "config": {
                 "workload": ("%dx%d synthetic RGB (gradient + triangular noise k=%d, seed %d), 256x256 tiles, "
-                             "choh -s0 encode + dhoh decode, %s" % (W, H, args.noise, args.seed,
-                                                                   "side index" if index else "serial decode")),
+                             "choh -s0 encode + dhoh decode, %s, %d image(s) in flight"
+                             % (W, H, args.noise, args.seed, "side index" if index else "serial decode", D)),
                 "W": W, "H": H, "tiles": (W // 256) * (H // 256), "per_gpu": "%dx%d" % (W, rows),
                 "parallelism": "tile rows sharded over %d GPU(s), RCCL gather to rank 0" % world
                                if world > 1 else "1 GPU",
             },
             "roofline": roof,
             "detail": {
-                "enc_MBps": round(raw_total * K / t_enc / 1e6, 2),
-                "dec_MBps": round(raw_total * K / t_dec / 1e6, 2),
+                "inflight": D,
+                "latency_ms_enc": round(t_enc / K * 1e3, 3),
+                "latency_ms_dec": round(t_dec / K * 1e3, 3),
                 "compressed_bytes": comp_total,
                 "ratio": round(ratio, 5),
                 "lossless": lossless,
