@@ -106,7 +106,7 @@ __global__ __launch_bounds__(64) void k_tables(EncodeJob j) {
   const uint32_t target = 1u << pb;
   for (uint32_t i = 1 + lane; i <= range; i += 64) cum[i] = (uint32_t)(((uint64_t)target * cum[i]) / total);
   __syncthreads();
-  for (uint32_t base = 0; base < range; base += 64) {
+  for (uint32_t base = 0; base < ((j.dbg & 64) ? 0u : range); base += 64) {
     const uint32_t i0 = base + lane;
     uint64_t zm = __ballot(i0 < range && fr[i0] && cum[i0 + 1] == cum[i0]);
     while (zm) {
@@ -169,69 +169,132 @@ __global__ __launch_bounds__(64) void k_tables(EncodeJob j) {
       j.tab_gen[(size_t)s * j.gen_stride + i] = g;
     }
   }
-  if (lane != 0) return;
-  // ---- header + table bytes (entropy_encoding.hpp:43-200), lane 0
+  // ---- header + table bytes (entropy_encoding.hpp:43-200).  Lane 0 runs the clamp scans
+  // (they stop at the first frequency needing prob_bits bits, so they are short); the fields are
+  // then written by the whole wave when every value fits its field (the stuffer's unmasked
+  // overflow cannot occur), else by lane 0 with the exact serial stuffer.
+  __shared__ uint16_t s_lower[16], s_upper[16];
+  __shared__ uint32_t s_mode;
   const uint32_t maxbits = hoh_bitlen(range - 1);
   const uint64_t expected_stored = vlen + 1 + ((uint64_t)maxbits * n + 8 - 1) / 8;
   const uint64_t expected_raw = ((uint64_t)pb * range + 8 - 1) / 8;
   const uint32_t cn32 = (pb - 1) / 4 + 2;
-  uint64_t exp_cl = (uint64_t)(uint32_t)((uint32_t)(2 * ((int)maxbits - 1)) * cn32);
-  exp_cl += (uint64_t)(uint32_t)(pb * 2);
   const uint32_t cn = (uint8_t)cn32;
-  uint16_t lower[16], upper[16];
-  uint64_t size_bits = 0, climb = 0, lci = 0;
-  for (; climb < range; climb++) {
-    while ((uint64_t)fr[climb] >= (uint64_t)(1u << size_bits)) {
-      uint64_t idx;
-      if (size_bits == 0) { size_bits = 1; idx = 0; lci = 1; }
-      else if (size_bits == 1) { size_bits = 4; idx = 1; lci = 2; }
-      else { idx = size_bits / 4 + 1; size_bits += 4; lci++; }
-      if (idx < cn && idx < 16) lower[idx] = (uint16_t)climb;    // overrun write dropped (see oracle)
+  if (lane == 0) {
+    uint64_t exp_cl = (uint64_t)(uint32_t)((uint32_t)(2 * ((int)maxbits - 1)) * cn32);
+    exp_cl += (uint64_t)(uint32_t)(pb * 2);
+    uint16_t lower[16], upper[16];
+    for (int i = 0; i < 16; i++) { lower[i] = 0; upper[i] = 0; }
+    uint64_t size_bits = 0, climb = 0, lci = 0;
+    for (; climb < range; climb++) {
+      while ((uint64_t)fr[climb] >= (uint64_t)(1u << size_bits)) {
+        uint64_t idx;
+        if (size_bits == 0) { size_bits = 1; idx = 0; lci = 1; }
+        else if (size_bits == 1) { size_bits = 4; idx = 1; lci = 2; }
+        else { idx = size_bits / 4 + 1; size_bits += 4; lci++; }
+        if (idx < cn && idx < 16) lower[idx] = (uint16_t)climb;    // overrun write dropped (see oracle)
+      }
+      if (size_bits >= pb) { size_bits = pb; exp_cl += size_bits; break; }
+      exp_cl += size_bits;
     }
-    if (size_bits >= pb) { size_bits = pb; exp_cl += size_bits; break; }
-    exp_cl += size_bits;
-  }
-  while (lci < cn && lci < 16) lower[lci++] = (uint16_t)(range - 1);
-  size_bits = 0;
-  uint64_t climb2 = range - 1, uci = 0;
-  for (;; climb2--) {
-    while ((uint64_t)fr[climb2] >= (uint64_t)(1u << size_bits)) {
-      uint64_t idx;
-      if (size_bits == 0) { size_bits = 1; idx = 0; uci = 1; }
-      else if (size_bits == 1) { size_bits = 4; idx = 1; uci = 2; }
-      else { idx = size_bits / 4 + 1; size_bits += 4; uci++; }
-      if (idx < cn && idx < 16) upper[idx] = (uint16_t)climb2;
+    while (lci < cn && lci < 16) lower[lci++] = (uint16_t)(range - 1);
+    size_bits = 0;
+    uint64_t climb2 = range - 1, uci = 0;
+    for (;; climb2--) {
+      while ((uint64_t)fr[climb2] >= (uint64_t)(1u << size_bits)) {
+        uint64_t idx;
+        if (size_bits == 0) { size_bits = 1; idx = 0; uci = 1; }
+        else if (size_bits == 1) { size_bits = 4; idx = 1; uci = 2; }
+        else { idx = size_bits / 4 + 1; size_bits += 4; uci++; }
+        if (idx < cn && idx < 16) upper[idx] = (uint16_t)climb2;
+      }
+      if (size_bits >= pb) { size_bits = pb; exp_cl += size_bits; break; }
+      exp_cl += size_bits;
+      if (climb2 == 0) break;
     }
-    if (size_bits >= pb) { size_bits = pb; exp_cl += size_bits; break; }
-    exp_cl += size_bits;
-    if (climb2 == 0) break;
+    while (uci < cn && uci < 16) upper[uci++] = 0;
+    exp_cl += size_bits * (climb2 - climb - 1);                          // size_t wrap (Q5)
+    exp_cl = (exp_cl + 8 - 1) / 8;
+    const bool raw = expected_raw < exp_cl;
+    hd[vlen] = (uint8_t)((1u << 7) + (pb << 2) + (raw ? 1 : 2));
+    for (int i = 0; i < 16; i++) { s_lower[i] = lower[i]; s_upper[i] = upper[i]; }
+    s_mode = raw ? 1 : 2;
   }
-  while (uci < cn && uci < 16) upper[uci++] = 0;
-  exp_cl += size_bits * (climb2 - climb - 1);                          // size_t wrap (Q5)
-  exp_cl = (exp_cl + 8 - 1) / 8;
-  Sink sk{hd, vlen, 0, 8};
-  if (expected_raw < exp_cl) {
-    hd[sk.loc++] = (uint8_t)((1u << 7) + (pb << 2) + 1);
-    for (uint32_t i = 0; i < range; i++) stuff(sk, fr[i], maxbits);
+  __syncthreads();
+  const bool raw = s_mode == 1;
+  auto sbits = [&](uint32_t i) -> uint32_t {                           // entropy_encoding.hpp:176-190
+    uint32_t sb = 0;
+    if (s_lower[0] <= i && s_upper[0] >= i) sb = 1;
+    if (s_lower[1] <= i && s_upper[1] >= i) sb = 4;
+    for (uint32_t jj = 2; jj < cn && jj < 16; jj++)
+      if (s_lower[jj] <= i && s_upper[jj] >= i) sb = 4 * jj;
+    return sb > pb ? pb : sb;
+  };
+  const uint32_t chunk2 = (range + 63) / 64;
+  const uint32_t d0 = lane * chunk2, d1 = min(range, d0 + chunk2);
+  bool fits = !raw;
+  uint32_t mybits = 0;
+  if (!raw)
+    for (uint32_t i = d0; i < d1; i++) {
+      const uint32_t sb = sbits(i);
+      if (fr[i] >> sb) fits = false;
+      mybits += sb;
+    }
+  uint32_t loc;
+  if (__ballot(!fits) == 0 && !(j.dbg & 128)) {
+    // parallel writer: fields MSB-first into an LDS bit buffer (cum is free now), then copied
+    uint32_t* bb = cum;
+    const uint32_t head = 2 * cn * maxbits;
+    uint32_t incl = mybits;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(incl, o);
+      if (lane >= o) incl += u;
+    }
+    const uint32_t total = head + __shfl(incl, 63);
+    const uint32_t nbytes = (total + 7) / 8;
+    for (uint32_t w = lane; w < (nbytes + 3) / 4; w += 64) bb[w] = 0;
+    __syncthreads();
+    auto put = [&](uint32_t pos, uint32_t v, uint32_t nb) {
+      if (!nb || !v) return;
+      const uint32_t off = pos & 7;
+      const uint32_t al = v << (32 - off - nb);                       // big-endian window at byte pos/8
+      for (uint32_t k = 0; k < 4; k++) {
+        const uint32_t byte = (al >> (24 - 8 * k)) & 255u;
+        if (byte) {
+          const uint32_t bi = (pos >> 3) + k;
+          atomicOr(&bb[bi >> 2], byte << (8 * (bi & 3)));
+        }
+      }
+    };
+    if (lane < 2 * (int)cn) put((uint32_t)lane * maxbits, (lane & 1) ? s_upper[lane >> 1] : s_lower[lane >> 1], maxbits);
+    uint32_t pos = head + incl - mybits;
+    for (uint32_t i = d0; i < d1; i++) {
+      const uint32_t sb = sbits(i);
+      put(pos, fr[i], sb);
+      pos += sb;
+    }
+    __syncthreads();
+    const uint8_t* bs = (const uint8_t*)bb;
+    for (uint32_t k = lane; k < nbytes; k += 64) hd[vlen + 1 + k] = bs[k];
+    loc = vlen + 1 + nbytes;
   } else {
-    hd[sk.loc++] = (uint8_t)((1u << 7) + (pb << 2) + 2);
-    for (uint32_t i = 0; i < cn; i++) {
-      stuff(sk, lower[i], maxbits);
-      stuff(sk, upper[i], maxbits);
+    if (lane != 0) return;
+    Sink sk{hd, vlen + 1, 0, 8};
+    if (raw) {
+      for (uint32_t i = 0; i < range; i++) stuff(sk, fr[i], maxbits);
+    } else {
+      for (uint32_t i = 0; i < cn; i++) {
+        stuff(sk, s_lower[i], maxbits);
+        stuff(sk, s_upper[i], maxbits);
+      }
+      for (uint32_t i = 0; i < range; i++) stuff(sk, fr[i], sbits(i));
     }
-    for (uint32_t i = 0; i < range; i++) {
-      uint32_t sb = 0;
-      if (lower[0] <= i && upper[0] >= i) sb = 1;
-      if (lower[1] <= i && upper[1] >= i) sb = 4;
-      for (uint32_t jj = 2; jj < cn; jj++)
-        if (lower[jj] <= i && upper[jj] >= i) sb = 4 * jj;
-      if (sb > pb) sb = pb;
-      stuff(sk, fr[i], sb);
-    }
+    if (sk.br != 8) hd[sk.loc++] = (uint8_t)sk.rem;
+    loc = sk.loc;
   }
-  if (sk.br != 8) hd[sk.loc++] = (uint8_t)sk.rem;
+  if (lane != 0) return;
   st.vlen = vlen;
-  st.hdr_len = sk.loc;
+  st.hdr_len = loc;
   st.maxbits = maxbits;
   st.expected_stored = expected_stored;
   st.fast = fast ? 1 : 0;
