@@ -1,23 +1,21 @@
 // Encoder front end, one workgroup (4 waves) per 256x256 tile (choh.cpp:464-500 tiles are
-// independent), streaming the tile in raster blocks of 256 pixels:
+// independent), streaming the tile in raster blocks of 256 pixels (one barrier per block):
 //  * subtract-green (channel.hpp:73-79) + MED fast-path residuals for the three planes
 //    (prediction.hpp:6-44), written to the residual arena, histograms in LDS;
 //  * grey test (channel.hpp:21-31) and distinct-colour count capped at 257 (choh.cpp:17-46);
 //  * LZ candidate detection for find_lz_rgb at -s0 (lz.hpp:32-53): a position q is a candidate
 //    iff some back distance b in [1, min(64, q)] gives 4 equal RGB pixels q..q+3 vs q-b..q-b+3.
-//    Every position gets a 32-bit fingerprint of its 4-pixel window.  Per block, an LDS hash
-//    table counts the fingerprints of positions [base - 64, base + 256); a position whose
-//    fingerprint occurs there more than once (its own occurrence) may have an equal window
-//    within 64 back, and only those positions are checked exactly (b = 1..64, first hit wins),
-//    so the candidate set is exact at one table probe per position.  The greedy selection runs
-//    in k_lz.hip over the (sparse) candidate bitmap.
+//    Each wave fingerprints the 4-pixel windows of its 64 positions and of the 64 before them,
+//    counts the 128 fingerprints in a wave-private LDS hash table, and checks exactly (b = 1..64,
+//    first hit wins) only the positions whose fingerprint occurs twice; equal windows have equal
+//    fingerprints, so the candidate set is exact.  The greedy selection runs in k_lz.hip over
+//    the (sparse) candidate bitmap.
 // Pixels live in an LDS ring (stored twice, so reads at q+k and q-d never wrap); every pixel is
 // read from HBM once, one block ahead of its use.
 #include "hoh_internal.h"
 
 #define RING 2048               // pixels: >= the 1024-pixel span [q - 512, q + 512) in use
-#define HRING 512               // fingerprints: >= the 320-position span [base - 64, base + 256)
-#define HTAB 1024               // fingerprint table slots (>= 3x the 320 keys of a block)
+#define WTAB 512                // slots of a wave's fingerprint table (128 keys)
 #define NT 256
 
 __device__ __forceinline__ uint16_t med16(uint16_t a, uint16_t b, uint16_t c) {
@@ -39,22 +37,36 @@ __device__ __forceinline__ uint32_t fp32(uint32_t a, uint32_t b, uint32_t c, uin
   return (h ^ (h >> 15)) | 1u;                     // never 0 (the empty-slot key)
 }
 
+// insert key k into a wave table (open addressing, keys are odd), return its slot; a key
+// inserted a second time sets the slot's duplicate bit
+__device__ __forceinline__ uint32_t wt_insert(uint32_t* key, uint32_t* dup, uint32_t k) {
+  uint32_t sl = (k >> 1) & (WTAB - 1);
+  for (int probe = 0; probe < WTAB; probe++) {
+    const uint32_t old = atomicCAS(&key[sl], 0u, k);
+    if (old == 0u) return sl;
+    if (old == k) { atomicOr(&dup[sl >> 5], 1u << (sl & 31)); return sl; }
+    sl = (sl + 1) & (WTAB - 1);
+  }
+  return WTAB;
+}
+
 __global__ __launch_bounds__(NT) void k_front(EncodeJob j) {
   __shared__ uint32_t ring[2 * RING];
-  __shared__ uint32_t hring[HRING];
-  __shared__ uint32_t hkey[HTAB];
-  __shared__ uint32_t hcnt[HTAB];
+  __shared__ uint32_t wkey[4][WTAB];
+  __shared__ uint32_t wdup[4][WTAB / 32];
   __shared__ uint32_t hist[3][512];
   __shared__ uint32_t hset[1024];
   __shared__ int s_ncol, s_notgrey, s_ncand;
 
-  const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int gt = j.t0 + t;
   const int x0 = (gt % j.xt) * j.tw, y0 = (gt / j.xt) * j.th;
   const int w = min(j.tw, j.W - x0), h = min(j.th, j.H - y0);
   const uint32_t npix = (uint32_t)w * h;
   for (int i = tid; i < 3 * 512; i += NT) (&hist[0][0])[i] = 0;
   for (int i = tid; i < 1024; i += NT) hset[i] = 0xffffffffu;
+  for (int i = lane; i < WTAB; i += 64) wkey[wv][i] = 0;
+  if (lane < WTAB / 32) wdup[wv][lane] = 0;
   if (tid == 0) { s_ncol = 0; s_notgrey = 0; s_ncand = 0; }
 
   uint16_t* res[3];
@@ -63,9 +75,7 @@ __global__ __launch_bounds__(NT) void k_front(EncodeJob j) {
   const uint8_t* img = j.rgb + ((size_t)y0 * j.W + x0) * 3;
   const size_t pitch = (size_t)j.W * 3;
 
-  // loader: this thread's pixel of block `blk` (raster position blk*256 + tid), (x, y) walked
-  // incrementally (w >= 256 for tiled images, so a block step wraps at most one row... or more
-  // for narrow edge tiles, hence the loop)
+  // loader cursor: this thread's pixel of the block being loaded (raster blk*256 + tid)
   int lx = tid, ly = 0;
   while (lx >= w) { lx -= w; ly++; }
   auto load_px = [&](uint32_t q) -> uint32_t {
@@ -74,7 +84,6 @@ __global__ __launch_bounds__(NT) void k_front(EncodeJob j) {
     return p[0] | (p[1] << 8) | (p[2] << 16);
   };
   auto advance = [&]() { lx += NT; while (lx >= w) { lx -= w; ly++; } };
-  // block 0 into the ring, block 1 in flight
   {
     const uint32_t v0 = load_px(tid);
     ring[tid & (RING - 1)] = v0;
@@ -83,6 +92,9 @@ __global__ __launch_bounds__(NT) void k_front(EncodeJob j) {
   }
   uint32_t nextv = load_px(NT + tid);
   advance();
+  // compute cursor: (x, y) of position base + tid
+  uint32_t cx = tid, cy = 0;
+  while (cx >= (uint32_t)w) { cx -= w; cy++; }
   __syncthreads();
 
   int notgrey = 0, ncand = 0;
@@ -103,10 +115,7 @@ __global__ __launch_bounds__(NT) void k_front(EncodeJob j) {
     const uint32_t* fwd = ring + ri;              // fwd[k] = pixel q + k
     const uint32_t* bwd = ring + ri + RING;       // bwd[-d] = pixel q - d
     const uint32_t v = fwd[0];
-    const bool win = q + 3 < npix;                 // a 4-pixel window starts here
-    uint32_t hq = 0;
     if (act) {
-      const uint32_t x = q % (uint32_t)w, y = q / (uint32_t)w;
       const uint32_t pr = v & 255, pg = (v >> 8) & 255, pbb = v >> 16;
       notgrey |= (pr != pg) | (pr != pbb);
       if (s_ncol <= 256 && !(j.dbg & 1)) {         // distinct colours, stop past 256
@@ -118,7 +127,7 @@ __global__ __launch_bounds__(NT) void k_front(EncodeJob j) {
           hsh = (hsh + 1) & 1023;
         }
       }
-      const bool hasL = x > 0, hasT = y > 0;
+      const bool hasL = cx > 0, hasT = cy > 0;
       const uint32_t vL = hasL ? bwd[-1] : 0;
       const uint32_t vT = hasT ? bwd[-w] : 0;
       const uint32_t vTL = (hasL && hasT) ? bwd[-w - 1] : 0;
@@ -133,49 +142,39 @@ __global__ __launch_bounds__(NT) void k_front(EncodeJob j) {
         res[k][q] = (uint16_t)r;
         if (!(j.dbg & 2)) atomicAdd(&hist[k][r], 1u);
       }
-      if (win) hq = fp32(v, fwd[1], fwd[2], fwd[3]);
     }
-    hring[q & (HRING - 1)] = hq;                    // 0: no window at q
-    for (int i = tid; i < HTAB; i += NT) { hkey[i] = 0; hcnt[i] = 0; }
-    __syncthreads();
-    // count the fingerprints of positions [base - 64, base + 256)
-    for (int i = tid; i < NT + 64; i += NT) {
-      const int p = (int)base - 64 + i;
-      if (p < 0) continue;
-      const uint32_t f = hring[p & (HRING - 1)];
-      if (!f) continue;
-      uint32_t sl = f & (HTAB - 1);
-      for (int probe = 0; probe < HTAB; probe++) {
-        const uint32_t old = atomicCAS(&hkey[sl], 0u, f);
-        if (old == 0u || old == f) { atomicAdd(&hcnt[sl], 1u); break; }
-        sl = (sl + 1) & (HTAB - 1);
-      }
+    cx += NT;
+    while (cx >= (uint32_t)w) { cx -= w; cy++; }
+    // LZ screen (wave-private): windows at q and at q - 64
+    const bool win = q + 3 < npix;                 // a 4-pixel window starts here
+    const uint32_t hq = win ? fp32(v, fwd[1], fwd[2], fwd[3]) : 0u;
+    const bool winp = q >= 64 && q - 61 < npix;    // window at q - 64 lies in the tile
+    const uint32_t hp = winp ? fp32(bwd[-64], bwd[-63], bwd[-62], bwd[-61]) : 0u;
+    uint32_t* key = wkey[wv];
+    uint32_t* dup = wdup[wv];
+    uint32_t sq = WTAB, sp = WTAB;
+    if (!(j.dbg & 4)) {
+      if (hq) sq = wt_insert(key, dup, hq);
+      if (hp) sp = wt_insert(key, dup, hp);
     }
-    __syncthreads();
-    bool hit = false;
-    if (win && !(j.dbg & 4)) {
-      uint32_t sl = hq & (HTAB - 1);
-      for (int probe = 0; probe < HTAB; probe++) {
-        const uint32_t k = hkey[sl];
-        if (k == hq) { hit = hcnt[sl] > 1; break; }
-        if (k == 0) break;
-        sl = (sl + 1) & (HTAB - 1);
-      }
-    }
-    const uint64_t flag = __ballot(win && hit);
+    const bool hit = hq && sq < WTAB && ((dup[sq >> 5] >> (sq & 31)) & 1);
+    const uint64_t flag = __ballot(hit);
     uint64_t word = 0;
     if (flag) {
       // exact check for the flagged lanes (lz.hpp:37-42 with offset < 4)
       bool c = false;
-      if ((flag >> lane) & 1) {
+      if (hit) {
         const uint32_t bmax = q < 64 ? q : 64;
         const uint32_t v1 = fwd[1], v2 = fwd[2], v3 = fwd[3];
         for (uint32_t b = 1; b <= bmax && !c; b++)
-          if (hring[(q - b) & (HRING - 1)] == hq)
-            c = bwd[-(int)b] == v && bwd[1 - (int)b] == v1 && bwd[2 - (int)b] == v2 && bwd[3 - (int)b] == v3;
+          c = bwd[-(int)b] == v && bwd[1 - (int)b] == v1 && bwd[2 - (int)b] == v2 && bwd[3 - (int)b] == v3;
       }
       word = __ballot(c);
     }
+    // clear the slots this wave used (wave-ordered LDS: the reads above are done)
+    if (sq < WTAB) key[sq] = 0;
+    if (sp < WTAB) key[sp] = 0;
+    if (lane < WTAB / 32) dup[lane] = 0;
     if (lane == 0 && (q >> 6) < (npix + 63) / 64) cand[q >> 6] = word;
     ncand += lane == 0 ? __popcll(word) : 0;
   }
