@@ -9,7 +9,9 @@ SRCS := $(wildcard $(CSRC)/*.hip) $(wildcard $(CSRC)/*.cpp)
 OBJS := $(patsubst $(CSRC)/%,build/%.o,$(SRCS))
 HDRS := $(wildcard $(CSRC)/*.h) include/hoh_ans.h
 
-all: $(LIBDIR)/libhohgpu.so oracle/liboracle.so
+BINDIR := hoh-ans_amd/bin
+
+all: $(LIBDIR)/libhohgpu.so oracle/liboracle.so $(BINDIR)/choh $(BINDIR)/dhoh $(BINDIR)/dropin_test
 
 build/%.hip.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p build
@@ -23,10 +25,14 @@ $(LIBDIR)/libhohgpu.so: $(OBJS)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
 
+$(BINDIR)/%: tools/cli/%.cpp $(LIBDIR)/libhohgpu.so include/hoh_ans.h $(wildcard include/hoh/*.hpp)
+	@mkdir -p $(BINDIR)
+	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -o $@ $< -L$(LIBDIR) -lhohgpu -Wl,-rpath,'$$ORIGIN/../lib'
+
 oracle/liboracle.so: oracle/hoh_oracle.c oracle/hoh_oracle.h
 	gcc -O2 -shared -fPIC -o $@ oracle/hoh_oracle.c
 
 clean:
-	rm -rf build $(LIBDIR)/libhohgpu.so oracle/liboracle.so
+	rm -rf build $(LIBDIR)/libhohgpu.so oracle/liboracle.so $(BINDIR)
 
 .PHONY: all clean

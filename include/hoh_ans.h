@@ -65,7 +65,7 @@ size_t hoh_encode_bound(int W, int H);
 int hoh_encode_image(hoh_ctx* ctx, const uint8_t* d_rgb, int W, int H, int speed,
                      uint8_t* d_out, size_t cap, size_t* out_size, size_t* printed, void* stream);
 
-/* Decode side index: the encoder's coder state every 1024 symbols of each plane stream (a
+/* Decode side index: the encoder's coder state every 256 symbols of each plane stream (a
  * Recoil-style checkpoint list kept BESIDE the .hoh, never inside it -- the file bytes are
  * identical with or without it).  With an index the decoder splits every stream into
  * independent segments; without one (any foreign .hoh) it decodes each stream serially.  A

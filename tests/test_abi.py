@@ -59,3 +59,15 @@ def test_no_device_fails_loudly():
     with pytest.raises(hoh_ans.HohError) as e:
         hoh_ans.Context(0)
     assert e.value.code == 8
+
+
+def test_dropin_headers_compile(tmp_path):
+    """include/hoh/*.hpp re-expose the reference's call surface; they must compile as C++17
+    with nothing but the C ABI header (no HIP, no torch)."""
+    import subprocess
+    src = tmp_path / "t.cpp"
+    inc = os.path.join(ROOT, "include", "hoh")
+    src.write_text("".join('#include "%s"\n' % os.path.join(inc, h) for h in sorted(os.listdir(inc))) +
+                   "int main() { return 0; }\n")
+    r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", str(src)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr

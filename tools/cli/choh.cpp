@@ -1,0 +1,63 @@
+// choh drop-in (choh.cpp:394-527): `choh in.rgb out.hoh width height [-s0]` on the GPU.
+// Writes the bytes the reference writes and prints the size it prints (header +
+// tile size for untiled images, of which only the header is written).  Only -s0 is implemented;
+// without a speed argument the reference would use -s1, here -s0 is used and a note printed.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+#include "../../include/hoh_ans.h"
+
+static bool read_file(const char* path, std::vector<uint8_t>& b) {
+  FILE* f = std::fopen(path, "rb");
+  if (!f) return false;
+  std::fseek(f, 0, SEEK_END);
+  const long n = std::ftell(f);
+  std::fseek(f, 0, SEEK_SET);
+  b.resize(n > 0 ? (size_t)n : 0);
+  const bool ok = b.empty() || std::fread(b.data(), 1, b.size(), f) == b.size();
+  std::fclose(f);
+  return ok;
+}
+
+int main(int argc, char** argv) {
+  if (argc < 5) {
+    std::printf("not enough arguments\nusage: choh infile.rgb outfile.hoh width height -s0\n");
+    return 1;
+  }
+  const int W = std::atoi(argv[3]), H = std::atoi(argv[4]);
+  if (W == 0 || H == 0) {
+    std::printf("invalid width or height\n");
+    return 2;
+  }
+  if (argc > 5 && std::strcmp(argv[5], "-s0") != 0) {
+    std::fprintf(stderr, "choh (GPU): only -s0 is implemented\n");
+    return HOH_E_UNSUPPORTED;
+  }
+  if (argc == 5) std::fprintf(stderr, "choh (GPU): no speed given, using -s0\n");
+  std::vector<uint8_t> in;
+  if (!read_file(argv[1], in)) { std::printf("could not read %s\n", argv[1]); return 3; }
+  const size_t raw = (size_t)W * H * 3;
+  if (in.size() < raw) { std::printf("input shorter than width*height*3\n"); return 3; }
+  hoh_ctx* ctx = nullptr;
+  int r = hoh_ctx_create(&ctx, 0);
+  if (r != HOH_OK) { std::fprintf(stderr, "choh: %s\n", hoh_strerror(r)); return r; }
+  const size_t cap = hoh_encode_bound(W, H);
+  uint8_t *d_in = nullptr, *d_out = nullptr;
+  if (hipMalloc(&d_in, raw) != hipSuccess || hipMalloc(&d_out, cap) != hipSuccess) return HOH_E_HIP;
+  if (hipMemcpy(d_in, in.data(), raw, hipMemcpyHostToDevice) != hipSuccess) return HOH_E_HIP;
+  size_t n = 0, printed = 0;
+  r = hoh_encode_image(ctx, d_in, W, H, 0, d_out, cap, &n, &printed, nullptr);
+  if (r != HOH_OK) { std::fprintf(stderr, "choh: %s\n", hoh_strerror(r)); return r; }
+  std::vector<uint8_t> out(n);
+  if (n && hipMemcpy(out.data(), d_out, n, hipMemcpyDeviceToHost) != hipSuccess) return HOH_E_HIP;
+  std::printf("%d\n", (int)printed);
+  FILE* f = std::fopen(argv[2], "wb");
+  if (!f || (n && std::fwrite(out.data(), 1, n, f) != n)) { std::printf("could not write %s\n", argv[2]); return 3; }
+  std::fclose(f);
+  (void)hipFree(d_in);
+  (void)hipFree(d_out);
+  hoh_ctx_destroy(ctx);
+  return 0;
+}
