@@ -465,18 +465,26 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams, uint32_t
   __syncthreads();
   uint64_t Ta = 0;
   if (j.dbg & 16) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(Ta)::"memory");
-  // slot table, one thread per 32-slot bucket: first symbol (binary search) then a walk
-  for (uint32_t b = tid; b < (M >> bsh); b += DR_T) {
-    const uint32_t slot0 = b << bsh;
-    uint32_t lo = 0, hi = range;                             // cum[lo] <= slot0 < cum[hi]
-    while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (cum_s[mid] <= slot0) lo = mid; else hi = mid; }
-    sy_s[b] = (uint16_t)lo;
-    uint32_t s = lo, cn = cum_s[lo + 1];
-    for (uint32_t k = 0; k < (1u << bsh); k++) {
-      while (cn <= slot0 + k && s + 1 < range) { s++; cn = cum_s[s + 1]; }
-      if (s - lo > 255) wide = 1;
-      tb[slot0 + k] = (uint8_t)(s - lo);
-    }
+  // slot table.  A slot's byte is (its symbol) - (first symbol of its 32-slot bucket), so it is
+  // 0 everywhere except in buckets where a symbol starts mid-bucket: (1) first symbol of every
+  // bucket, one thread per symbol; (2) zero fill; (3) each symbol writes its slots inside the
+  // bucket it starts in (at most 31).  All stores independent, no serial walk.
+  for (uint32_t s = tid; s < range; s += DR_T) {
+    const uint32_t c0 = cum_s[s], c1 = cum_s[s + 1];
+    if (c1 <= c0) continue;
+    const uint32_t b1 = (c1 - 1) >> bsh;
+    for (uint32_t b = (c0 + (1u << bsh) - 1) >> bsh; b <= b1; b++) sy_s[b] = (uint16_t)s;
+  }
+  for (uint32_t q = tid; q < (M + 3) / 4; q += DR_T) ((uint32_t*)tb)[q] = 0;
+  __syncthreads();
+  for (uint32_t s = tid; s < range; s += DR_T) {
+    const uint32_t c0 = cum_s[s], c1 = cum_s[s + 1];
+    if (c1 <= c0 || (c0 & ((1u << bsh) - 1)) == 0) continue;  // starts a bucket: bytes stay 0
+    const uint32_t b = c0 >> bsh;
+    const uint32_t off = s - sy_s[b];
+    if (off > 255) wide = 1;
+    const uint32_t e = min(c1, (b + 1) << bsh);
+    for (uint32_t slot = c0; slot < e; slot++) tb[slot] = (uint8_t)off;
   }
   __syncthreads();
   uint16_t* out = j.dsym + d.out_off;
