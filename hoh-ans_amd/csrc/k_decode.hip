@@ -666,7 +666,7 @@ __device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
   return max(min(a, b), min(max(a, b), c));
 }
 
-#define UP_P 8   // residual prefetch depth (steps)
+#define UP_P 8   // residual prefetch group (steps)
 
 // Wavefront MED inverse (prediction.hpp:26-41 inverted on every row, Q9 fixed) of the three
 // planes of one tile + inverse subtract-green (channel.hpp:73-79), one wave per tile.
@@ -702,20 +702,32 @@ __global__ __launch_bounds__(64) void k_dunpred_fast(DecJob j) {
     const int last = min(63, h - r0 - 1);
     const bool rowok = y < h;
     const size_t bo = (size_t)(r0 >> 6) * nst * 64;
-    uint32_t qG[UP_P], qR[UP_P], qB[UP_P];
+    // residuals of the next UP_P steps are loaded one group ahead into nG/nR/nB and landed at
+    // the group start (the asm operand pins the wait there, so the compiler never parks a
+    // pending load across the loop latch)
+    uint32_t nG[UP_P], nR[UP_P], nB[UP_P];
 #pragma unroll
-    for (int u = 0; u < UP_P; u++) { qG[u] = skG[bo + u * 64]; qR[u] = skR[bo + u * 64]; qB[u] = skB[bo + u * 64]; }
+    for (int u = 0; u < UP_P; u++) { nG[u] = skG[bo + u * 64]; nR[u] = skR[bo + u * 64]; nB[u] = skB[bo + u * 64]; }
     uint32_t cG = 0, cR = 0, cB = 0;      // this lane's value at the previous step (L)
     uint32_t pG = 128, pR = 256, pB = 256; // T of the previous step (TL)
     uint8_t* orow = ob + (size_t)lane * opitch;
     for (int s0 = 0; s0 < nst; s0 += UP_P) {
+      uint32_t qG[UP_P], qR[UP_P], qB[UP_P];
+#pragma unroll
+      for (int u = 0; u < UP_P; u++) {
+        asm volatile("" ::"v"(nG[u]), "v"(nR[u]), "v"(nB[u]));
+        qG[u] = nG[u]; qR[u] = nR[u]; qB[u] = nB[u];
+      }
+#pragma unroll
+      for (int u = 0; u < UP_P; u++) {
+        const size_t nx = bo + (size_t)(s0 + UP_P + u) * 64;
+        nG[u] = skG[nx]; nR[u] = skR[nx]; nB[u] = skB[nx];
+      }
 #pragma unroll
       for (int u = 0; u < UP_P; u++) {
         const int st = s0 + u;
         const int x = st - lane;
         const uint32_t rG = qG[u], rR = qR[u], rB = qB[u];
-        const size_t nx = bo + (size_t)(st + UP_P) * 64;
-        qG[u] = skG[nx]; qR[u] = skR[nx]; qB[u] = skB[nx];
         uint32_t oG = 128, oR = 256, oB = 256;        // lane 0: row above the band
         if (r0 > 0 && lane == 0 && x < w) { oG = lastG[x]; oR = lastR[x]; oB = lastB[x]; }
         const uint32_t TG = wave_shr1(cG, oG), TR = wave_shr1(cR, oR), TB = wave_shr1(cB, oB);
@@ -1028,7 +1040,7 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   j.npix_cap = (uint32_t)(((size_t)j.tw * j.th + 63) / 64 * 64);
   j.lz_cap = (uint32_t)((j.npix_cap / 4 + j.npix_cap / 255 + 16 + 7) / 8 * 8);
   {
-    const size_t skew = (size_t)((j.th + 63) / 64) * (j.tw + 63) * 64 + (size_t)UP_P * 64;
+    const size_t skew = (size_t)((j.th + 63) / 64) * (j.tw + 63) * 64 + (size_t)2 * UP_P * 64;
     j.plane_cap = (uint32_t)((std::max((size_t)j.npix_cap, skew) + 63) / 64 * 64);
   }
   const int S = j.ntiles * SK_PER_TILE;
