@@ -45,7 +45,7 @@ struct hoh_index {
 struct hoh_ctx {
   int device = 0;
   hipStream_t own = nullptr;
-  Buf sym, hist, candbits, matches, streams, tiles, hdr, tab_fast, tab_gen, slabs, ckpt, misc, tsizes;
+  Buf sym, hist, candbits, matches, pal, streams, tiles, hdr, tab_fast, tab_gen, slabs, ckpt, misc, tsizes;
   DecWork dec;                  // decoder workspaces (k_decode.hip)
   uint64_t* pinned = nullptr;   // small host staging (status words, sizes)
   int profiling = 0;
@@ -139,7 +139,7 @@ static void freebuf(Buf& b) { if (b.p) (void)hipFree(b.p); b.p = nullptr; b.n = 
 void hoh_ctx_destroy(hoh_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  Buf* all[] = {&c->sym, &c->hist, &c->candbits, &c->matches, &c->streams, &c->tiles, &c->hdr,
+  Buf* all[] = {&c->sym, &c->hist, &c->candbits, &c->matches, &c->pal, &c->streams, &c->tiles, &c->hdr,
                 &c->tab_fast, &c->tab_gen, &c->slabs, &c->ckpt, &c->misc, &c->tsizes};
   for (Buf* b : all) freebuf(*b);
   dec_free(c->dec);
@@ -274,14 +274,16 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   j.gen_stride = 512;
   j.hdr_cap = HOH_HDR_CAP;
   const size_t S = (size_t)ntiles * SK_PER_TILE;
-  const size_t nsym = (size_t)ntiles * 3 * j.npix_cap + (size_t)ntiles * 3 * j.lz_cap;
-  const size_t nslab = (size_t)ntiles * 3 * (j.npix_cap + 8) + (size_t)ntiles * 3 * (j.lz_cap + 8);
+  // arenas: [tile][3] planes, [tile][3] LZ streams, [tile] indexed plane (hoh_internal.h)
+  const size_t nsym = (size_t)ntiles * 3 * (j.npix_cap + j.lz_cap) + (size_t)ntiles * j.npix_cap;
+  const size_t nslab = (size_t)ntiles * 3 * (j.npix_cap + 8 + j.lz_cap + 8) + (size_t)ntiles * (j.npix_cap + 8);
   const size_t nck = S * (j.npix_cap / HOH_SEG + 2);
   int e = HOH_OK;
   if ((e = ensure(c->sym, nsym * 2 + 64))) return e;
   if ((e = ensure(c->hist, S * 512 * 4))) return e;
   if ((e = ensure(c->candbits, (size_t)ntiles * (j.npix_cap / 64) * 8))) return e;
   if ((e = ensure(c->matches, (size_t)ntiles * 3 * (j.lz_cap + 1) * 4))) return e;
+  if ((e = ensure(c->pal, (size_t)ntiles * 256 * 4))) return e;
   if ((e = ensure(c->streams, S * sizeof(StreamInfo)))) return e;
   if ((e = ensure(c->tiles, (size_t)ntiles * sizeof(TileInfo)))) return e;
   if ((e = ensure(c->hdr, S * HOH_HDR_CAP))) return e;
@@ -294,6 +296,7 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   j.hist = (uint32_t*)c->hist.p;
   j.candbits = (uint64_t*)c->candbits.p;
   j.matches = (uint32_t*)c->matches.p;
+  j.palette = (uint32_t*)c->pal.p;
   j.streams = (StreamInfo*)c->streams.p;
   j.tiles = (TileInfo*)c->tiles.p;
   j.hdr = (uint8_t*)c->hdr.p;
@@ -312,9 +315,10 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   if (hipMemsetAsync(c->misc.p, 0, 64, s) != hipSuccess) return HOH_E_HIP;
   prof.mark("memset");
   launch_front(j, s);            prof.mark("front");
+  launch_palette(j, s);          prof.mark("palette");
   launch_lz(j, s);               prof.mark("lz");
   launch_tables(j, (int)S, s);   prof.mark("tables");
-  launch_rans_fast(j, nullptr, ntiles * 3, s); prof.mark("rans_enc_fast");
+  launch_rans_fast(j, nullptr, ntiles * 4, s); prof.mark("rans_enc_fast");
   launch_rans_gen(j, (int)S, s); prof.mark("rans_enc_gen");
   launch_finalize(j, (int)S, s); prof.mark("finalize");
   launch_layout(j, s);           prof.mark("layout");

@@ -12,8 +12,10 @@
 #define HOH_MAX_TILE_W 65535
 #define HOH_LZ_WINDOW 64          // -s0 seek distance 6 -> 1 << 6 pixels back (choh.cpp:125, lz.hpp:20)
 
-// stream kinds inside a tile (stream id = tile * 6 + kind)
-enum { SK_LZ_FUTURE = 0, SK_LZ_LENGTH = 1, SK_LZ_BACKBY = 2, SK_G = 3, SK_R = 4, SK_B = 5, SK_PER_TILE = 6 };
+// stream kinds inside a tile (stream id = tile * SK_PER_TILE + kind); SK_I is the indexed
+// (palette) plane that competes with the three sub-green planes (choh.cpp:298-308)
+enum { SK_LZ_FUTURE = 0, SK_LZ_LENGTH = 1, SK_LZ_BACKBY = 2, SK_G = 3, SK_R = 4, SK_B = 5, SK_I = 6,
+       SK_PER_TILE = 7 };
 
 // stream coding modes (entropy_encoding.hpp)
 enum { SM_EMPTY = 0, SM_RANS = 1, SM_STORED = 2 };
@@ -47,6 +49,8 @@ struct StreamInfo {
   uint64_t expected_stored;
   uint32_t fast;          // encoded by the LDS-table fast kernel
   uint32_t ckpt_off;      // index of the first checkpoint of this stream
+  uint32_t drop;          // coded but not part of the file (losing colour mode)
+  uint32_t clip;          // nonzero: only the first clip bytes go to the file (Q15 prefix)
 };
 
 struct TileInfo {
@@ -58,7 +62,7 @@ struct TileInfo {
   uint32_t size;          // tile bytes
   uint32_t lz_bytes;      // 1 + the three LZ stream sizes
   uint64_t off;           // output byte offset of the tile
-  uint32_t mode;          // internal colour mode byte (128 sub-green, 0 bitimage)
+  uint32_t mode;          // internal colour mode byte (128 sub-green, 127 indexed, 0 bitimage)
   uint32_t pad;           // layout: byte offset of this tile's size varint
 };
 
@@ -119,7 +123,8 @@ struct EncodeJob {
   uint32_t* hist;         // [stream][512]
   uint64_t* candbits;     // [tile][npix_cap/64] LZ candidate bitmap
   uint32_t* matches;      // [tile][lz_cap] packed (pos, len, back) triples (3 words each)
-  StreamInfo* streams;    // [ntiles * 6]
+  uint32_t* palette;      // [tile][256] colours in first-occurrence order (palette tiles)
+  StreamInfo* streams;    // [ntiles * SK_PER_TILE]
   TileInfo* tiles;        // [ntiles]
   uint8_t* hdr;           // [stream][HOH_HDR_CAP]
   EncFast* tab_fast;      // [stream][512]
@@ -137,7 +142,16 @@ struct EncodeJob {
   int write_table;        // write the n-1 tile size varints (a whole .hoh); 0 for a shard blob
 };
 
+// arena offsets (elements / words): [tile][3] planes, [tile][3] LZ streams, [tile] indexed plane
+__host__ __device__ inline size_t idx_plane_off(const EncodeJob& j, int t) {
+  return (size_t)j.ntiles * 3 * (j.npix_cap + j.lz_cap) + (size_t)t * j.npix_cap;
+}
+__host__ __device__ inline size_t idx_slab_off(const EncodeJob& j, int t) {
+  return (size_t)j.ntiles * 3 * (j.npix_cap + 8 + j.lz_cap + 8) + (size_t)t * (j.npix_cap + 8);
+}
+
 void launch_front(const EncodeJob& j, hipStream_t s);
+void launch_palette(const EncodeJob& j, hipStream_t s);
 void launch_lz(const EncodeJob& j, hipStream_t s);
 void launch_tables(const EncodeJob& j, int nstreams, hipStream_t s);
 void launch_rans_fast(const EncodeJob& j, const uint32_t* fast_ids, int nfast, hipStream_t s);

@@ -55,15 +55,26 @@ __global__ __launch_bounds__(1024) void k_layout(EncodeJob j) {
       TileInfo ti = j.tiles[t];
       const StreamInfo* st = j.streams + (size_t)t * SK_PER_TILE;
       uint32_t bad = ti.flags & (TF_UNREPRODUCIBLE | TF_UNSUPPORTED | TF_OVERFLOW);
-      if (!(ti.flags & TF_GREY) && (ti.flags & TF_PALETTE_CAND)) bad |= TF_UNSUPPORTED;
       for (int k = 0; k < SK_PER_TILE; k++) if (st[k].err) bad |= TF_OVERFLOW;
-      if (bad) atomicOr(j.gerr, (uint32_t)bad << 8);
       const uint32_t lzb = 1 + st[0].size + st[1].size + st[2].size;   // lz.hpp:98 + 3 streams
       uint64_t s64 = 2 + 1 + lzb;                                        // choh.cpp:115-116, :328-331
-      if (ti.mode == 128) {
+      if (ti.mode == 128 || ti.mode == 127) {
         const uint32_t L1 = 5 + st[3].size, L2 = 5 + st[4].size, L3 = 5 + st[5].size;
-        s64 += 1 + hoh_varint_len(L1) + hoh_varint_len(L2) + L1 + L2 + L3;   // :352-363
+        ti.mode = 128;
+        if (!(ti.flags & TF_GREY) && (ti.flags & TF_PALETTE_CAND)) {
+          // palette_encode (choh.cpp:90-99) vs sub-green (:295-308): the indexed layer wins when
+          // layer + 3 * colours + 1 < G + R' + B' layers; the tile then carries channel_size1
+          // (the GREEN layer's size) bytes of the indexed layer and no palette (Q15)
+          const uint64_t Li = 5 + (uint64_t)st[SK_I].size;
+          if (Li + 3 * (uint64_t)ti.colours + 1 < (uint64_t)L1 + L2 + L3) {
+            ti.mode = 127;
+            if (Li < L1) bad |= TF_UNREPRODUCIBLE;                       // prefix runs past the layer
+          }
+        }
+        if (ti.mode == 128) s64 += 1 + hoh_varint_len(L1) + hoh_varint_len(L2) + L1 + L2 + L3;   // :352-363
+        else s64 += L1;                                                  // :335-338
       }
+      if (bad) atomicOr(j.gerr, (uint32_t)bad << 8);
       ti.lz_bytes = lzb;
       ti.size = (uint32_t)s64;
       j.tiles[t] = ti;
@@ -103,6 +114,11 @@ __global__ __launch_bounds__(1024) void k_layout(EncodeJob j) {
         const uint32_t L1 = 5 + st[3].size, L2 = 5 + st[4].size;
         o += 1 + hoh_varint_len(L1) + hoh_varint_len(L2);
         for (int k = 3; k < 6; k++) { st[k].out_off = o + 5; o += 5 + st[k].size; }
+        st[SK_I].drop = 1;
+      } else if (ti.mode == 127) {
+        for (int k = 3; k < 6; k++) st[k].drop = 1;
+        st[SK_I].out_off = o + 5;
+        st[SK_I].clip = st[3].size;
       }
     }
     carry_s += chunk_s;
@@ -121,6 +137,10 @@ __global__ __launch_bounds__(64) void k_tilebytes(EncodeJob j) {
   o[2] = (uint8_t)ti.mode;                             // internal colour mode (:328)
   o[3] = 0x03;                                         // LZ flags (lz.hpp:98)
   if (j.write_table && t + 1 < j.ntiles) hoh_write_varint(j.out, ti.pad, ti.size);   // choh.cpp:496-498
+  if (ti.mode == 127) {                                // indexed layer header (layer_encode.hpp:57, :320-325)
+    uint8_t* q = o + 3 + ti.lz_bytes;
+    q[0] = 0x10; q[1] = 0; q[2] = 0; q[3] = 0x00; q[4] = 0x10;
+  }
   if (ti.mode == 128) {
     uint32_t p = 3 + ti.lz_bytes;
     o[p++] = 0x24;                                     // channel order G R B (:352)
@@ -138,34 +158,46 @@ __global__ __launch_bounds__(256) void k_streambytes(EncodeJob j) {
   const int s = blockIdx.x, tid = threadIdx.x;
   if (*j.total > j.cap || *j.gerr) return;
   const StreamInfo st = j.streams[s];
-  if (st.range == 0) return;
+  if (st.range == 0 || st.drop) return;
   uint8_t* o = j.out + st.out_off;
   const uint8_t* hd = j.hdr + (size_t)s * j.hdr_cap;
+  const uint64_t lim = st.clip ? st.clip : ~0ull;   // bytes of the stream that reach the file
   if (st.mode == SM_EMPTY) {
-    for (uint32_t i = tid; i < st.vlen; i += 256) o[i] = hd[i];
+    for (uint32_t i = tid; i < st.vlen && i < lim; i += 256) o[i] = hd[i];
     return;
   }
   if (st.mode == SM_RANS) {
     const uint64_t rb = (uint64_t)st.words * 4;
     const uint32_t vl = hoh_varint_len(rb);
-    for (uint32_t i = tid; i < st.hdr_len; i += 256) o[i] = hd[i];
-    if (tid == 0) hoh_write_varint(o, st.hdr_len, rb);
-    uint8_t* pay = o + st.hdr_len + vl;
+    for (uint32_t i = tid; i < st.hdr_len && i < lim; i += 256) o[i] = hd[i];
+    if (tid == 0) {
+      uint8_t v[3];
+      const uint32_t n = hoh_write_varint(v, 0, rb);
+      for (uint32_t k = 0; k < n; k++) if (st.hdr_len + k < lim) o[st.hdr_len + k] = v[k];
+    }
+    const uint64_t p0 = st.hdr_len + vl;
+    uint8_t* pay = o + p0;
     const uint32_t* w = j.slabs + st.slab_off + st.widx_end;
-    for (uint32_t i = tid; i < st.words; i += 256) {
-      const uint32_t v = w[i];
-      pay[4 * i] = (uint8_t)v; pay[4 * i + 1] = (uint8_t)(v >> 8);
-      pay[4 * i + 2] = (uint8_t)(v >> 16); pay[4 * i + 3] = (uint8_t)(v >> 24);
+    if (p0 + 4ull * st.words <= lim) {
+      for (uint32_t i = tid; i < st.words; i += 256) {
+        const uint32_t v = w[i];
+        pay[4 * i] = (uint8_t)v; pay[4 * i + 1] = (uint8_t)(v >> 8);
+        pay[4 * i + 2] = (uint8_t)(v >> 16); pay[4 * i + 3] = (uint8_t)(v >> 24);
+      }
+    } else {
+      for (uint64_t b = tid; p0 + b < lim && b < 4ull * st.words; b += 256)
+        pay[b] = (uint8_t)(w[b / 4] >> (8 * (b % 4)));
     }
     return;
   }
   // stored: varint(range-1) varint(n) 0x00, then n symbols of maxbits bits, MSB first
-  for (uint32_t i = tid; i < st.vlen; i += 256) o[i] = hd[i];
-  if (tid == 0) o[st.vlen] = 0;
+  for (uint32_t i = tid; i < st.vlen && i < lim; i += 256) o[i] = hd[i];
+  if (tid == 0 && st.vlen < lim) o[st.vlen] = 0;
   uint8_t* pay = o + st.vlen + 1;
   const uint16_t* sy = j.sym + st.sym_off;
   const uint32_t mb = st.maxbits;
-  const uint64_t nbytes = ((uint64_t)mb * st.n + 7) / 8;
+  uint64_t nbytes = ((uint64_t)mb * st.n + 7) / 8;
+  if (st.vlen + 1 + nbytes > lim) nbytes = lim > st.vlen + 1 ? lim - st.vlen - 1 : 0;
   for (uint64_t k = tid; k < nbytes; k += 256) {
     uint32_t byte = 0;
     for (int bit = 0; bit < 8; bit++) {

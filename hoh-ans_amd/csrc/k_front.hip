@@ -56,7 +56,8 @@ __global__ __launch_bounds__(NT) void k_front(EncodeJob j) {
   __shared__ uint32_t wdup[4][WTAB / 32];
   __shared__ uint32_t hist[3][512];
   __shared__ uint32_t hset[1024];
-  __shared__ int s_ncol, s_notgrey, s_ncand;
+  __shared__ uint32_t hpos[1024];                   // first raster position of each colour
+  __shared__ int s_ncol, s_notgrey, s_ncand, s_np;
 
   const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int gt = j.t0 + t;
@@ -64,10 +65,10 @@ __global__ __launch_bounds__(NT) void k_front(EncodeJob j) {
   const int w = min(j.tw, j.W - x0), h = min(j.th, j.H - y0);
   const uint32_t npix = (uint32_t)w * h;
   for (int i = tid; i < 3 * 512; i += NT) (&hist[0][0])[i] = 0;
-  for (int i = tid; i < 1024; i += NT) hset[i] = 0xffffffffu;
+  for (int i = tid; i < 1024; i += NT) { hset[i] = 0xffffffffu; hpos[i] = 0xffffffffu; }
   for (int i = lane; i < WTAB; i += 64) wkey[wv][i] = 0;
   if (lane < WTAB / 32) wdup[wv][lane] = 0;
-  if (tid == 0) { s_ncol = 0; s_notgrey = 0; s_ncand = 0; }
+  if (tid == 0) { s_ncol = 0; s_notgrey = 0; s_ncand = 0; s_np = 0; }
 
   uint16_t* res[3];
   for (int k = 0; k < 3; k++) res[k] = j.sym + (size_t)(t * 3 + k) * j.npix_cap;
@@ -122,8 +123,8 @@ __global__ __launch_bounds__(NT) void k_front(EncodeJob j) {
         uint32_t hsh = (v * 2654435761u) >> 22;
         for (int probe = 0; probe < 1024; probe++) {
           uint32_t old = atomicCAS(&hset[hsh], 0xffffffffu, v);
-          if (old == 0xffffffffu) { atomicAdd(&s_ncol, 1); break; }
-          if (old == v) break;
+          if (old == 0xffffffffu) { atomicAdd(&s_ncol, 1); atomicMin(&hpos[hsh], q); break; }
+          if (old == v) { atomicMin(&hpos[hsh], q); break; }
           hsh = (hsh + 1) & 1023;
         }
       }
@@ -185,6 +186,26 @@ __global__ __launch_bounds__(NT) void k_front(EncodeJob j) {
     const int k = i / 512, s = i % 512;
     j.hist[(size_t)(t * SK_PER_TILE + SK_G + k) * 512 + s] = hist[k][s];
   }
+  if (s_ncol <= 256 && s_notgrey) {
+    // palette in first-occurrence order (choh.cpp:64-88): rank of a colour = number of colours
+    // whose first position is smaller (the ring is free now)
+    uint32_t* pc = ring;
+    uint32_t* pp = ring + 256;
+    for (int i = tid; i < 1024; i += NT) {
+      if (hset[i] != 0xffffffffu) {
+        const int k = atomicAdd(&s_np, 1);
+        pc[k] = hset[i];
+        pp[k] = hpos[i];
+      }
+    }
+    __syncthreads();
+    if (tid < s_np) {
+      const uint32_t me = pp[tid];
+      uint32_t rank = 0;
+      for (int m = 0; m < s_np; m++) rank += pp[m] < me;
+      j.palette[(size_t)t * 256 + rank] = pc[tid];
+    }
+  }
   if (tid == 0) {
     TileInfo ti;
     ti.x0 = x0; ti.y0 = y0; ti.w = w; ti.h = h;
@@ -202,6 +223,69 @@ __global__ __launch_bounds__(NT) void k_front(EncodeJob j) {
     ti.pad = 0;
     j.tiles[t] = ti;
   }
+}
+
+// Indexed plane of a palette-candidate tile (choh.cpp:48-102 palette_encode + layer_encode -s0):
+// index = first-occurrence rank of the pixel's colour, then the MED fast-path residual at depth 8
+// (prediction.hpp:6-44) and its histogram.  One workgroup per tile; pass 1 writes the indices
+// into the tile's indexed-plane slot, pass 2 turns them into residuals in place, walking blocks
+// from the last to the first so every neighbour (q-1, q-w, q-w-1) is still an index when read.
+__global__ __launch_bounds__(NT) void k_palette(EncodeJob j) {
+  __shared__ uint32_t hk[1024];
+  __shared__ uint32_t hv[1024];
+  __shared__ uint32_t phist[256];
+  const int t = blockIdx.x, tid = threadIdx.x;
+  const TileInfo ti = j.tiles[t];
+  if (!(ti.flags & TF_PALETTE_CAND) || (ti.flags & TF_GREY)) return;
+  const int w = ti.w, h = ti.h, ncol = ti.colours;
+  const uint32_t npix = (uint32_t)w * h;
+  for (int i = tid; i < 1024; i += NT) hk[i] = 0xffffffffu;
+  phist[tid] = 0;
+  __syncthreads();
+  if (tid < ncol) {
+    const uint32_t c = j.palette[(size_t)t * 256 + tid];
+    uint32_t hsh = (c * 2654435761u) >> 22;
+    while (atomicCAS(&hk[hsh], 0xffffffffu, c) != 0xffffffffu) hsh = (hsh + 1) & 1023;
+    hv[hsh] = (uint32_t)tid;
+  }
+  __syncthreads();
+  uint16_t* pl = j.sym + idx_plane_off(j, t);
+  const uint8_t* img = j.rgb + ((size_t)ti.y0 * j.W + ti.x0) * 3;
+  const size_t pitch = (size_t)j.W * 3;
+  int x = tid, y = 0;
+  while (x >= w) { x -= w; y++; }
+  for (uint32_t q = tid; q < npix; q += NT) {
+    const uint8_t* p = img + (size_t)y * pitch + (size_t)x * 3;
+    const uint32_t c = p[0] | (p[1] << 8) | (p[2] << 16);
+    uint32_t hsh = (c * 2654435761u) >> 22;
+    for (int probe = 0; probe < 1024 && hk[hsh] != c; probe++) hsh = (hsh + 1) & 1023;
+    pl[q] = (uint16_t)hv[hsh];
+    x += NT;
+    while (x >= w) { x -= w; y++; }
+  }
+  __syncthreads();
+  const uint32_t nblk = (npix + NT - 1) / NT;
+  for (int b = (int)nblk - 1; b >= 0; b--) {
+    const uint32_t q = (uint32_t)b * NT + tid;
+    uint32_t r = 0;
+    if (q < npix) {
+      const uint32_t qx = q % (uint32_t)w, qy = q / (uint32_t)w;
+      const uint16_t v = pl[q];
+      const uint16_t L = qx ? pl[q - 1] : (uint16_t)128;
+      const uint16_t T = qy ? pl[q - w] : (uint16_t)128;
+      const uint16_t TL = (qx && qy) ? pl[q - w - 1] : (uint16_t)128;
+      r = ((int)v - (int)med16(T, L, (uint16_t)(T + L - TL)) + 128 + 256) & 255;
+    }
+    __syncthreads();
+    if (q < npix) { pl[q] = (uint16_t)r; atomicAdd(&phist[r], 1u); }
+    __syncthreads();
+  }
+  uint32_t* hs = j.hist + (size_t)(t * SK_PER_TILE + SK_I) * 512;
+  for (int i = tid; i < 512; i += NT) hs[i] = i < 256 ? phist[i] : 0u;
+}
+
+void launch_palette(const EncodeJob& j, hipStream_t s) {
+  hipLaunchKernelGGL(k_palette, dim3(j.ntiles), dim3(NT), 0, s, j);
 }
 
 void launch_front(const EncodeJob& j, hipStream_t s) {

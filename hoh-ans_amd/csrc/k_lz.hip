@@ -4,7 +4,7 @@
 // distances (lane = back-1) and reduce to (longest, smallest back) exactly like lz.hpp:35-53.
 // Then the three LZ symbol streams are generated, and if any pixel was matched ("nuked") the
 // residual streams of the three planes are compacted and their histograms corrected
-// (layer_encode.hpp:93-99).  Also fills the StreamInfo of the tile's six streams.
+// (layer_encode.hpp:93-99).  Also fills the StreamInfo of the tile's streams.
 #include "hoh_internal.h"
 
 __device__ __forceinline__ uint32_t img_px(const EncodeJob& j, int x0, int y0, int w, uint32_t q) {
@@ -123,7 +123,7 @@ __global__ __launch_bounds__(64) void k_lz(EncodeJob j) {
         st.n = k == 0 ? nf : nmk;
         st.range = 256;
         st.pb = 10;                                                   // lz.hpp:100-142
-      } else {
+      } else if (k < SK_I) {
         st.sym_off = (size_t)(t * 3 + k - 3) * j.npix_cap;
         st.slab_off = (size_t)(t * 3 + k - 3) * pl_slab;
         st.slab_cap = (uint32_t)pl_slab;
@@ -131,6 +131,15 @@ __global__ __launch_bounds__(64) void k_lz(EncodeJob j) {
         st.range = planes ? (k == SK_G ? 256 : 512) : 0;              // choh.cpp:221-255; 0 = absent
         st.pb = 15;                                                   // layer_encode.hpp:59
         st.fast = planes ? 1 : 0;
+      } else {                                                        // indexed plane (choh.cpp:90-99)
+        const bool pal = planes && (ti.flags & TF_PALETTE_CAND);
+        st.sym_off = idx_plane_off(j, t);
+        st.slab_off = idx_slab_off(j, t);
+        st.slab_cap = (uint32_t)pl_slab;
+        st.n = pal ? nclean : 0;
+        st.range = pal ? 256 : 0;
+        st.pb = 15;
+        st.fast = pal ? 1 : 0;
       }
       st.mode = SM_EMPTY;
       st.ckpt_off = (uint32_t)((size_t)(t * SK_PER_TILE + k) * (j.npix_cap / HOH_SEG + 2));
@@ -140,8 +149,8 @@ __global__ __launch_bounds__(64) void k_lz(EncodeJob j) {
 }
 
 // Residual compaction of tiles with LZ copies (layer_encode.hpp:93-99): nuked pixels leave
-// the three residual planes (order kept) and their histograms.  One 256-thread workgroup per
-// tile; the nuke bitmap is built in LDS from the match list, then the plane is walked in
+// the three residual planes (four with the indexed plane; order kept) and their histograms.
+// One 256-thread workgroup per tile; the nuke bitmap is built in LDS from the match list, then the plane is walked in
 // 256-pixel blocks with a block-wide rank of the kept pixels.
 __global__ __launch_bounds__(256) void k_nuke(EncodeJob j) {
   extern __shared__ uint32_t nk_bits[];                  // npix_cap / 32 words
@@ -159,9 +168,10 @@ __global__ __launch_bounds__(256) void k_nuke(EncodeJob j) {
     for (uint32_t p = a + tid; p < e; p += 256) atomicOr(&nk_bits[p >> 5], 1u << (p & 31));
   }
   __syncthreads();
-  for (int k = 0; k < 3; k++) {
-    uint16_t* r = j.sym + (size_t)(t * 3 + k) * j.npix_cap;
-    uint32_t* hk = j.hist + (size_t)(t * SK_PER_TILE + SK_G + k) * 512;
+  const int nplanes = (ti.flags & TF_PALETTE_CAND) && !(ti.flags & TF_GREY) ? 4 : 3;
+  for (int k = 0; k < nplanes; k++) {
+    uint16_t* r = j.sym + (k < 3 ? (size_t)(t * 3 + k) * j.npix_cap : idx_plane_off(j, t));
+    uint32_t* hk = j.hist + (size_t)(t * SK_PER_TILE + (k < 3 ? SK_G + k : SK_I)) * 512;
     uint32_t outc = 0;
     uint16_t vnext = tid < npix ? r[tid] : 0;
     for (uint32_t base = 0; base < npix; base += 256) {

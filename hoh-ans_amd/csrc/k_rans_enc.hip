@@ -21,7 +21,10 @@
 
 #define WIN 32
 
-__device__ __forceinline__ uint32_t plane_sid(int pi) { return (pi / 3) * SK_PER_TILE + SK_G + pi % 3; }
+// plane index -> stream: [0, 3*ntiles) the sub-green planes, then one indexed plane per tile
+__device__ __forceinline__ uint32_t plane_sid(int pi, int ntiles) {
+  return pi < 3 * ntiles ? (pi / 3) * SK_PER_TILE + SK_G + pi % 3 : (pi - 3 * ntiles) * SK_PER_TILE + SK_I;
+}
 
 __device__ __forceinline__ void lookup8(EncFast* e, uint4 sy, const EncFast* tab) {
   const uint32_t w[4] = {sy.x, sy.y, sy.z, sy.w};
@@ -81,7 +84,7 @@ __global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane) {
   const int lane = threadIdx.x;
   const int pi = blockIdx.x * LANES + lane;
   if (lane >= LANES || pi >= nplane) return;
-  const uint32_t sid = plane_sid(pi);
+  const uint32_t sid = plane_sid(pi, j.ntiles);
   StreamInfo st = j.streams[sid];
   if (!st.fast || st.mode != SM_RANS || st.err || st.n == 0) return;
   const uint32_t n = st.n;

@@ -33,8 +33,9 @@ extern "C" {
 #define HOH_E_UNREPRODUCIBLE 5  /* the reference writes uninitialised bytes for this input
                                    (grey non-binary tiles, choh.cpp:196-205; palette prefix
                                    longer than the indexed layer, choh.cpp:301-308)             */
-#define HOH_E_UNSUPPORTED 6     /* valid but not implemented on this path (palette tiles,
-                                   -s1..-s4 predictor search, 4-channel formats)                */
+#define HOH_E_UNSUPPORTED 6     /* valid but not implemented on this path (-s1..-s4 predictor
+                                   search, 4-channel formats); decoder: indexed (mode 127)
+                                   tiles, which carry no palette                   */
 #define HOH_E_CORRUPT 7         /* decoder: malformed or undecodable bitstream (incl. the
                                    reference's lossy raw tables)                     */
 #define HOH_E_NODEV 8           /* no GPU / HIP device unavailable                              */

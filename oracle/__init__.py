@@ -117,7 +117,9 @@ def ref_bin(name):
 # ------------------------------------------------------------------ numpy-level helpers (oracle)
 
 class OracleError(RuntimeError):
-    pass
+    def __init__(self, code):
+        self.code = int(code)
+        super().__init__("oracle error %d" % self.code)
 
 
 def encode_entropy(sym, rng, pb):

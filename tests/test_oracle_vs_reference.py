@@ -48,7 +48,7 @@ def test_lz_and_tiles_random_patterns():
         try:
             mine = O.encode_tile(img)
         except O.OracleError as e:
-            assert int(str(e)) == -4  # unreproducible in the reference (uninitialised bytes)
+            assert e.code == -4  # unreproducible in the reference (uninitialised bytes)
             continue
         assert mine == out[:r].tobytes(), it
 
@@ -60,3 +60,33 @@ def test_single_symbol_overrun():
                           (100000, 256, 16, 9), (65536, 1024, 12, 5), (1, 256, 8, 3), (3, 5, 12, 4)]:
         sym = np.full(n, v, np.uint16)
         assert O.encode_entropy(sym, rng, pb) == ref_encode(sym, rng, pb), (n, rng, pb)
+
+
+def test_palette_files_vs_reference_choh(tmp_path):
+    """whole files with palette tiles (choh.cpp:298-308, Q15) through the reference's own choh"""
+    import importlib.util
+    import os
+    import subprocess
+    exe = O.ref_bin("choh")
+    if exe is None:
+        pytest.skip("reference choh not built")
+    here = os.path.dirname(os.path.abspath(__file__))
+    spec = importlib.util.spec_from_file_location("tge", os.path.join(here, "test_gpu_encode.py"))
+    tge = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(tge)
+    n_ok = 0
+    for name, img in tge.palette_cases():
+        try:
+            mine, printed = O.choh(img)
+        except O.OracleError as e:
+            assert e.code == -4, name
+            continue
+        H, W, _ = img.shape
+        src, dst = tmp_path / (name + ".rgb"), tmp_path / (name + ".hoh")
+        src.write_bytes(np.ascontiguousarray(img).tobytes())
+        r = subprocess.run([exe, str(src), str(dst), str(W), str(H), "-s0"], capture_output=True, timeout=120)
+        assert r.returncode == 0, name
+        assert int(r.stdout.split()[-1]) == printed, name
+        assert dst.read_bytes() == mine, name
+        n_ok += 1
+    assert n_ok >= 4
