@@ -30,7 +30,7 @@ $(BINDIR)/%: tools/cli/%.cpp $(LIBDIR)/libhohgpu.so include/hoh_ans.h $(wildcard
 	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -o $@ $< -L$(LIBDIR) -lhohgpu -Wl,-rpath,'$$ORIGIN/../lib'
 
 oracle/liboracle.so: oracle/hoh_oracle.c oracle/hoh_oracle.h
-	gcc -O2 -shared -fPIC -o $@ oracle/hoh_oracle.c
+	gcc -O2 -shared -fPIC -o $@ oracle/hoh_oracle.c -lm
 
 clean:
 	rm -rf build $(LIBDIR)/libhohgpu.so oracle/liboracle.so $(BINDIR)

@@ -28,7 +28,7 @@ def build():
     so = os.path.join(HERE, "liboracle.so")
     src = os.path.join(HERE, "hoh_oracle.c")
     if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
-        subprocess.check_call(["gcc", "-O2", "-shared", "-fPIC", "-o", so, src])
+        subprocess.check_call(["gcc", "-O2", "-shared", "-fPIC", "-o", so, src, "-lm"])
     if os.path.isdir("/root/reference"):
         subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "ref")])
 
@@ -70,6 +70,16 @@ def lib():
         L.or_tile_bound.argtypes = [C.c_int, C.c_int]
         L.or_choh_s0.restype = C.c_long
         L.or_choh_s0.argtypes = [u8p, C.c_int, C.c_int, u8p, C.c_size_t, szp]
+        L.or_layer_encode.restype = C.c_long
+        L.or_layer_encode.argtypes = [u16p, C.c_size_t, C.c_int, C.c_int, C.c_int, C.c_int, u8p, u8p]
+        L.or_encode_tile.restype = C.c_long
+        L.or_encode_tile.argtypes = [u8p, C.c_int, C.c_int, C.c_int, u8p, C.c_size_t]
+        L.or_choh.restype = C.c_long
+        L.or_choh.argtypes = [u8p, C.c_int, C.c_int, C.c_int, u8p, C.c_size_t, szp]
+        L.or_predict_section.restype = C.c_size_t
+        L.or_predict_section.argtypes = [u16p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                         C.c_uint16, u16p]
+        L.or_predict_all.argtypes = [u16p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, u16p, u16p]
         L.or_choh_bound.restype = C.c_size_t
         L.or_choh_bound.argtypes = [C.c_int, C.c_int]
         L.or_dhoh.restype = C.c_long
@@ -96,6 +106,10 @@ def ref():
         R.ref_enc_put.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_int64)]
         R.ref_channelpredict_fastpath.argtypes = [u16p, C.c_int, C.c_int, C.c_int, u16p]
         R.ref_unpredict_all.argtypes = [u16p, C.c_int, C.c_int, C.c_int, C.c_uint16, u16p, u16p]
+        R.ref_channelpredict_section.restype = C.c_size_t
+        R.ref_channelpredict_section.argtypes = [u16p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                                 C.c_int, C.c_uint16, u16p]
+        R.ref_channelpredict_all.argtypes = [u16p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, u16p, u16p]
         R.ref_subtract_green.argtypes = [u8p, C.c_size_t, u16p, u16p, u16p]
         R.ref_count_colours.restype = C.c_int
         R.ref_count_colours.argtypes = [u8p, C.c_size_t]
@@ -183,30 +197,60 @@ def subtract_green(rgb):
     return G, R, B
 
 
-def encode_tile(rgb):
+def encode_tile(rgb, speed=0):
     rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
     h, w, _ = rgb.shape
     L = lib()
     cap = L.or_tile_bound(w, h)
     out = np.empty(cap, np.uint8)
-    r = L.or_encode_tile_s0(_p(rgb, u8p), w, h, _p(out, u8p), cap)
+    r = L.or_encode_tile(_p(rgb, u8p), w, h, speed, _p(out, u8p), cap)
     if r < 0:
         raise OracleError(r)
     return out[:r].tobytes()
 
 
-def choh(rgb):
-    """-> (file bytes, printed size) exactly as `choh in out W H -s0` (SURVEY Q13 included)."""
+def choh(rgb, speed=0):
+    """-> (file bytes, printed size) exactly as `choh in out W H -sN` (SURVEY Q13 included)."""
     rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
     H, W, _ = rgb.shape
     L = lib()
     cap = L.or_choh_bound(W, H)
     out = np.empty(cap, np.uint8)
     printed = C.c_size_t(0)
-    r = L.or_choh_s0(_p(rgb, u8p), W, H, _p(out, u8p), cap, C.byref(printed))
+    r = L.or_choh(_p(rgb, u8p), W, H, speed, _p(out, u8p), cap, C.byref(printed))
     if r < 0:
         raise OracleError(r)
     return out[:r].tobytes(), printed.value
+
+
+def predict_section(plane, depth, xt, yt, cx, cy, mask):
+    plane = np.ascontiguousarray(plane, dtype=np.uint16)
+    h, w = plane.shape
+    out = np.empty(w * h, np.uint16)
+    k = lib().or_predict_section(_p(plane, u16p), w, h, depth, xt, yt, cx, cy, mask, _p(out, u16p))
+    return out[:k].copy()
+
+
+def predict_all(plane, depth, xt, yt, tile_map):
+    plane = np.ascontiguousarray(plane, dtype=np.uint16)
+    tm = np.ascontiguousarray(tile_map, dtype=np.uint16)
+    h, w = plane.shape
+    out = np.empty(w * h, np.uint16)
+    lib().or_predict_all(_p(plane, u16p), w, h, depth, xt, yt, _p(tm, u16p), _p(out, u16p))
+    return out
+
+
+def layer_encode(plane, depth, speed, nuke=None):
+    plane = np.ascontiguousarray(plane, dtype=np.uint16)
+    h, w = plane.shape
+    n = w * h
+    L = lib()
+    out = np.empty(L.or_entropy_bound(n, 1 << depth, 31) + 4096, np.uint8)
+    nk = None if nuke is None else np.ascontiguousarray(nuke, dtype=np.uint8)
+    r = L.or_layer_encode(_p(plane, u16p), n, w, h, depth, speed, None if nk is None else _p(nk, u8p), _p(out, u8p))
+    if r < 0:
+        raise OracleError(r)
+    return out[:r].tobytes()
 
 
 def dhoh(data):

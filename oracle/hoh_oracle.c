@@ -1,13 +1,17 @@
 /*
  * hoh_oracle.c -- TEST INFRASTRUCTURE ONLY (see hoh_oracle.h).
  *
- * CPU restatement of the hoh-ANS -s0 encode path and a corrected decoder.  Written from the
+ * CPU restatement of the hoh-ANS encode path (-s0 and the -s1..-s4 predictor search) and a
+ * corrected decoder.  Written from the
  * reference's documented behaviour -- the reference's integer promotion
  * rules are reproduced explicitly where they change bytes (entropy_encoding.hpp:48,121).
- * Build: gcc -O2 -shared -fPIC -o oracle/liboracle.so oracle/hoh_oracle.c
+ * Build: gcc -O2 -shared -fPIC -o oracle/liboracle.so oracle/hoh_oracle.c -lm
+ * (glibc log2 and IEEE double sums in the reference's order: the -s>=1 cost estimate matches the
+ * reference's selection bit for bit)
  */
 #include "hoh_oracle.h"
 
+#include <math.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -432,6 +436,107 @@ long or_unpredict_fastpath(const uint16_t* res, size_t nres, const uint16_t* bac
   return (long)k;
 }
 
+/* predictor_operations.hpp:8-10, 66-68, 89-106 (uint16_t overloads) */
+static inline uint16_t midp16(uint16_t a, uint16_t b) { return (uint16_t)((int)a + ((int)b - (int)a) / 2); }
+static inline uint16_t avg3(uint16_t a, uint16_t b, uint16_t c) { return (uint16_t)(((int)a + (int)b + (int)c) / 3); }
+static inline uint16_t paeth16(uint16_t A, uint16_t B, uint16_t C) {
+  int p = (int)A + (int)B - (int)C;
+  int Ap = abs((int)A - p), Bp = abs((int)B - p), Cp = abs((int)C - p);
+  if (Ap < Bp) return Ap < Cp ? A : C;
+  return Bp < Cp ? B : C;
+}
+
+/* the 16 stock predictions (prediction.hpp:116-133 / :190-207; `all` passes paeth(L, TL, T)) */
+static void preds16(uint16_t L, uint16_t T, uint16_t TL, uint16_t TR, int all, uint16_t* p) {
+  p[0] = L; p[1] = T; p[2] = TL; p[3] = TR;
+  p[4] = med16(T, L, (uint16_t)(T + L - TL));
+  p[5] = midp16(L, T); p[6] = midp16(L, TL); p[7] = midp16(TL, T); p[8] = midp16(T, TR);
+  p[9] = all ? paeth16(L, TL, T) : paeth16(L, T, TL);
+  p[10] = avg3(L, L, TL); p[11] = avg3(L, TL, TL); p[12] = avg3(TL, TL, T);
+  p[13] = avg3(TL, T, T); p[14] = avg3(T, T, TR); p[15] = avg3(T, TR, TR);
+}
+
+/* argmin_j |v - p[j]| over the masked predictors, first minimum (prediction.hpp:138-146) */
+static inline int best_pred(uint16_t v, const uint16_t* p, uint16_t mask, int c) {
+  int bv = 2 * c, b = 0;
+  for (int j = 0; j < 16; j++) {
+    int d = abs((int)v - (int)p[j]);
+    if (d < bv && (mask & (1u << j))) { bv = d; b = j; }
+  }
+  return b;
+}
+
+/* prediction.hpp:46-151 (channelpredict_section): residuals of cell (cx, cy) of an xt x yt grid in
+ * raster order within the cell; returns the count.  Reproduces the cell-local top row (read from
+ * the row above the cell, wrapping into the cell's own row past the right edge), the TR wrap to
+ * top_row[0] and best_pred reset to 4 per cell. */
+size_t or_predict_section(const uint16_t* d, int w, int h, int depth, int xt, int yt, int cx, int cy,
+                          uint16_t mask, uint16_t* out) {
+  if (mask == 0x0010 && xt == 1 && yt == 1 && cx == 0 && cy == 0) {
+    or_predict_fastpath(d, w, h, depth, out);
+    return (size_t)w * h;
+  }
+  int c = 1 << depth, half = c / 2;
+  int tw = (w + xt - 1) / xt, th = (h + yt - 1) / yt;
+  int x0 = cx * tw, y0 = cy * th;
+  int* bp = (int*)malloc(sizeof(int) * tw);
+  uint16_t* top = (uint16_t*)malloc(2 * (size_t)tw);
+  for (int i = 0; i < tw; i++) {
+    bp[i] = 4;
+    top[i] = cy ? d[(long)y0 * w + x0 + i - w] : (uint16_t)half;
+  }
+  size_t k = 0;
+  for (int ym = 0; ym < th && y0 + ym < h; ym++) {
+    uint16_t L, TL;
+    if (cx) {
+      L = d[(long)(y0 + ym) * w + x0 - 1];
+      TL = (ym || cy) ? d[(long)(y0 + ym - 1) * w + x0 - 1] : (uint16_t)half;
+    } else {
+      L = TL = (uint16_t)half;
+    }
+    for (int xm = 0; xm < tw && x0 + xm < w; xm++) {
+      long loc = (long)(y0 + ym) * w + x0 + xm;
+      uint16_t T = top[xm], TR = top[(xm + tw + 1) % tw], p[16];
+      preds16(L, T, TL, TR, 0, p);
+      out[k++] = (uint16_t)(((int)d[loc] - (int)midp16(p[bp[xm]], p[bp[(xm + tw - 1) % tw]]) + half + c) % c);
+      TL = top[xm];
+      top[xm] = d[loc];
+      L = d[loc];
+      bp[xm] = best_pred(d[loc], p, mask, c);
+    }
+  }
+  free(bp);
+  free(top);
+  return k;
+}
+
+/* prediction.hpp:153-229 (channelpredict_all): whole plane with a predictor mask per cell; the
+ * best predictor of row y+1 is chosen with row y+1's cell mask, and the last row keeps 0. */
+void or_predict_all(const uint16_t* d, int w, int h, int depth, int xt, int yt, const uint16_t* map,
+                    uint16_t* out) {
+  int c = 1 << depth, half = c / 2;
+  int tw = (w + xt - 1) / xt, th = (h + yt - 1) / yt;
+  int* bp = (int*)malloc(sizeof(int) * w);
+  uint16_t* top = (uint16_t*)malloc(2 * (size_t)w);
+  for (int i = 0; i < w; i++) { bp[i] = 4; top[i] = (uint16_t)half; }
+  for (int y = 0; y < h; y++) {
+    uint16_t L = (uint16_t)half, TL = (uint16_t)half;
+    for (int x = 0; x < w; x++) {
+      long loc = (long)y * w + x;
+      uint16_t T = top[x], TR = top[(x + w + 1) % w], p[16];
+      preds16(L, T, TL, TR, 1, p);
+      out[loc] = (uint16_t)(((int)d[loc] - (int)midp16(p[bp[x]], p[bp[(x + w - 1) % w]]) + half + c) % c);
+      TL = top[x];
+      top[x] = d[loc];
+      L = d[loc];
+      bp[x] = 0;
+      if (y + 1 < h) bp[x] = best_pred(d[loc], p, map[((y + 1) / th) * xt + x / tw], c);
+    }
+  }
+  free(bp);
+  free(top);
+}
+
 /* ------------------------------------------------------------------ colour */
 
 void or_subtract_green(const uint8_t* s, size_t npix, uint16_t* G, uint16_t* R, uint16_t* B) {
@@ -549,38 +654,149 @@ out:
 
 /* ------------------------------------------------------------------ layer / tile / file */
 
-/* layer_encode.hpp:11-412 with cruncher_mode 0 */
-long or_layer_encode_s0(const uint16_t* data, size_t n, int w, int h, int depth, const uint8_t* nuke,
-                        uint8_t* out) {
+/* stock predictor masks of the -s>=1 search (layer_encode.hpp:159-175) */
+static const uint16_t kMasks[14] = {0x0001, 0x0002, 0x0020, 0x0010, 0xffbf, 0x0003, 0xfffd,
+                                    0xfffb, 0xfff7, 0xffef, 0xffdf, 0xff7f, 0xfdff, 0xffff};
+
+/* layer_encode.hpp:133-147: -log2((1 + count) / n) per symbol, counts over all n residuals */
+static void entropy_table(const uint16_t* res, size_t n, int range, double* ent) {
+  int* fr = (int*)malloc(sizeof(int) * range);
+  for (int i = 0; i < range; i++) fr[i] = 1;
+  for (size_t i = 0; i < n; i++) fr[res[i]]++;
+  for (int i = 0; i < range; i++) ent[i] = -log2((double)fr[i] / (double)n);
+  free(fr);
+}
+
+/* layer_encode.hpp:176-203: per cell, the first stock mask of least estimated cost */
+static void search_cells(const uint16_t* d, int w, int h, int depth, int xt, int yt, int npred,
+                         const double* ent, uint16_t* plist, uint8_t* pidx, uint16_t* scratch) {
+  for (int i = 0; i < xt * yt; i++) {
+    double best = 99999999999.0;
+    for (int pr = 0; pr < npred; pr++) {
+      size_t k = or_predict_section(d, w, h, depth, xt, yt, i % xt, i / xt, kMasks[pr], scratch);
+      double cost = 0;
+      for (size_t v = 0; v < k; v++) cost += ent[scratch[v]];
+      if (cost < best) { best = cost; plist[i] = kMasks[pr]; pidx[i] = (uint8_t)pr; }
+    }
+  }
+}
+
+/* layer_encode.hpp:11-412.  cruncher 0: MED fast path, prob_bits 15.  cruncher >= 1: 40-px grid
+ * predictor search (5 / 10 / 14 masks), refined once at cruncher > 2, predictor map stream, then
+ * prob_bits 16 vs 15 and three more prob_bits in that direction; the output is `possible_size`
+ * bytes of the `permanent` buffer, which is not swapped for the 16/15 pair (Q14), so it may be a
+ * prefix of an older stream. */
+long or_layer_encode(const uint16_t* data, size_t n, int w, int h, int depth, int cruncher,
+                     const uint8_t* nuke, uint8_t* out) {
   size_t oi = 0;
   size_t possible = ((size_t)depth * n + ((size_t)depth * n) % 8 + 1024) / 8;   /* :22 */
+  const int range = 1 << depth;
   out[oi++] = 0x10;                                                 /* :57 */
   uint16_t* res = (uint16_t*)malloc((n ? n : 1) * 2);
   uint16_t* clean = (uint16_t*)malloc((n ? n : 1) * 2);
   or_predict_fastpath(data, w, h, depth, res);                      /* :63-75 */
   size_t nc = 0;
   for (size_t i = 0; i < n; i++) if (!nuke || !nuke[i]) clean[nc++] = res[i];   /* :93-99 */
-  uint8_t* tmp = (uint8_t*)malloc(or_entropy_bound(nc, 1u << depth, 15));
-  long sz = or_encode_entropy(clean, nc, 1u << depth, 15, tmp);     /* :106-113 */
-  free(res);
-  free(clean);
-  if (sz < 0) { free(tmp); return sz; }
-  if ((size_t)sz >= possible) { free(tmp); return OR_E_UNREPRODUCIBLE; }  /* copies garbage */
-  out[oi++] = 0; out[oi++] = 0; out[oi++] = 0x00; out[oi++] = 0x10; /* :320-325 */
-  memcpy(out + oi, tmp, (size_t)sz);
-  oi += (size_t)sz;
-  free(tmp);
-  return (long)oi;
+  const size_t cap = or_entropy_bound(nc, (size_t)range, 31);
+  uint8_t* bufa = (uint8_t*)malloc(cap);
+  uint8_t* bufb = (uint8_t*)malloc(cap);
+  uint8_t* dummy = bufa;                                            /* dummyrand (:103) */
+  uint8_t* perm = bufb;                                             /* permanent (:104) */
+  int valid = 0;                                                    /* perm holds a stream */
+  long r = or_encode_entropy(clean, nc, (size_t)range, 15, dummy);  /* :106-113 */
+  if (r < 0) goto fail;
+  if ((size_t)r < possible) {                                       /* :115-120 */
+    possible = (size_t)r;
+    uint8_t* x = perm; perm = dummy; dummy = x;
+    valid = 1;
+  }
+  if (cruncher && ((w + 39) / 40 > 1 || (h + 39) / 40 > 1)) {       /* :124-132 */
+    int xt = (w + 39) / 40, yt = (h + 39) / 40, T = xt * yt;
+    int npred = cruncher * 5 < 14 ? (int)cruncher * 5 : 14;
+    double* ent = (double*)malloc(sizeof(double) * range);
+    uint16_t* plist = (uint16_t*)malloc(2 * (size_t)T);
+    uint8_t* pidx = (uint8_t*)malloc((size_t)T);
+    uint16_t* scratch = (uint16_t*)malloc((n ? n : 1) * 2);
+    entropy_table(res, n, range, ent);
+    search_cells(data, w, h, depth, xt, yt, npred, ent, plist, pidx, scratch);
+    or_predict_all(data, w, h, depth, xt, yt, plist, res);          /* :205-214 */
+    if (cruncher > 2) {                                             /* :215-272 */
+      entropy_table(res, n, range, ent);
+      search_cells(data, w, h, depth, xt, yt, npred, ent, plist, pidx, scratch);
+      or_predict_all(data, w, h, depth, xt, yt, plist, res);
+    }
+    out[oi++] = (uint8_t)(xt - 1);                                  /* :276-277 */
+    out[oi++] = (uint8_t)(yt - 1);
+    int used[14] = {0}, nused = 0, map[14];
+    for (int i = 0; i < T; i++) used[pidx[i]] = 1;
+    for (int j = 0; j < 14; j++) nused += used[j];
+    out[oi++] = (uint8_t)nused;                                     /* :291-297 */
+    for (int j = 0, k = 0; j < 14; j++) {
+      if (!used[j]) continue;
+      out[oi++] = (uint8_t)(kMasks[j] >> 8);
+      out[oi++] = (uint8_t)(kMasks[j] % 256);
+      map[j] = k++;
+    }
+    for (int i = 0; i < T; i++) scratch[i] = (uint16_t)map[pidx[i]];
+    long m = or_encode_entropy(scratch, (size_t)T, (size_t)nused, 8, out + oi);   /* :308-317 */
+    free(ent); free(plist); free(pidx); free(scratch);
+    if (m < 0) { r = m; goto fail; }
+    oi += (size_t)m;
+  } else {
+    out[oi++] = 0; out[oi++] = 0; out[oi++] = 0x00; out[oi++] = 0x10;   /* :320-325 */
+  }
+  if (cruncher) {                                                   /* :326-392 */
+    nc = 0;
+    for (size_t i = 0; i < n; i++) if (!nuke || !nuke[i]) clean[nc++] = res[i];
+    long t1 = or_encode_entropy(clean, nc, (size_t)range, 16, dummy);
+    long t2 = t1 < 0 ? t1 : or_encode_entropy(clean, nc, (size_t)range, 15, dummy);
+    if (t2 < 0) { r = t2; goto fail; }
+    int pb0 = t1 < t2 ? 17 : 14, step = t1 < t2 ? 1 : -1;
+    long t12 = t1 < t2 ? t1 : t2;
+    if ((size_t)t12 < possible) possible = (size_t)t12;            /* no swap (Q14) */
+    for (int k = 0; k < 3; k++) {
+      long t = or_encode_entropy(clean, nc, (size_t)range, (uint32_t)(pb0 + step * k), dummy);
+      if (t < 0) { r = t; goto fail; }
+      if ((size_t)t < possible) {
+        possible = (size_t)t;
+        uint8_t* x = perm; perm = dummy; dummy = x;
+        valid = 1;
+      }
+    }
+  }
+  if (!valid) { r = OR_E_UNREPRODUCIBLE; goto fail; }               /* copies garbage */
+  memcpy(out + oi, perm, possible);                                 /* :396-398 */
+  oi += possible;
+  r = (long)oi;
+fail:
+  free(res); free(clean); free(bufa); free(bufb);
+  return r;
 }
 
-/* worst case of one tile: three stored planes (<= 9/8 B per pixel each), three LZ streams */
+long or_layer_encode_s0(const uint16_t* data, size_t n, int w, int h, int depth, const uint8_t* nuke,
+                        uint8_t* out) {
+  return or_layer_encode(data, n, w, h, depth, 0, nuke, out);
+}
+
+/* bytes a layer can take: the larger of the -s0 bound and the -s>=1 header + table + payload */
+static size_t layer_bound(size_t n, int depth) {
+  return or_entropy_bound(n, (size_t)1 << depth, 31) + 2 * 14 + 3 + or_entropy_bound(256, 14, 8) + 16;
+}
+
+/* worst case of one tile: stored planes (<= 9/8 B per pixel each, five planes at -s>=3) and the
+ * LZ streams */
 size_t or_tile_bound(int w, int h) {
   size_t npix = (size_t)w * h;
-  return 5 * npix + 4096;
+  return 8 * npix + 16384;
 }
 
-/* choh.cpp:104-383, cruncher_mode 0 */
-long or_encode_tile_s0(const uint8_t* s, int w, int h, uint8_t* out, size_t cap) {
+/* choh.cpp:125-137 */
+static int seek_distance(int cruncher) {
+  return cruncher == 1 ? 10 : cruncher == 2 ? 11 : cruncher == 3 ? 12 : cruncher == 4 ? 14 : 6;
+}
+
+/* choh.cpp:104-383 */
+long or_encode_tile(const uint8_t* s, int w, int h, int cruncher, uint8_t* out, size_t cap) {
   size_t npix = (size_t)w * h, size = npix * 3, o = 0;
   if (cap < or_tile_bound(w, h)) return OR_E_CAP;
   out[o++] = 0; out[o++] = 0;                                       /* :115-116 */
@@ -595,7 +811,7 @@ long or_encode_tile_s0(const uint8_t* s, int w, int h, uint8_t* out, size_t cap)
     else if (cc <= 16) bonus = 10;
     else if (cc <= 32) bonus = 2;
   }
-  long lzn = or_find_lz_rgb(s, size, w, h, lz, nuke, 6, bonus);     /* :156-165 */
+  long lzn = or_find_lz_rgb(s, size, w, h, lz, nuke, seek_distance(cruncher), bonus);   /* :156-165 */
   if (lzn < 0) { ret = lzn; goto done; }
   int grey = 1;
   for (size_t i = 0; i < size; i += 3)                              /* channel.hpp:21-31 */
@@ -620,18 +836,32 @@ long or_encode_tile_s0(const uint8_t* s, int w, int h, uint8_t* out, size_t cap)
     uint16_t* G = (uint16_t*)malloc(npix * 2);
     uint16_t* R = (uint16_t*)malloc(npix * 2);
     uint16_t* B = (uint16_t*)malloc(npix * 2);
-    size_t pb_ = or_entropy_bound(npix, 512, 15) + 64;
+    size_t pb_ = layer_bound(npix, 9);
     uint8_t* c1 = (uint8_t*)malloc(pb_);
     uint8_t* c2 = (uint8_t*)malloc(pb_);
     uint8_t* c3 = (uint8_t*)malloc(pb_);
+    uint8_t* a2 = (uint8_t*)malloc(pb_);
+    uint8_t* a3 = (uint8_t*)malloc(pb_);
+    uint8_t* ci = (uint8_t*)malloc(pb_);
     or_subtract_green(s, npix, G, R, B);                            /* :215-219 */
-    long s1 = or_layer_encode_s0(G, npix, w, h, 8, nuke, c1);
-    long s2 = s1 < 0 ? s1 : or_layer_encode_s0(R, npix, w, h, 9, nuke, c2);
-    long s3 = s2 < 0 ? s2 : or_layer_encode_s0(B, npix, w, h, 9, nuke, c3);
+    long s1 = or_layer_encode(G, npix, w, h, 8, cruncher, nuke, c1);
+    long s2 = s1 < 0 ? s1 : or_layer_encode(R, npix, w, h, 9, cruncher, nuke, c2);
+    long s3 = s2 < 0 ? s2 : or_layer_encode(B, npix, w, h, 9, cruncher, nuke, c3);
+    long sr = -1, sb = -1;
+    if (s3 >= 0 && cruncher > 2) {                                  /* :265-293 plain R and B */
+      for (size_t i = 0; i < npix; i++) { R[i] = s[3 * i]; B[i] = s[3 * i + 2]; }
+      sr = or_layer_encode(R, npix, w, h, 8, cruncher, nuke, a2);
+      sb = sr < 0 ? sr : or_layer_encode(B, npix, w, h, 8, cruncher, nuke, a3);
+      if (sb < 0) s3 = sb;
+    }
     if (s3 < 0) { ret = s3; }
     else {
       long best = s1 + s2 + s3 + lzn;                               /* :295 */
-      int palette = 0;
+      int mode = 128, chn = 3, ch1_indexed = 0;
+      long si = -1;
+      size_t z2 = (size_t)s2, z3 = (size_t)s3;
+      const uint8_t *p2 = c2, *p3 = c3;
+      ret = 0;
       if (cc != -1) {                                               /* :298-308 palette_encode */
         uint16_t* idx = (uint16_t*)malloc(npix * 2);
         uint32_t pal[256];
@@ -643,41 +873,48 @@ long or_encode_tile_s0(const uint8_t* s, int w, int h, uint8_t* out, size_t cap)
           if (j == k) pal[k++] = v;
           idx[i] = (uint16_t)j;
         }
-        uint8_t* ci = (uint8_t*)malloc(pb_);
-        long si = or_layer_encode_s0(idx, npix, w, h, 8, nuke, ci);
-        if (si >= 0 && si + 3 * k + 1 + lzn < best) palette = 1;
-        if (palette) {
-          /* mode 127 copies channel_size1 (the GREEN layer's size) bytes of the indexed
-           * layer and no palette (Q15); reproducible only as a prefix */
-          if (s1 > si) ret = OR_E_UNREPRODUCIBLE;
-          else {
-            out[o++] = 127;
-            memcpy(out + o, lz, (size_t)lzn); o += (size_t)lzn;
-            memcpy(out + o, ci, (size_t)s1); o += (size_t)s1;
-            ret = (long)o;
-          }
-        }
-        free(ci);
+        si = or_layer_encode(idx, npix, w, h, 8, cruncher, nuke, ci);
         free(idx);
+        if (si < 0) ret = si;
+        else if (si + 3 * k + 1 + lzn < best) {
+          best = si + 3 * k + 1 + lzn;
+          mode = 127; chn = 1; ch1_indexed = 1;
+        }
       }
-      if (!palette) {
-        out[o++] = 128;                                             /* :296, :328 */
+      if (ret == 0 && sr >= 0 && sr + s1 + sb + lzn < best) {       /* :309-325 */
+        mode = 2; chn = 3;
+        z2 = (size_t)sr; z3 = (size_t)sb; p2 = a2; p3 = a3;
+      }
+      /* channel_compressed1 is the indexed layer once the palette has won (:305-307), but its
+       * size stays the GREEN layer's (Q15): reproducible only as a prefix */
+      if (ret == 0 && ch1_indexed && s1 > si) ret = OR_E_UNREPRODUCIBLE;
+      if (ret == 0) {
+        const uint8_t* p1 = ch1_indexed ? ci : c1;
+        out[o++] = (uint8_t)mode;                                   /* :328 */
         memcpy(out + o, lz, (size_t)lzn); o += (size_t)lzn;         /* :329-331 */
-        out[o++] = 0x24;                                            /* :352 */
-        o = or_write_varint(out, o, (size_t)s1);
-        o = or_write_varint(out, o, (size_t)s2);
-        memcpy(out + o, c1, (size_t)s1); o += (size_t)s1;
-        memcpy(out + o, c2, (size_t)s2); o += (size_t)s2;
-        memcpy(out + o, c3, (size_t)s3); o += (size_t)s3;
+        if (chn == 1) {
+          memcpy(out + o, p1, (size_t)s1); o += (size_t)s1;         /* :335-338 */
+        } else {
+          out[o++] = 0x24;                                          /* :351-363 */
+          o = or_write_varint(out, o, (size_t)s1);
+          o = or_write_varint(out, o, z2);
+          memcpy(out + o, p1, (size_t)s1); o += (size_t)s1;
+          memcpy(out + o, p2, z2); o += z2;
+          memcpy(out + o, p3, z3); o += z3;
+        }
         ret = (long)o;
       }
     }
-    free(G); free(R); free(B); free(c1); free(c2); free(c3);
+    free(G); free(R); free(B); free(c1); free(c2); free(c3); free(a2); free(a3); free(ci);
   }
 done:
   free(nuke);
   free(lz);
   return ret;
+}
+
+long or_encode_tile_s0(const uint8_t* s, int w, int h, uint8_t* out, size_t cap) {
+  return or_encode_tile(s, w, h, 0, out, cap);
 }
 
 int or_tiling(int W, int H, int* xt, int* yt, int* tw, int* th) {
@@ -700,8 +937,8 @@ size_t or_choh_bound(int W, int H) {
   return 64 + (size_t)xt * yt * 3 + 5 * (size_t)W * H + (size_t)xt * yt * 4096;
 }
 
-/* choh.cpp:394-527, -s0 */
-long or_choh_s0(const uint8_t* rgb, int W, int H, uint8_t* out, size_t cap, size_t* printed) {
+/* choh.cpp:394-527 (speed = the -sN argument) */
+long or_choh(const uint8_t* rgb, int W, int H, int speed, uint8_t* out, size_t cap, size_t* printed) {
   if (W <= 0 || H <= 0) return OR_E_ARG;
   if (cap < 64) return OR_E_CAP;
   size_t o = 0;
@@ -729,7 +966,7 @@ long or_choh_s0(const uint8_t* rgb, int W, int H, uint8_t* out, size_t cap, size
       if (H - yo < nh) nh = H - yo;
       for (int y = 0; y < nh; y++)
         memcpy(trgb + (size_t)y * nw * 3, rgb + ((size_t)(y + yo) * W + xo) * 3, (size_t)nw * 3);
-      long r = or_encode_tile_s0(trgb, nw, nh, tbuf, tcap);
+      long r = or_encode_tile(trgb, nw, nh, speed, tbuf, tcap);
       if (r < 0) { ret = r; break; }
       sizes[i] = (size_t)r;
       tiles[i] = (uint8_t*)malloc((size_t)r);
@@ -750,13 +987,17 @@ long or_choh_s0(const uint8_t* rgb, int W, int H, uint8_t* out, size_t cap, size
     /* :508-520 -- the tile is encoded and discarded (Q13) */
     size_t tcap = or_tile_bound(W, H);
     uint8_t* t = (uint8_t*)malloc(tcap);
-    long r = or_encode_tile_s0(rgb, W, H, t, tcap);
+    long r = or_encode_tile(rgb, W, H, speed, t, tcap);
     free(t);
     if (r < 0) return r;
     tile_size = (size_t)r;
   }
   if (printed) *printed = o + tile_size;                            /* :522 */
   return (long)o;
+}
+
+long or_choh_s0(const uint8_t* rgb, int W, int H, uint8_t* out, size_t cap, size_t* printed) {
+  return or_choh(rgb, W, H, 0, out, cap, printed);
 }
 
 /* ------------------------------------------------------------------ decoder (corrected) */

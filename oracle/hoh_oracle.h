@@ -73,6 +73,17 @@ int or_count_colours(const uint8_t* rgb, size_t size);
 long or_find_lz_rgb(const uint8_t* rgb, size_t size, int w, int h, uint8_t* lz_out, uint8_t* nuke,
                     int distance, int bonus);
 
+/* prediction.hpp:46-151 / :153-229 (the -s>=1 predictors); section returns the cell's count */
+size_t or_predict_section(const uint16_t* data, int w, int h, int depth, int xt, int yt, int cx, int cy,
+                          uint16_t mask, uint16_t* out);
+void or_predict_all(const uint16_t* data, int w, int h, int depth, int xt, int yt, const uint16_t* map,
+                    uint16_t* out);
+/* layer_encode.hpp:11-412 / choh.cpp:104-383 / choh.cpp:394-527 at any cruncher_mode (-sN) */
+long or_layer_encode(const uint16_t* data, size_t n, int w, int h, int depth, int cruncher,
+                     const uint8_t* nuke, uint8_t* out);
+long or_encode_tile(const uint8_t* rgb, int w, int h, int cruncher, uint8_t* out, size_t cap);
+long or_choh(const uint8_t* rgb, int W, int H, int speed, uint8_t* out, size_t cap, size_t* printed);
+
 /* layer_encode.hpp:11-412, cruncher_mode 0 */
 long or_layer_encode_s0(const uint16_t* data, size_t n, int w, int h, int depth, const uint8_t* nuke,
                         uint8_t* out);

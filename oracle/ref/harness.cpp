@@ -80,6 +80,24 @@ void ref_unpredict_all(const uint16_t* res, int w, int h, int depth, uint16_t pr
   delete[] r;
 }
 
+size_t ref_channelpredict_section(const uint16_t* data, int w, int h, int depth, int xt, int yt, int cx,
+                                  int cy, uint16_t mask, uint16_t* out) {
+  size_t bs = 0;
+  uint16_t* r = channelpredict_section((uint16_t*)data, (size_t)w * h, w, h, depth, xt, yt, cx, cy, mask,
+                                       &bs);                     // prediction.hpp:46
+  memcpy(out, r, bs * 2);
+  delete[] r;
+  return bs;
+}
+
+void ref_channelpredict_all(const uint16_t* data, int w, int h, int depth, int xt, int yt,
+                            const uint16_t* tile_map, uint16_t* out) {
+  uint16_t* r = channelpredict_all((uint16_t*)data, (size_t)w * h, w, h, depth, xt, yt,
+                                   (uint16_t*)tile_map);          // prediction.hpp:153
+  memcpy(out, r, (size_t)w * h * 2);
+  delete[] r;
+}
+
 void ref_subtract_green(const uint8_t* rgb, size_t npix, uint16_t* G, uint16_t* R, uint16_t* B) {
   subtract_green((uint8_t*)rgb, npix * 3, G, R, B);                // channel.hpp:73
 }
