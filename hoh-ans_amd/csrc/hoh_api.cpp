@@ -266,6 +266,8 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
     const char* e = getenv("HOH_ENC_DBG");
     j.dbg = e ? (uint32_t)atoi(e) : 0;
   }
+  j.speed = 0;
+  j.spt = SK_PER_TILE;
   j.rgb = d_rgb; j.W = W; j.H = H;
   j.xt = xt; j.yt = yt; j.tw = tw; j.th = th;
   j.t0 = t0; j.ntiles = ntiles;
@@ -316,9 +318,10 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   prof.mark("memset");
   launch_front(j, s);            prof.mark("front");
   launch_palette(j, s);          prof.mark("palette");
-  launch_lz(j, s);               prof.mark("lz");
+  launch_lz(j, s);
+  launch_nuke(j, s);             prof.mark("lz");
   launch_tables(j, (int)S, s);   prof.mark("tables");
-  launch_rans_fast(j, nullptr, ntiles * 4, s); prof.mark("rans_enc_fast");
+  launch_rans_fast(j, ntiles * 4, s, SidMap{3, SK_G}, ntiles * 3, SidMap{1, SK_I}); prof.mark("rans_enc_fast");
   launch_rans_gen(j, (int)S, s); prof.mark("rans_enc_gen");
   launch_finalize(j, (int)S, s); prof.mark("finalize");
   launch_layout(j, s);           prof.mark("layout");
@@ -466,6 +469,7 @@ int encode_streams_impl(hoh_ctx* c, const uint16_t* d_syms, const uint64_t* off,
   j.total = (uint64_t*)((uint8_t*)c->misc.p + 8);
   j.out = d_out;
   j.cap = ~0ull;
+  j.spt = 1;
   if (hipMemcpyAsync(c->streams.p, st.data(), st.size() * sizeof(StreamInfo), hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;
   if (hipMemsetAsync(c->misc.p, 0, 64, s) != hipSuccess) return HOH_E_HIP;
   launch_tables(j, nstreams, s);

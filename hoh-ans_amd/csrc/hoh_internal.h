@@ -17,6 +17,32 @@
 enum { SK_LZ_FUTURE = 0, SK_LZ_LENGTH = 1, SK_LZ_BACKBY = 2, SK_G = 3, SK_R = 4, SK_B = 5, SK_I = 6,
        SK_PER_TILE = 7 };
 
+// -s1..-s4 stream kinds (stream id = tile * SPT_S + kind).  Planes p: 0 G, 1 R', 2 B' (sub-green),
+// 3 indexed (palette candidates), 4 R, 5 B (plain, -s>=3 RGB mode, choh.cpp:265-293)
+enum { KS_LZ = 0,          // 4 LZ streams (lz.hpp:100-142, backby2 at distance > 8)
+       KS_MED = 4,         // + p: MED fast-path residuals at prob_bits 15 (layer_encode.hpp:106-120)
+       KS_FIN = 10,        // + p: searched residuals at the winning prob_bits (full encode)
+       KS_MAP = 16,        // + p: predictor map stream (layer_encode.hpp:308-317)
+       KS_VAR = 22,        // + p * 8 + v: searched residuals, size-only, prob_bits kVarPb[v]
+       SPT_S = 70 };
+#define HOH_NPLANE_S 6
+#define HOH_MAPCAP 176     // cells of the 40-px grid: ceil(511 / 40)^2 = 169, rounded to 8
+
+struct PlaneInfo {         // one -s>=1 layer (layer_encode.hpp:11-412)
+  uint32_t present;
+  uint32_t depth;
+  uint32_t xt, yt;         // predictor grid (0 = no grid: 00 00 00 10 header)
+  uint32_t used;           // distinct masks used
+  uint32_t used_bits;      // bit j: stock mask j used
+  uint32_t fixed_len;      // 0x10 + fixed header bytes before the map stream
+  uint32_t possible;       // bytes of the permanent buffer that reach the layer
+  uint32_t perm_final;     // 1: the permanent buffer is the KS_FIN stream, 0: KS_MED (prefix)
+  uint32_t valid;          // 0: permanent holds uninitialised bytes
+  uint32_t size;           // layer bytes
+  uint32_t limit;          // bytes of this layer that reach the tile (Q15 prefix), else size
+  uint64_t out_off;        // file offset of the layer
+};
+
 // stream coding modes (entropy_encoding.hpp)
 enum { SM_EMPTY = 0, SM_RANS = 1, SM_STORED = 2 };
 
@@ -51,6 +77,8 @@ struct StreamInfo {
   uint32_t ckpt_off;      // index of the first checkpoint of this stream
   uint32_t drop;          // coded but not part of the file (losing colour mode)
   uint32_t clip;          // nonzero: only the first clip bytes go to the file (Q15 prefix)
+  uint32_t sizeonly;      // rANS state chain only: words counted, none stored
+  uint32_t hist_src;      // 0: count the symbols; k + 1: the histogram of stream k
 };
 
 struct TileInfo {
@@ -118,12 +146,20 @@ struct EncodeJob {
   uint32_t npix_cap;      // max pixels of one tile (per-plane stride of the residual arena)
   uint32_t lz_cap;        // symbols per LZ stream slot
   uint32_t dbg;           // measurement knobs (HOH_ENC_DBG), 0 in production
+  int speed;              // cruncher_mode (-sN)
+  int spt;                // streams per tile: SK_PER_TILE (-s0) or SPT_S
   // arenas
   uint16_t* sym;          // residual planes + LZ symbols
   uint32_t* hist;         // [stream][512]
   uint64_t* candbits;     // [tile][npix_cap/64] LZ candidate bitmap
   uint32_t* matches;      // [tile][lz_cap] packed (pos, len, back) triples (3 words each)
   uint32_t* palette;      // [tile][256] colours in first-occurrence order (palette tiles)
+  uint8_t* idx8;          // -s>=1: [tile][npix_cap] palette indices (the indexed plane's data)
+  uint32_t* fpb;          // -s>=1: [tile][npix_cap] 4-pixel window fingerprints (LZ)
+  PlaneInfo* pinfo;       // -s>=1: [tile][6]
+  const double* lg;       // -s>=1: -log2(k / n) for k = 0..n+1, one table per tile pixel count
+  uint32_t lg_n[4];
+  uint64_t lg_off[4];
   StreamInfo* streams;    // [ntiles * SK_PER_TILE]
   TileInfo* tiles;        // [ntiles]
   uint8_t* hdr;           // [stream][HOH_HDR_CAP]
@@ -150,13 +186,57 @@ __host__ __device__ inline size_t idx_slab_off(const EncodeJob& j, int t) {
   return (size_t)j.ntiles * 3 * (j.npix_cap + 8 + j.lz_cap + 8) + (size_t)t * (j.npix_cap + 8);
 }
 
+// MED residual plane p of tile t and the kind of its stream / histogram
+__host__ __device__ inline size_t med_plane_off(const EncodeJob& j, int t, int p) {
+  if (j.speed == 0) return p < 3 ? (size_t)(t * 3 + p) * j.npix_cap : idx_plane_off(j, t);
+  return (size_t)(t * HOH_NPLANE_S + p) * j.npix_cap;
+}
+__host__ __device__ inline int med_kind(const EncodeJob& j, int p) { return (j.speed == 0 ? SK_G : KS_MED) + p; }
+
+// -s>=1 arenas: sym = [t][6] MED | [t][6] searched | [t][4][lz_cap] LZ | [t][6][MAPCAP] maps;
+// slabs = [t][6] planes | [t][4] LZ | [t][6] maps
+__host__ __device__ inline size_t fin_plane_off(const EncodeJob& j, int t, int p) {
+  return (size_t)j.ntiles * HOH_NPLANE_S * j.npix_cap + (size_t)(t * HOH_NPLANE_S + p) * j.npix_cap;
+}
+__host__ __device__ inline size_t lz_sym_off_s(const EncodeJob& j, int t, int k) {
+  return (size_t)j.ntiles * 2 * HOH_NPLANE_S * j.npix_cap + (size_t)(t * 4 + k) * j.lz_cap;
+}
+__host__ __device__ inline size_t map_sym_off(const EncodeJob& j, int t, int p) {
+  return (size_t)j.ntiles * (2 * HOH_NPLANE_S * (size_t)j.npix_cap + 4 * (size_t)j.lz_cap) +
+         (size_t)(t * HOH_NPLANE_S + p) * HOH_MAPCAP;
+}
+__host__ __device__ inline size_t sym_total_s(int ntiles, uint32_t npix_cap, uint32_t lz_cap) {
+  return (size_t)ntiles * (2 * HOH_NPLANE_S * (size_t)npix_cap + 4 * (size_t)lz_cap + HOH_NPLANE_S * HOH_MAPCAP);
+}
+__host__ __device__ inline size_t plane_slab_off_s(const EncodeJob& j, int t, int p) {
+  return (size_t)(t * HOH_NPLANE_S + p) * (j.npix_cap + 8);
+}
+__host__ __device__ inline size_t lz_slab_off_s(const EncodeJob& j, int t, int k) {
+  return (size_t)j.ntiles * HOH_NPLANE_S * (j.npix_cap + 8) + (size_t)(t * 4 + k) * (j.lz_cap + 8);
+}
+__host__ __device__ inline size_t map_slab_off_s(const EncodeJob& j, int t, int p) {
+  return (size_t)j.ntiles * (HOH_NPLANE_S * ((size_t)j.npix_cap + 8) + 4 * ((size_t)j.lz_cap + 8)) +
+         (size_t)(t * HOH_NPLANE_S + p) * (HOH_MAPCAP + 8);
+}
+__host__ __device__ inline size_t slab_total_s(int ntiles, uint32_t npix_cap, uint32_t lz_cap) {
+  return (size_t)ntiles * (HOH_NPLANE_S * ((size_t)npix_cap + 8) + 4 * ((size_t)lz_cap + 8) + HOH_NPLANE_S * (HOH_MAPCAP + 8));
+}
+
+// stream subsets: sid(i) = (i / per) * spt + base + i % per (per == 0: sid = i)
+struct SidMap { int per, base; };
+__host__ __device__ inline int map_sid(const SidMap& m, int spt, int i) {
+  return m.per ? (i / m.per) * spt + m.base + i % m.per : i;
+}
+
 void launch_front(const EncodeJob& j, hipStream_t s);
 void launch_palette(const EncodeJob& j, hipStream_t s);
 void launch_lz(const EncodeJob& j, hipStream_t s);
-void launch_tables(const EncodeJob& j, int nstreams, hipStream_t s);
-void launch_rans_fast(const EncodeJob& j, const uint32_t* fast_ids, int nfast, hipStream_t s);
-void launch_rans_gen(const EncodeJob& j, int nstreams, hipStream_t s);
-void launch_finalize(const EncodeJob& j, int nstreams, hipStream_t s);
+void launch_tables(const EncodeJob& j, int nstreams, hipStream_t s, SidMap m = SidMap{0, 0});
+void launch_rans_fast(const EncodeJob& j, int nplane, hipStream_t s, SidMap a, int na, SidMap b);
+void launch_rans_gen(const EncodeJob& j, int nstreams, hipStream_t s, SidMap m = SidMap{0, 0});
+void launch_finalize(const EncodeJob& j, int nstreams, hipStream_t s, SidMap m = SidMap{0, 0});
+void launch_nuke(const EncodeJob& j, hipStream_t s);
+void encode_speed_s(const EncodeJob& j, hipStream_t s, void (*mark)(void*, const char*), void* mctx);
 void launch_layout(const EncodeJob& j, hipStream_t s);
 void launch_assemble(const EncodeJob& j, int nstreams, hipStream_t s);
 void launch_streambytes(const EncodeJob& j, int nstreams, hipStream_t s);

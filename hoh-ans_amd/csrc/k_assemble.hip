@@ -6,9 +6,10 @@
 //            tile writes the fixed framing bytes.
 #include "hoh_internal.h"
 
-__global__ __launch_bounds__(64) void k_finalize(EncodeJob j, int nstreams) {
-  const int s = blockIdx.x * 64 + threadIdx.x;
-  if (s >= nstreams) return;
+__global__ __launch_bounds__(64) void k_finalize(EncodeJob j, int nstreams, SidMap sm) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= nstreams) return;
+  const int s = map_sid(sm, j.spt, i);
   StreamInfo st = j.streams[s];
   if (st.err) return;
   if (st.mode == SM_RANS) {
@@ -20,7 +21,7 @@ __global__ __launch_bounds__(64) void k_finalize(EncodeJob j, int nstreams) {
     } else {
       st.size = (uint32_t)es;
     }
-    if (st.words > st.slab_cap) { st.err = 9; atomicOr(j.gerr, 8u); }
+    if (st.words > st.slab_cap && !st.sizeonly) { st.err = 9; atomicOr(j.gerr, 8u); }
   }
   j.streams[s] = st;
 }
@@ -53,9 +54,9 @@ __global__ __launch_bounds__(1024) void k_layout(EncodeJob j) {
     uint64_t sz = 0, vl = 0;
     if (t < j.ntiles) {
       TileInfo ti = j.tiles[t];
-      const StreamInfo* st = j.streams + (size_t)t * SK_PER_TILE;
+      const StreamInfo* st = j.streams + (size_t)t * j.spt;
       uint32_t bad = ti.flags & (TF_UNREPRODUCIBLE | TF_UNSUPPORTED | TF_OVERFLOW);
-      for (int k = 0; k < SK_PER_TILE; k++) if (st[k].err) bad |= TF_OVERFLOW;
+      for (int k = 0; k < j.spt; k++) if (st[k].err) bad |= TF_OVERFLOW;
       const uint32_t lzb = 1 + st[0].size + st[1].size + st[2].size;   // lz.hpp:98 + 3 streams
       uint64_t s64 = 2 + 1 + lzb;                                        // choh.cpp:115-116, :328-331
       if (ti.mode == 128 || ti.mode == 127) {
@@ -107,7 +108,7 @@ __global__ __launch_bounds__(1024) void k_layout(EncodeJob j) {
       ti.off = first + carry_s + es;
       ti.pad = (uint32_t)(j.prefix + carry_v + ev);     // where this tile's size varint goes
       j.tiles[t] = ti;
-      StreamInfo* st = j.streams + (size_t)t * SK_PER_TILE;
+      StreamInfo* st = j.streams + (size_t)t * j.spt;
       uint64_t o = ti.off + 3 + 1;
       for (int k = 0; k < 3; k++) { st[k].out_off = o; o += st[k].size; }
       if (ti.mode == 128) {
@@ -131,7 +132,7 @@ __global__ __launch_bounds__(64) void k_tilebytes(EncodeJob j) {
   const int t = blockIdx.x * 64 + threadIdx.x;
   if (t >= j.ntiles || *j.total > j.cap || *j.gerr) return;
   const TileInfo ti = j.tiles[t];
-  const StreamInfo* st = j.streams + (size_t)t * SK_PER_TILE;
+  const StreamInfo* st = j.streams + (size_t)t * j.spt;
   uint8_t* o = j.out + ti.off;
   o[0] = 0; o[1] = 0;                                  // 1x1 inner tiling (choh.cpp:115-116)
   o[2] = (uint8_t)ti.mode;                             // internal colour mode (:328)
@@ -214,8 +215,9 @@ __global__ __launch_bounds__(256) void k_streambytes(EncodeJob j) {
   }
 }
 
-void launch_finalize(const EncodeJob& j, int nstreams, hipStream_t s) {
-  hipLaunchKernelGGL(k_finalize, dim3((nstreams + 63) / 64), dim3(64), 0, s, j, nstreams);
+void launch_finalize(const EncodeJob& j, int nstreams, hipStream_t s, SidMap m) {
+  if (nstreams <= 0) return;
+  hipLaunchKernelGGL(k_finalize, dim3((nstreams + 63) / 64), dim3(64), 0, s, j, nstreams, m);
 }
 
 void launch_layout(const EncodeJob& j, hipStream_t s) {

@@ -71,7 +71,7 @@ __global__ __launch_bounds__(NT) void k_front(EncodeJob j) {
   if (tid == 0) { s_ncol = 0; s_notgrey = 0; s_ncand = 0; s_np = 0; }
 
   uint16_t* res[3];
-  for (int k = 0; k < 3; k++) res[k] = j.sym + (size_t)(t * 3 + k) * j.npix_cap;
+  for (int k = 0; k < 3; k++) res[k] = j.sym + med_plane_off(j, t, k);
   uint64_t* cand = j.candbits + (size_t)t * (j.npix_cap / 64);
   const uint8_t* img = j.rgb + ((size_t)y0 * j.W + x0) * 3;
   const size_t pitch = (size_t)j.W * 3;
@@ -184,7 +184,7 @@ __global__ __launch_bounds__(NT) void k_front(EncodeJob j) {
   __syncthreads();
   for (int i = tid; i < 3 * 512; i += NT) {
     const int k = i / 512, s = i % 512;
-    j.hist[(size_t)(t * SK_PER_TILE + SK_G + k) * 512 + s] = hist[k][s];
+    j.hist[(size_t)(t * j.spt + med_kind(j, k)) * 512 + s] = hist[k][s];
   }
   if (s_ncol <= 256 && s_notgrey) {
     // palette in first-occurrence order (choh.cpp:64-88): rank of a colour = number of colours
@@ -249,7 +249,7 @@ __global__ __launch_bounds__(NT) void k_palette(EncodeJob j) {
     hv[hsh] = (uint32_t)tid;
   }
   __syncthreads();
-  uint16_t* pl = j.sym + idx_plane_off(j, t);
+  uint16_t* pl = j.sym + med_plane_off(j, t, 3);
   const uint8_t* img = j.rgb + ((size_t)ti.y0 * j.W + ti.x0) * 3;
   const size_t pitch = (size_t)j.W * 3;
   int x = tid, y = 0;
@@ -260,6 +260,7 @@ __global__ __launch_bounds__(NT) void k_palette(EncodeJob j) {
     uint32_t hsh = (c * 2654435761u) >> 22;
     for (int probe = 0; probe < 1024 && hk[hsh] != c; probe++) hsh = (hsh + 1) & 1023;
     pl[q] = (uint16_t)hv[hsh];
+    if (j.idx8) j.idx8[(size_t)t * j.npix_cap + q] = (uint8_t)hv[hsh];
     x += NT;
     while (x >= w) { x -= w; y++; }
   }
@@ -280,7 +281,7 @@ __global__ __launch_bounds__(NT) void k_palette(EncodeJob j) {
     if (q < npix) { pl[q] = (uint16_t)r; atomicAdd(&phist[r], 1u); }
     __syncthreads();
   }
-  uint32_t* hs = j.hist + (size_t)(t * SK_PER_TILE + SK_I) * 512;
+  uint32_t* hs = j.hist + (size_t)(t * j.spt + med_kind(j, 3)) * 512;
   for (int i = tid; i < 512; i += NT) hs[i] = i < 256 ? phist[i] : 0u;
 }
 

@@ -113,7 +113,7 @@ __global__ __launch_bounds__(64) void k_lz(EncodeJob j) {
     const bool planes = !(ti.flags & TF_GREY);
     const size_t pl_slab = (size_t)j.npix_cap + 8;
     const size_t lz_slab = (size_t)j.lz_cap + 8;
-    for (int k = 0; k < SK_PER_TILE; k++) {
+    for (int k = 0; k < j.spt; k++) {
       StreamInfo st;
       memset(&st, 0, sizeof(st));
       if (k < 3) {
@@ -142,8 +142,9 @@ __global__ __launch_bounds__(64) void k_lz(EncodeJob j) {
         st.fast = pal ? 1 : 0;
       }
       st.mode = SM_EMPTY;
-      st.ckpt_off = (uint32_t)((size_t)(t * SK_PER_TILE + k) * (j.npix_cap / HOH_SEG + 2));
-      j.streams[t * SK_PER_TILE + k] = st;
+      st.hist_src = k >= SK_G ? (uint32_t)(t * j.spt + k) + 1 : 0;   // planes: k_front's histograms
+      st.ckpt_off = (uint32_t)((size_t)(t * j.spt + k) * (j.npix_cap / HOH_SEG + 2));
+      j.streams[t * j.spt + k] = st;
     }
   }
 }
@@ -168,10 +169,23 @@ __global__ __launch_bounds__(256) void k_nuke(EncodeJob j) {
     for (uint32_t p = a + tid; p < e; p += 256) atomicOr(&nk_bits[p >> 5], 1u << (p & 31));
   }
   __syncthreads();
-  const int nplanes = (ti.flags & TF_PALETTE_CAND) && !(ti.flags & TF_GREY) ? 4 : 3;
-  for (int k = 0; k < nplanes; k++) {
-    uint16_t* r = j.sym + (k < 3 ? (size_t)(t * 3 + k) * j.npix_cap : idx_plane_off(j, t));
-    uint32_t* hk = j.hist + (size_t)(t * SK_PER_TILE + (k < 3 ? SK_G + k : SK_I)) * 512;
+  const bool grey = ti.flags & TF_GREY, pal = !grey && (ti.flags & TF_PALETTE_CAND);
+  const int nslots = j.speed ? 2 * HOH_NPLANE_S : 4;
+  for (int k = 0; k < nslots; k++) {
+    // plane slots: -s0 the MED planes G R' B' (+ indexed); -s>=1 the six MED planes, then the six
+    // searched planes, each with its stream's histogram
+    const int p = k % HOH_NPLANE_S;
+    const bool present = !grey && (p < 3 || (p == 3 && pal) || (p >= 4 && j.speed >= 3));
+    if (!present) continue;
+    uint16_t* r;
+    uint32_t* hk;
+    if (k < HOH_NPLANE_S || !j.speed) {
+      r = j.sym + med_plane_off(j, t, p);
+      hk = j.hist + (size_t)(t * j.spt + med_kind(j, p)) * 512;
+    } else {
+      r = j.sym + fin_plane_off(j, t, p);
+      hk = j.hist + (size_t)(t * j.spt + KS_FIN + p) * 512;
+    }
     uint32_t outc = 0;
     uint16_t vnext = tid < npix ? r[tid] : 0;
     for (uint32_t base = 0; base < npix; base += 256) {
@@ -200,5 +214,8 @@ __global__ __launch_bounds__(256) void k_nuke(EncodeJob j) {
 
 void launch_lz(const EncodeJob& j, hipStream_t s) {
   hipLaunchKernelGGL(k_lz, dim3(j.ntiles), dim3(64), 0, s, j);
+}
+
+void launch_nuke(const EncodeJob& j, hipStream_t s) {
   hipLaunchKernelGGL(k_nuke, dim3(j.ntiles), dim3(256), (size_t)(j.npix_cap / 32 + 1) * 4, s, j);
 }

@@ -21,9 +21,10 @@
 
 #define WIN 32
 
-// plane index -> stream: [0, 3*ntiles) the sub-green planes, then one indexed plane per tile
-__device__ __forceinline__ uint32_t plane_sid(int pi, int ntiles) {
-  return pi < 3 * ntiles ? (pi / 3) * SK_PER_TILE + SK_G + pi % 3 : (pi - 3 * ntiles) * SK_PER_TILE + SK_I;
+// plane index -> stream: [0, na) through map a, then map b (e.g. the sub-green planes of every
+// tile first, the rarely present indexed planes after them, so idle lanes share few waves)
+__device__ __forceinline__ uint32_t plane_sid(int pi, int spt, SidMap a, int na, SidMap b) {
+  return pi < na ? map_sid(a, spt, pi) : map_sid(b, spt, pi - na);
 }
 
 __device__ __forceinline__ void lookup8(EncFast* e, uint4 sy, const EncFast* tab) {
@@ -79,12 +80,12 @@ __device__ __forceinline__ void ckpt(const Coder& c, Checkpoint* ck, uint32_t k)
 }
 
 template <int LANES>
-__global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane) {
+__global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane, SidMap ma, int na, SidMap mb) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int lane = threadIdx.x;
   const int pi = blockIdx.x * LANES + lane;
   if (lane >= LANES || pi >= nplane) return;
-  const uint32_t sid = plane_sid(pi, j.ntiles);
+  const uint32_t sid = plane_sid(pi, j.spt, ma, na, mb);
   StreamInfo st = j.streams[sid];
   if (!st.fast || st.mode != SM_RANS || st.err || st.n == 0) return;
   const uint32_t n = st.n;
@@ -146,9 +147,10 @@ __global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane) {
 }
 
 // Generic: one lane per stream, rans64.hpp:262-278 verbatim (64x64 high product).
-__global__ __launch_bounds__(64) void k_rans_gen(EncodeJob j, int nstreams) {
-  const int sid = blockIdx.x * 64 + threadIdx.x;
-  if (sid >= nstreams) return;
+__global__ __launch_bounds__(64) void k_rans_gen(EncodeJob j, int nstreams, SidMap sm) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= nstreams) return;
+  const int sid = map_sid(sm, j.spt, i);
   StreamInfo st = j.streams[sid];
   if (st.fast || st.mode != SM_RANS || st.err || st.n == 0) return;
   const uint16_t* sp = j.sym + st.sym_off;
@@ -157,41 +159,45 @@ __global__ __launch_bounds__(64) void k_rans_gen(EncodeJob j, int nstreams) {
   Checkpoint* ck = j.ckpt + st.ckpt_off;
   uint32_t widx = st.slab_cap;
   const uint32_t pb = st.pb;
+  const bool so = st.sizeonly;                  // size-only: count the words, store nothing
   uint64_t x = 1ull << 31;
   for (uint32_t i = st.n; i > 0; i--) {
     const EncGen g = tab[sp[i - 1]];
     const uint64_t x_max = (((1ull << 31) >> pb) << 32) * g.freq;
     if (x >= x_max) {
-      slab[--widx] = (uint32_t)x;
+      --widx;
+      if (!so) slab[widx] = (uint32_t)x;
       x >>= 32;
     }
     const uint64_t q = __umul64hi(x, g.rcp) >> g.shift;
     x = x + g.bias + q * g.cmpl;
-    if (((i - 1) % HOH_SEG) == 0) {
+    if (!so && ((i - 1) % HOH_SEG) == 0) {
       Checkpoint p;
       p.xl = (uint32_t)x; p.xh = (uint32_t)(x >> 32); p.widx = widx; p.pad = 0;
       ck[(i - 1) / HOH_SEG] = p;
     }
   }
-  slab[--widx] = (uint32_t)(x >> 32);
-  slab[--widx] = (uint32_t)x;
+  widx -= 2;
+  if (!so) { slab[widx + 1] = (uint32_t)(x >> 32); slab[widx] = (uint32_t)x; }
   j.streams[sid].words = st.slab_cap - widx;
   j.streams[sid].widx_end = widx;
 }
 
-void launch_rans_fast(const EncodeJob& j, const uint32_t*, int nplane, hipStream_t s) {
+void launch_rans_fast(const EncodeJob& j, int nplane, hipStream_t s, SidMap a, int na, SidMap b) {
   const int lanes = (j.dbg >> 8) & 127 ? (j.dbg >> 8) & 127 : 64;     // measurement knob
+  if (nplane <= 0) return;
   if (lanes == 16) {
-    hipLaunchKernelGGL(k_rans_fast<16>, dim3((nplane + 15) / 16), dim3(64), 16 * WIN * 4, s, j, nplane);
+    hipLaunchKernelGGL(k_rans_fast<16>, dim3((nplane + 15) / 16), dim3(64), 16 * WIN * 4, s, j, nplane, a, na, b);
   } else if (lanes == 32) {
-    hipLaunchKernelGGL(k_rans_fast<32>, dim3((nplane + 31) / 32), dim3(64), 32 * WIN * 4, s, j, nplane);
+    hipLaunchKernelGGL(k_rans_fast<32>, dim3((nplane + 31) / 32), dim3(64), 32 * WIN * 4, s, j, nplane, a, na, b);
   } else if (lanes == 8) {
-    hipLaunchKernelGGL(k_rans_fast<8>, dim3((nplane + 7) / 8), dim3(64), 8 * WIN * 4, s, j, nplane);
+    hipLaunchKernelGGL(k_rans_fast<8>, dim3((nplane + 7) / 8), dim3(64), 8 * WIN * 4, s, j, nplane, a, na, b);
   } else {
-    hipLaunchKernelGGL(k_rans_fast<64>, dim3((nplane + 63) / 64), dim3(64), 64 * WIN * 4, s, j, nplane);
+    hipLaunchKernelGGL(k_rans_fast<64>, dim3((nplane + 63) / 64), dim3(64), 64 * WIN * 4, s, j, nplane, a, na, b);
   }
 }
 
-void launch_rans_gen(const EncodeJob& j, int nstreams, hipStream_t s) {
-  hipLaunchKernelGGL(k_rans_gen, dim3((nstreams + 63) / 64), dim3(64), 0, s, j, nstreams);
+void launch_rans_gen(const EncodeJob& j, int nstreams, hipStream_t s, SidMap m) {
+  if (nstreams <= 0) return;
+  hipLaunchKernelGGL(k_rans_gen, dim3((nstreams + 63) / 64), dim3(64), 0, s, j, nstreams, m);
 }

@@ -47,12 +47,12 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
   return v;
 }
 
-__global__ __launch_bounds__(64) void k_tables(EncodeJob j) {
+__global__ __launch_bounds__(64) void k_tables(EncodeJob j, SidMap sm) {
   extern __shared__ uint32_t tb_lds[];             // fr[gen_stride] | cum[gen_stride + 1]
   uint32_t* fr = tb_lds;
   uint32_t* cum = tb_lds + j.gen_stride;
   __shared__ uint32_t s_err;
-  const int s = blockIdx.x, lane = threadIdx.x;
+  const int s = map_sid(sm, j.spt, blockIdx.x), lane = threadIdx.x;
   StreamInfo st = j.streams[s];
   uint8_t* hd = j.hdr + (size_t)s * j.hdr_cap;
   if (st.range == 0) {                     // absent stream (bitimage tile)
@@ -74,9 +74,8 @@ __global__ __launch_bounds__(64) void k_tables(EncodeJob j) {
   for (uint32_t i = lane; i < range; i += 64) fr[i] = 0;
   __syncthreads();
   const uint16_t* sy = j.sym + st.sym_off;
-  const int kind = s % SK_PER_TILE;
-  if (j.hist && kind >= SK_G && j.tiles) {
-    for (uint32_t i = lane; i < range; i += 64) fr[i] = j.hist[(size_t)s * 512 + i];
+  if (j.hist && st.hist_src) {
+    for (uint32_t i = lane; i < range; i += 64) fr[i] = j.hist[(size_t)(st.hist_src - 1) * 512 + i];
   } else {
     for (uint32_t i = lane; i < n; i += 64) {
       uint32_t v = sy[i];
@@ -302,8 +301,9 @@ __global__ __launch_bounds__(64) void k_tables(EncodeJob j) {
   j.streams[s] = st;
 }
 
-void launch_tables(const EncodeJob& j, int nstreams, hipStream_t s) {
+void launch_tables(const EncodeJob& j, int nstreams, hipStream_t s, SidMap m) {
   // LDS sized to the job's largest alphabet (512 for images): many streams per CU at once, so
   // the serial header writer of each runs concurrently with the others
-  hipLaunchKernelGGL(k_tables, dim3(nstreams), dim3(64), (size_t)(2 * j.gen_stride + 1) * 4, s, j);
+  if (nstreams <= 0) return;
+  hipLaunchKernelGGL(k_tables, dim3(nstreams), dim3(64), (size_t)(2 * j.gen_stride + 1) * 4, s, j, m);
 }
