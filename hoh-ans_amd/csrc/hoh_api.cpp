@@ -6,6 +6,7 @@
 #include "hoh_dec.h"
 #include "../../include/hoh_ans.h"
 
+#include <math.h>
 #include <string.h>
 #include <stdlib.h>
 #include <vector>
@@ -45,6 +46,9 @@ struct hoh_index {
 struct hoh_ctx {
   int device = 0;
   hipStream_t own = nullptr;
+  Buf idx8, fpb, pinfo, lg;     // -s>=1 workspaces
+  uint32_t lg_key[4] = {0, 0, 0, 0};
+  uint64_t lg_off[4] = {0, 0, 0, 0};
   Buf sym, hist, candbits, matches, pal, streams, tiles, hdr, tab_fast, tab_gen, slabs, ckpt, misc, tsizes;
   DecWork dec;                  // decoder workspaces (k_decode.hip)
   uint64_t* pinned = nullptr;   // small host staging (status words, sizes)
@@ -139,7 +143,7 @@ static void freebuf(Buf& b) { if (b.p) (void)hipFree(b.p); b.p = nullptr; b.n = 
 void hoh_ctx_destroy(hoh_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  Buf* all[] = {&c->sym, &c->hist, &c->candbits, &c->matches, &c->pal, &c->streams, &c->tiles, &c->hdr,
+  Buf* all[] = {&c->idx8, &c->fpb, &c->pinfo, &c->lg, &c->sym, &c->hist, &c->candbits, &c->matches, &c->pal, &c->streams, &c->tiles, &c->hdr,
                 &c->tab_fast, &c->tab_gen, &c->slabs, &c->ckpt, &c->misc, &c->tsizes};
   for (Buf* b : all) freebuf(*b);
   dec_free(c->dec);
@@ -251,10 +255,41 @@ int hoh_peek_header(const uint8_t* h, size_t size, int* W, int* H, int* xt, int*
 
 // ---------------------------------------------------------------- image encode
 
+static void prof_cb(void* p, const char* name) { ((Prof*)p)->mark(name); }
+
+// -log2(k / n) for k = 0..n+1 and every tile pixel count n of the image (layer_encode.hpp:143),
+// computed once per image shape with the host's log2 so the -s>=1 search sees the reference's
+// exact doubles
+static int ensure_log2_tables(hoh_ctx* c, int W, int H, EncodeJob& j) {
+  const int rw = W - (j.xt - 1) * j.tw, bh = H - (j.yt - 1) * j.th;
+  uint32_t ns[4] = {(uint32_t)(j.tw * j.th), (uint32_t)(rw * j.th), (uint32_t)(j.tw * bh), (uint32_t)(rw * bh)};
+  uint32_t un[4] = {0, 0, 0, 0};
+  int nu = 0;
+  for (int i = 0; i < 4; i++) {
+    bool dup = false;
+    for (int k = 0; k < nu; k++) dup |= un[k] == ns[i];
+    if (!dup && ns[i]) un[nu++] = ns[i];
+  }
+  if (!(c->lg_key[0] == un[0] && c->lg_key[1] == un[1] && c->lg_key[2] == un[2] && c->lg_key[3] == un[3])) {
+    std::vector<double> tab;
+    for (int k = 0; k < nu; k++) {
+      c->lg_off[k] = tab.size();
+      for (uint32_t f = 0; f <= un[k] + 1; f++) tab.push_back(f ? -log2((double)f / (double)un[k]) : 0.0);
+    }
+    int e = ensure(c->lg, tab.size() * sizeof(double));
+    if (e) return e;
+    if (hipMemcpy(c->lg.p, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) return HOH_E_HIP;
+    for (int k = 0; k < 4; k++) c->lg_key[k] = un[k];
+  }
+  j.lg = (const double*)c->lg.p;
+  for (int k = 0; k < 4; k++) { j.lg_n[k] = c->lg_key[k]; j.lg_off[k] = c->lg_off[k]; }
+  return HOH_OK;
+}
+
 static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int t0, int ntiles,
                              uint8_t* d_out, size_t cap, uint64_t prefix, int write_table,
                              uint32_t* d_tile_sizes, uint64_t* total_out, hoh_index* idx,
-                             hipStream_t s) {
+                             hipStream_t s, int speed = 0) {
   int xt, yt, tw, th;
   hoh_tiling(W, H, &xt, &yt, &tw, &th);
   if (tw > HOH_MAX_TILE_W || (size_t)tw * th > (1u << 24)) return HOH_E_UNSUPPORTED;
@@ -266,8 +301,8 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
     const char* e = getenv("HOH_ENC_DBG");
     j.dbg = e ? (uint32_t)atoi(e) : 0;
   }
-  j.speed = 0;
-  j.spt = SK_PER_TILE;
+  j.speed = speed;
+  j.spt = speed ? SPT_S : SK_PER_TILE;
   j.rgb = d_rgb; j.W = W; j.H = H;
   j.xt = xt; j.yt = yt; j.tw = tw; j.th = th;
   j.t0 = t0; j.ntiles = ntiles;
@@ -275,12 +310,26 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   j.lz_cap = (uint32_t)rup(j.npix_cap / 4 + j.npix_cap / 255 + 16, 8);
   j.gen_stride = 512;
   j.hdr_cap = HOH_HDR_CAP;
-  const size_t S = (size_t)ntiles * SK_PER_TILE;
-  // arenas: [tile][3] planes, [tile][3] LZ streams, [tile] indexed plane (hoh_internal.h)
-  const size_t nsym = (size_t)ntiles * 3 * (j.npix_cap + j.lz_cap) + (size_t)ntiles * j.npix_cap;
-  const size_t nslab = (size_t)ntiles * 3 * (j.npix_cap + 8 + j.lz_cap + 8) + (size_t)ntiles * (j.npix_cap + 8);
-  const size_t nck = S * (j.npix_cap / HOH_SEG + 2);
+  const size_t S = (size_t)ntiles * j.spt;
+  // arenas: [tile][3] planes, [tile][3] LZ streams, [tile] indexed plane (hoh_internal.h); the
+  // -s>=1 layout is in hoh_internal.h too
+  size_t nsym = (size_t)ntiles * 3 * (j.npix_cap + j.lz_cap) + (size_t)ntiles * j.npix_cap;
+  size_t nslab = (size_t)ntiles * 3 * (j.npix_cap + 8 + j.lz_cap + 8) + (size_t)ntiles * (j.npix_cap + 8);
+  if (speed) {
+    nsym = sym_total_s(ntiles, j.npix_cap, j.lz_cap);
+    nslab = slab_total_s(ntiles, j.npix_cap, j.lz_cap);
+  }
+  const size_t nck = speed ? 1 : S * (j.npix_cap / HOH_SEG + 2);
   int e = HOH_OK;
+  if (speed) {
+    if ((e = ensure(c->idx8, (size_t)ntiles * j.npix_cap))) return e;
+    if ((e = ensure(c->fpb, (size_t)ntiles * j.npix_cap * 4))) return e;
+    if ((e = ensure(c->pinfo, (size_t)ntiles * HOH_NPLANE_S * sizeof(PlaneInfo)))) return e;
+    if ((e = ensure_log2_tables(c, W, H, j))) return e;
+    j.idx8 = (uint8_t*)c->idx8.p;
+    j.fpb = (uint32_t*)c->fpb.p;
+    j.pinfo = (PlaneInfo*)c->pinfo.p;
+  }
   if ((e = ensure(c->sym, nsym * 2 + 64))) return e;
   if ((e = ensure(c->hist, S * 512 * 4))) return e;
   if ((e = ensure(c->candbits, (size_t)ntiles * (j.npix_cap / 64) * 8))) return e;
@@ -305,7 +354,7 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   j.tab_fast = (EncFast*)c->tab_fast.p;
   j.tab_gen = (EncGen*)c->tab_gen.p;
   j.slabs = (uint32_t*)c->slabs.p;
-  j.ckpt = (Checkpoint*)c->ckpt.p;
+  j.ckpt = speed ? nullptr : (Checkpoint*)c->ckpt.p;      // -s>=1 files get no side index
   j.gerr = (uint32_t*)c->misc.p;
   j.total = (uint64_t*)((uint8_t*)c->misc.p + 8);
   j.tile_sizes = d_tile_sizes;
@@ -318,6 +367,11 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   prof.mark("memset");
   launch_front(j, s);            prof.mark("front");
   launch_palette(j, s);          prof.mark("palette");
+  if (speed) {
+    encode_speed_s(j, s, prof_cb, &prof);
+    if (hipGetLastError() != hipSuccess) return HOH_E_HIP;
+    idx = nullptr;
+  } else {
   launch_lz(j, s);
   launch_nuke(j, s);             prof.mark("lz");
   launch_tables(j, (int)S, s);   prof.mark("tables");
@@ -326,6 +380,7 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   launch_finalize(j, (int)S, s); prof.mark("finalize");
   launch_layout(j, s);           prof.mark("layout");
   launch_assemble(j, (int)S, s); prof.mark("assemble");
+  }
   if (hipGetLastError() != hipSuccess) return HOH_E_HIP;
   if (idx) {
     int r = index_capture(idx, j, s);
@@ -368,7 +423,7 @@ int hoh_encode_tiles_ix(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int t0, 
 int hoh_encode_image_ix(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int speed, uint8_t* d_out,
                         size_t cap, size_t* out_size, size_t* printed, hoh_index* idx, void* stream) {
   if (!c || !d_rgb || !d_out || !out_size || W <= 0 || H <= 0) return HOH_E_ARG;
-  if (speed != 0) return HOH_E_UNSUPPORTED;                             // -s1..-s4 not on this path
+  if (speed < 0 || speed > 4) return HOH_E_ARG;                         // choh.cpp:408-427
   (void)hipSetDevice(c->device);
   hipStream_t s = pick(c, stream);
   uint8_t hb[32];
@@ -380,7 +435,8 @@ int hoh_encode_image_ix(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int spee
   uint64_t total = 0;
   int r;
   if (tiled) {
-    r = encode_tiles_impl(c, d_rgb, W, H, 0, xt * yt, d_out, cap, hl, 1, nullptr, &total, idx, s);
+    r = encode_tiles_impl(c, d_rgb, W, H, 0, xt * yt, d_out, cap, hl, 1, nullptr, &total, idx, s, speed);
+    if (speed && idx) idx->nstreams = 0;
     if (r == HOH_OK && hipMemcpyAsync(d_out, hb, hl, hipMemcpyHostToDevice, s) != hipSuccess) r = HOH_E_HIP;
     if (r == HOH_OK && hipStreamSynchronize(s) != hipSuccess) r = HOH_E_HIP;
     *out_size = (size_t)total;
@@ -390,7 +446,7 @@ int hoh_encode_image_ix(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int spee
     Buf scratch;
     const size_t b = hoh_encode_bound(W, H);
     if ((r = ensure(scratch, b))) return r;
-    r = encode_tiles_impl(c, d_rgb, W, H, 0, 1, (uint8_t*)scratch.p, b, 0, 0, nullptr, &total, nullptr, s);
+    r = encode_tiles_impl(c, d_rgb, W, H, 0, 1, (uint8_t*)scratch.p, b, 0, 0, nullptr, &total, nullptr, s, speed);
     freebuf(scratch);
     if (r == HOH_OK && hipMemcpyAsync(d_out, hb, hl, hipMemcpyHostToDevice, s) != hipSuccess) r = HOH_E_HIP;
     if (r == HOH_OK && hipStreamSynchronize(s) != hipSuccess) r = HOH_E_HIP;

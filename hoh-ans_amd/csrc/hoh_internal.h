@@ -92,6 +92,10 @@ struct TileInfo {
   uint64_t off;           // output byte offset of the tile
   uint32_t mode;          // internal colour mode byte (128 sub-green, 127 indexed, 0 bitimage)
   uint32_t pad;           // layout: byte offset of this tile's size varint
+  uint32_t nclean;        // -s>=1: pixels outside LZ copies
+  uint32_t nfut;          // -s>=1: symbols of the LZ "future" stream
+  uint32_t chmap;         // -s>=1: layers of channels 1..3 (plane index, 4 bits each)
+  uint32_t pad2;
 };
 
 struct Checkpoint {       // encoder state after coding symbol k*HOH_SEG == decoder state before it

@@ -154,7 +154,7 @@ __global__ __launch_bounds__(NT) void k_front(EncodeJob j) {
     uint32_t* key = wkey[wv];
     uint32_t* dup = wdup[wv];
     uint32_t sq = WTAB, sp = WTAB;
-    if (!(j.dbg & 4)) {
+    if (!(j.dbg & 4) && j.speed == 0) {         // -s>=1: k_lzcand screens a longer window
       if (hq) sq = wt_insert(key, dup, hq);
       if (hp) sp = wt_insert(key, dup, hp);
     }

@@ -74,6 +74,7 @@ __device__ __forceinline__ void step15(Coder& c, const EncFast& e) {
 }
 
 __device__ __forceinline__ void ckpt(const Coder& c, Checkpoint* ck, uint32_t k) {
+  if (!ck) return;                          // no side index for this job
   Checkpoint p;
   p.xl = c.xl; p.xh = c.xh; p.widx = c.widx - __popc(c.mask); p.pad = 0;
   ck[k] = p;
@@ -95,7 +96,7 @@ __global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane, SidMa
   c.slab = j.slabs + st.slab_off;
   c.widx = st.slab_cap;
   c.win = (uint32_t*)(lds + lane * WIN * 4);
-  Checkpoint* ck = j.ckpt + st.ckpt_off;
+  Checkpoint* ck = j.ckpt ? j.ckpt + st.ckpt_off : nullptr;
   const uint16_t* sp = j.sym + st.sym_off;
   // prologue: the top n % 32 symbols one at a time (descending); the rest is whole windows
   const uint32_t r = n & 31, nb = (n - r) / 8;   // nb 8-symbol blocks, a multiple of 4
@@ -156,10 +157,11 @@ __global__ __launch_bounds__(64) void k_rans_gen(EncodeJob j, int nstreams, SidM
   const uint16_t* sp = j.sym + st.sym_off;
   const EncGen* tab = j.tab_gen + (size_t)sid * j.gen_stride;
   uint32_t* slab = j.slabs + st.slab_off;
-  Checkpoint* ck = j.ckpt + st.ckpt_off;
+  Checkpoint* ck = j.ckpt ? j.ckpt + st.ckpt_off : nullptr;
   uint32_t widx = st.slab_cap;
   const uint32_t pb = st.pb;
   const bool so = st.sizeonly;                  // size-only: count the words, store nothing
+  const bool ckp = !so && ck != nullptr;
   uint64_t x = 1ull << 31;
   for (uint32_t i = st.n; i > 0; i--) {
     const EncGen g = tab[sp[i - 1]];
@@ -171,7 +173,7 @@ __global__ __launch_bounds__(64) void k_rans_gen(EncodeJob j, int nstreams, SidM
     }
     const uint64_t q = __umul64hi(x, g.rcp) >> g.shift;
     x = x + g.bias + q * g.cmpl;
-    if (!so && ((i - 1) % HOH_SEG) == 0) {
+    if (ckp && ((i - 1) % HOH_SEG) == 0) {
       Checkpoint p;
       p.xl = (uint32_t)x; p.xh = (uint32_t)(x >> 32); p.widx = widx; p.pad = 0;
       ck[(i - 1) / HOH_SEG] = p;

@@ -1,0 +1,826 @@
+// -s1..-s4 encoder: cruncher_mode >= 1 of choh (choh.cpp:104-383) and layer_encode
+// (layer_encode.hpp:11-412).  Per tile, on top of the -s0 front end (k_front, k_palette):
+//  * k_rawmed     MED residuals of the plain R and B planes (-s>=3 RGB mode, choh.cpp:265-293);
+//  * k_search     per (tile, plane): entropy estimate from the MED residual histogram, 40-px grid
+//                 predictor search (one thread per (cell, mask): the cell walked in raster order,
+//                 costs summed in f64 in the reference's order so the selection is bit-identical),
+//                 refinement at -s>=3, then channelpredict_all residuals + histogram and the
+//                 predictor map;
+//  * k_lzfp / k_lzcand / k_lzscan
+//                 find_lz_rgb with seek distance 10..14 plus the vertical search (lz.hpp:32-95):
+//                 window fingerprints, an exact candidate screen (some earlier equal 4-pixel
+//                 window within the seek distance or a whole number of rows above), then the
+//                 greedy scan evaluating only candidates, 64 back distances per step;
+//  * k_setup_s    stream descriptors: LZ x4, MED at prob_bits 15, size-only encodes of the
+//                 searched residuals at prob_bits 16,15,17,18,19,14,13,12, predictor maps;
+//  * k_choose_s   the prob_bits ladder and the permanent/dummy buffer logic, including the
+//                 stale prefix of Q14; activates the one full encode a layer still needs;
+//  * k_layout_s / k_tilebytes_s
+//                 colour mode (sub-green / indexed / RGB), layer sizes, offsets, fixed bytes.
+// The entropy streams themselves go through k_tables / k_rans_* / k_finalize / k_streambytes.
+#include "hoh_internal.h"
+
+#define NT 256
+
+__constant__ uint16_t kMasks[14] = {0x0001, 0x0002, 0x0020, 0x0010, 0xffbf, 0x0003, 0xfffd,
+                                    0xfffb, 0xfff7, 0xffef, 0xffdf, 0xff7f, 0xfdff, 0xffff};   // layer_encode.hpp:159-175
+__constant__ uint8_t kVarPb[8] = {16, 15, 17, 18, 19, 14, 13, 12};                        // :334-391
+
+__device__ __forceinline__ bool plane_present(const EncodeJob& j, const TileInfo& ti, int p) {
+  if (ti.flags & TF_GREY) return false;
+  if (p < 3) return true;
+  if (p == 3) return (ti.flags & TF_PALETTE_CAND) != 0;
+  return j.speed >= 3;
+}
+__device__ __forceinline__ int plane_depth(int p) { return (p == 1 || p == 2) ? 9 : 8; }
+
+// ---------------------------------------------------------------- predictor primitives (u16)
+
+__device__ __forceinline__ uint32_t med16s(uint32_t a, uint32_t b, uint32_t c) {   // predictor_operations.hpp:37-60
+  if (a > b) return b > c ? b : (c > a ? a : c);
+  return b < c ? b : (c > a ? c : a);
+}
+__device__ __forceinline__ uint32_t midp(uint32_t a, uint32_t b) {                 // :8-10
+  return (uint32_t)((int)a + ((int)b - (int)a) / 2);
+}
+__device__ __forceinline__ uint32_t avg3(uint32_t a, uint32_t b, uint32_t c) { return (a + b + c) / 3; }   // :66-68
+__device__ __forceinline__ uint32_t paeth(int A, int B, int C) {                   // :89-106
+  const int p = A + B - C;
+  const int Ap = abs(A - p), Bp = abs(B - p), Cp = abs(C - p);
+  if (Ap < Bp) return Ap < Cp ? A : C;
+  return Bp < Cp ? B : C;
+}
+
+struct Preds { uint32_t v[16]; };
+
+// prediction.hpp:116-133 (section: paeth(L, T, TL)) / :190-207 (all: paeth(L, TL, T))
+__device__ __forceinline__ void preds16(uint32_t L, uint32_t T, uint32_t TL, uint32_t TR, bool all, Preds& p) {
+  p.v[0] = L; p.v[1] = T; p.v[2] = TL; p.v[3] = TR;
+  p.v[4] = med16s(T, L, (T + L - TL) & 0xffffu);
+  p.v[5] = midp(L, T); p.v[6] = midp(L, TL); p.v[7] = midp(TL, T); p.v[8] = midp(T, TR);
+  p.v[9] = all ? paeth(L, TL, T) : paeth(L, T, TL);
+  p.v[10] = avg3(L, L, TL); p.v[11] = avg3(L, TL, TL); p.v[12] = avg3(TL, TL, T);
+  p.v[13] = avg3(TL, T, T); p.v[14] = avg3(T, T, TR); p.v[15] = avg3(T, TR, TR);
+}
+
+// p.v[k] for a lane-varying k without dynamic register indexing (4-level select tree)
+__device__ __forceinline__ uint32_t pick(const Preds& p, uint32_t k) {
+  uint32_t a[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) a[i] = (k & 1) ? p.v[2 * i + 1] : p.v[2 * i];
+  uint32_t b[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) b[i] = (k & 2) ? a[2 * i + 1] : a[2 * i];
+  const uint32_t c0 = (k & 4) ? b[1] : b[0], c1 = (k & 4) ? b[3] : b[2];
+  return (k & 8) ? c1 : c0;
+}
+
+// first masked predictor of least |v - p| (prediction.hpp:138-146, :213-224)
+__device__ __forceinline__ uint32_t best_pred(uint32_t v, const Preds& p, uint32_t mask, int c) {
+  int bv = 2 * c;
+  uint32_t b = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const int d = abs((int)v - (int)p.v[k]);
+    if (d < bv && ((mask >> k) & 1)) { bv = d; b = k; }
+  }
+  return b;
+}
+
+// ---------------------------------------------------------------- plane data
+
+// value of plane p at raster position q of tile t (channel.hpp:63-79, choh.cpp:62-88)
+__device__ __forceinline__ uint32_t plane_value(const EncodeJob& j, const TileInfo& ti, int t, int p, uint32_t q) {
+  if (p == 3) return j.idx8[(size_t)t * j.npix_cap + q];
+  const uint32_t y = q / (uint32_t)ti.w, x = q - y * (uint32_t)ti.w;
+  const uint8_t* px = j.rgb + ((size_t)(ti.y0 + y) * j.W + ti.x0 + x) * 3;
+  const uint32_t r = px[0], g = px[1], b = px[2];
+  switch (p) {
+    case 0: return g;
+    case 1: return r - g + 256;
+    case 2: return b - g + 256;
+    case 4: return r;
+    default: return b;
+  }
+}
+
+// MED residuals of the plain R and B planes (-s>=3), depth 8, + histograms
+__global__ __launch_bounds__(NT) void k_rawmed(EncodeJob j) {
+  __shared__ uint32_t hs[2][256];
+  const int t = blockIdx.x, tid = threadIdx.x;
+  const TileInfo ti = j.tiles[t];
+  if (!plane_present(j, ti, 4)) return;
+  for (int i = tid; i < 512; i += NT) (&hs[0][0])[i] = 0;
+  __syncthreads();
+  const uint32_t w = ti.w, npix = w * ti.h;
+  for (uint32_t q = tid; q < npix; q += NT) {
+    const uint32_t y = q / w, x = q - y * w;
+    for (int k = 0; k < 2; k++) {
+      const int p = 4 + k;
+      const uint32_t v = plane_value(j, ti, t, p, q);
+      const uint32_t L = x ? plane_value(j, ti, t, p, q - 1) : 128;
+      const uint32_t T = y ? plane_value(j, ti, t, p, q - w) : 128;
+      const uint32_t TL = (x && y) ? plane_value(j, ti, t, p, q - w - 1) : 128;
+      const uint32_t r = (v - med16s(T, L, (T + L - TL) & 0xffffu) + 128 + 256) & 255;   // prediction.hpp:35
+      j.sym[med_plane_off(j, t, p) + q] = (uint16_t)r;
+      atomicAdd(&hs[k][r], 1u);
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < 1024; i += NT) {
+    const int k = i / 512, s = i % 512;
+    j.hist[(size_t)(t * j.spt + KS_MED + 4 + k) * 512 + s] = s < 256 ? hs[k][s] : 0u;
+  }
+}
+
+// ---------------------------------------------------------------- predictor search
+
+struct SearchLds {
+  double ent[512];
+  double cost[HOH_MAPCAP * 14];
+  uint32_t hist[512];
+  uint16_t top[NT][40];
+  uint8_t bp[NT][40];
+  uint16_t plist[HOH_MAPCAP];
+  uint8_t pidx[HOH_MAPCAP];
+};
+
+// cost of mask m on cell (cx, cy): prediction.hpp:46-151 walked in the cell's raster order with
+// the reference's cell-local top row / best_pred state, sum of ent[] in f64 (layer_encode.hpp:192-195)
+__device__ double cell_cost(const uint16_t* D, int w, int h, int depth, int xt, int yt, int cx, int cy,
+                            uint32_t mask, const double* ent, uint16_t* top, uint8_t* bp) {
+  const int c = 1 << depth, half = c >> 1;
+  const int tw = (w + xt - 1) / xt, th = (h + yt - 1) / yt;
+  const int x0 = cx * tw, y0 = cy * th;
+  for (int i = 0; i < tw; i++) {
+    bp[i] = 4;
+    top[i] = cy ? D[(long)y0 * w + x0 + i - w] : (uint16_t)half;   // may run into the cell's own row
+  }
+  double cost = 0.0;
+  for (int ym = 0; ym < th && y0 + ym < h; ym++) {
+    uint32_t L, TL;
+    if (cx) {
+      L = D[(long)(y0 + ym) * w + x0 - 1];
+      TL = (ym || cy) ? D[(long)(y0 + ym - 1) * w + x0 - 1] : (uint32_t)half;
+    } else {
+      L = TL = half;
+    }
+    const uint16_t* row = D + (long)(y0 + ym) * w + x0;
+    for (int xm = 0; xm < tw && x0 + xm < w; xm++) {
+      const uint32_t v = row[xm];
+      const uint32_t T = top[xm];
+      const int xr = xm + 1 == tw ? 0 : xm + 1;
+      const uint32_t TR = top[xr];
+      Preds p;
+      preds16(L, T, TL, TR, false, p);
+      const int xl = xm == 0 ? tw - 1 : xm - 1;
+      const uint32_t pr = midp(pick(p, bp[xm]), pick(p, bp[xl]));
+      const uint32_t r = (uint32_t)(((int)v - (int)pr + half + c) % c);
+      cost += ent[r];
+      TL = T;
+      top[xm] = (uint16_t)v;
+      L = v;
+      bp[xm] = (uint8_t)best_pred(v, p, mask, c);
+    }
+  }
+  return cost;
+}
+
+// channelpredict_all (prediction.hpp:153-229) at one pixel, fully parallel: the best predictors
+// it needs (row above, left neighbour / end of the row above) are recomputed from the originals
+struct AllCtx {
+  const uint16_t* D;
+  int w, h, tw, th, xt, c, half;
+  const uint16_t* plist;
+};
+
+__device__ __forceinline__ void preds_all_at(const AllCtx& a, int x, int y, Preds& p) {
+  const int w = a.w;
+  const uint32_t L = x ? a.D[(long)y * w + x - 1] : (uint32_t)a.half;
+  const uint32_t T = y ? a.D[(long)(y - 1) * w + x] : (uint32_t)a.half;
+  const uint32_t TL = (x && y) ? a.D[(long)(y - 1) * w + x - 1] : (uint32_t)a.half;
+  uint32_t TR;
+  if (w == 1) TR = T;                                        // top_row[0] not yet overwritten
+  else if (x == w - 1) TR = a.D[(long)y * w];                // top_row[0]: this row's first value
+  else TR = y ? a.D[(long)(y - 1) * w + x + 1] : (uint32_t)a.half;
+  preds16(L, T, TL, TR, true, p);
+}
+
+__device__ __forceinline__ uint32_t bp_all(const AllCtx& a, int x, int y) {
+  if (y + 1 >= a.h) return 0;                                // last row keeps 0 (:214-216)
+  Preds p;
+  preds_all_at(a, x, y, p);
+  return best_pred(a.D[(long)y * a.w + x], p, a.plist[((y + 1) / a.th) * a.xt + x / a.tw], a.c);
+}
+
+__device__ __forceinline__ uint32_t resid_all(const AllCtx& a, int x, int y) {
+  const uint32_t bA = y ? bp_all(a, x, y - 1) : 4u;
+  const uint32_t bB = x ? bp_all(a, x - 1, y) : (y ? bp_all(a, a.w - 1, y - 1) : 4u);
+  Preds p;
+  preds_all_at(a, x, y, p);
+  const uint32_t pr = midp(pick(p, bA), pick(p, bB));
+  return (uint32_t)(((int)a.D[(long)y * a.w + x] - (int)pr + a.half + a.c) % a.c);
+}
+
+// one workgroup per (tile, plane)
+__global__ __launch_bounds__(NT) void k_search(EncodeJob j) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sl_raw[];
+  SearchLds& S = *(SearchLds*)sl_raw;
+  const int t = blockIdx.x / HOH_NPLANE_S, p = blockIdx.x % HOH_NPLANE_S, tid = threadIdx.x;
+  const TileInfo ti = j.tiles[t];
+  PlaneInfo* pi = j.pinfo + (size_t)t * HOH_NPLANE_S + p;
+  if (!plane_present(j, ti, p)) {
+    if (tid == 0) { PlaneInfo z; memset(&z, 0, sizeof(z)); *pi = z; }
+    return;
+  }
+  const int w = ti.w, h = ti.h, depth = plane_depth(p), c = 1 << depth, half = c >> 1;
+  const uint32_t npix = (uint32_t)w * h;
+  uint16_t* D = j.sym + fin_plane_off(j, t, p);
+  uint32_t* fh = j.hist + (size_t)(t * j.spt + KS_FIN + p) * 512;
+  const uint32_t* mh = j.hist + (size_t)(t * j.spt + KS_MED + p) * 512;
+  const int xt = (w + 39) / 40, yt = (h + 39) / 40;               // layer_encode.hpp:124-132, :150-151
+  const bool grid = xt > 1 || yt > 1;
+  if (!grid) {
+    // no search: the layer keeps the MED residuals (00 00 00 10 header)
+    const uint16_t* M = j.sym + med_plane_off(j, t, p);
+    for (uint32_t q = tid; q < npix; q += NT) D[q] = M[q];
+    for (int i = tid; i < 512; i += NT) fh[i] = mh[i];
+    if (tid == 0) {
+      PlaneInfo z; memset(&z, 0, sizeof(z));
+      z.present = 1; z.depth = depth; z.fixed_len = 5;
+      *pi = z;
+    }
+    return;
+  }
+  // the plane's data values, staged in the searched-residual slot (overwritten at the end)
+  for (uint32_t q = tid; q < npix; q += NT) D[q] = (uint16_t)plane_value(j, ti, t, p, q);
+  // entropy of the MED residuals over all pixels, freq = 1 + count (layer_encode.hpp:133-144)
+  const double* lg = nullptr;
+  for (int k = 0; k < 4; k++) if (j.lg_n[k] == npix) lg = j.lg + j.lg_off[k];
+  for (int i = tid; i < c; i += NT) S.ent[i] = lg[1 + mh[i]];
+  __syncthreads();
+  const int ncell = xt * yt, npred = j.speed * 5 < 14 ? j.speed * 5 : 14;
+  const int tw = (w + xt - 1) / xt, th = (h + yt - 1) / yt;
+  AllCtx a{D, w, h, tw, th, xt, c, half, S.plist};
+  for (int pass = 0; pass < (j.speed > 2 ? 2 : 1); pass++) {
+    if (pass == 1) {
+      // refine (:215-231): entropy of the first channelpredict_all residuals
+      for (int i = tid; i < 512; i += NT) S.hist[i] = 0;
+      __syncthreads();
+      for (uint32_t q = tid; q < npix; q += NT) {
+        const int y = (int)(q / (uint32_t)w), x = (int)(q - (uint32_t)y * w);
+        atomicAdd(&S.hist[resid_all(a, x, y)], 1u);
+      }
+      __syncthreads();
+      for (int i = tid; i < c; i += NT) S.ent[i] = lg[1 + S.hist[i]];
+      __syncthreads();
+    }
+    for (int k = tid; k < ncell * npred; k += NT) {
+      const int cell = k / npred, m = k % npred;
+      S.cost[cell * 14 + m] = cell_cost(D, w, h, depth, xt, yt, cell % xt, cell / xt, kMasks[m], S.ent,
+                                        S.top[tid], S.bp[tid]);
+    }
+    __syncthreads();
+    for (int cell = tid; cell < ncell; cell += NT) {
+      double best = 99999999999.0;                                // :177
+      int bi = 0;
+      for (int m = 0; m < npred; m++) {
+        const double v = S.cost[cell * 14 + m];
+        if (v < best) { best = v; bi = m; }
+      }
+      S.plist[cell] = kMasks[bi];
+      S.pidx[cell] = (uint8_t)bi;
+    }
+    __syncthreads();
+  }
+  // final channelpredict_all residuals, in place over the staged data: rows from the last up,
+  // each row read completely before it is overwritten (reads reach rows y-2..y only)
+  for (int i = tid; i < 512; i += NT) S.hist[i] = 0;
+  __syncthreads();
+  for (int y = h - 1; y >= 0; y--) {
+    uint32_t rv[4];
+    int n = 0;
+    for (int x = tid; x < w && n < 4; x += NT) rv[n++] = resid_all(a, x, y);   // w < 512
+    __syncthreads();
+    n = 0;
+    for (int x = tid; x < w && n < 4; x += NT) {
+      D[(long)y * w + x] = (uint16_t)rv[n];
+      atomicAdd(&S.hist[rv[n]], 1u);
+      n++;
+    }
+    __syncthreads();
+  }
+  for (int i = tid; i < 512; i += NT) fh[i] = S.hist[i];
+  // predictor map: used masks and their order (:279-307)
+  if (tid == 0) {
+    uint32_t used = 0;
+    for (int i = 0; i < ncell; i++) used |= 1u << S.pidx[i];
+    uint32_t rank[14], k = 0;
+    for (int m = 0; m < 14; m++) rank[m] = (used >> m) & 1 ? k++ : 0;
+    uint16_t* ms = j.sym + map_sym_off(j, t, p);
+    for (int i = 0; i < ncell; i++) ms[i] = (uint16_t)rank[S.pidx[i]];
+    PlaneInfo z; memset(&z, 0, sizeof(z));
+    z.present = 1; z.depth = depth; z.xt = xt; z.yt = yt;
+    z.used = k; z.used_bits = used;
+    z.fixed_len = 1 + 3 + 2 * k;
+    *pi = z;
+  }
+}
+
+// ---------------------------------------------------------------- LZ at seek distance 10..14
+
+__device__ __forceinline__ uint32_t tile_px(const EncodeJob& j, const TileInfo& ti, uint32_t q) {
+  const uint32_t y = q / (uint32_t)ti.w, x = q - y * (uint32_t)ti.w;
+  const uint8_t* px = j.rgb + ((size_t)(ti.y0 + y) * j.W + ti.x0 + x) * 3;
+  return px[0] | (px[1] << 8) | (px[2] << 16);
+}
+
+__device__ __forceinline__ uint32_t fp4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  uint32_t h = a * 0x9E3779B1u;
+  h = (h ^ b) * 0x85EBCA77u;
+  h = (h ^ c) * 0xC2B2AE3Du;
+  h = (h ^ d) * 0x27D4EB2Fu;
+  return (h ^ (h >> 15)) | 1u;
+}
+
+// fingerprint of the 4-pixel window starting at every position (0: fewer than 4 pixels left)
+__global__ __launch_bounds__(NT) void k_lzfp(EncodeJob j) {
+  const int t = blockIdx.y;
+  const TileInfo ti = j.tiles[t];
+  const uint32_t npix = (uint32_t)ti.w * ti.h;
+  for (uint32_t q = blockIdx.x * NT + threadIdx.x; q < npix; q += gridDim.x * NT) {
+    uint32_t f = 0;
+    if (q + 3 < npix) f = fp4(tile_px(j, ti, q), tile_px(j, ti, q + 1), tile_px(j, ti, q + 2), tile_px(j, ti, q + 3));
+    j.fpb[(size_t)t * j.npix_cap + q] = f;
+  }
+}
+
+// exact candidate screen: q can start a match of length >= 4 only if an equal window starts at
+// q - b for some b <= min(limit, q), or at q - k*w with k*w <= 65536 (lz.hpp:35, :55); equal
+// windows have equal fingerprints, so the screen never misses one.  Chunks of 256 positions in
+// order, the last `limit` fingerprints in an LDS ring.
+__global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring) {
+  extern __shared__ uint32_t fr[];
+  const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const TileInfo ti = j.tiles[t];
+  const uint32_t npix = (uint32_t)ti.w * ti.h, w = ti.w;
+  const uint32_t* F = j.fpb + (size_t)t * j.npix_cap;
+  uint64_t* cand = j.candbits + (size_t)t * (j.npix_cap / 64);
+  uint32_t ncand = 0;
+  for (uint32_t base = 0; base < npix; base += NT) {
+    const uint32_t q = base + tid;
+    const uint32_t f = q < npix ? F[q] : 0u;
+    fr[q & (ring - 1)] = f;
+    __syncthreads();
+    bool c = false;
+    if (f) {
+      const uint32_t bm = q < (uint32_t)limit ? q : (uint32_t)limit;
+      for (uint32_t b = 1; b <= bm; b++) {
+        if (fr[(q - b) & (ring - 1)] == f) { c = true; break; }
+      }
+      if (!c) {
+        for (uint32_t b = w; b <= 65536u && b <= q; b += w) {
+          if (b > bm && F[q - b] == f) { c = true; break; }
+        }
+      }
+    }
+    const uint64_t word = __ballot(c);
+    if (lane == 0 && q < npix) cand[q >> 6] = word;
+    ncand += lane == 0 ? (uint32_t)__popcll(word) : 0u;
+    __syncthreads();
+  }
+  if (lane == 0 && ncand) atomicAdd(&j.tiles[t].ncand, ncand);
+}
+
+__device__ __forceinline__ uint64_t wmax64(uint64_t v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t u = __shfl_xor(v, o);
+    v = u > v ? u : v;
+  }
+  return v;
+}
+
+// run length of the match of q against q - b (lz.hpp:37-45), at most 259
+__device__ __forceinline__ uint32_t run_len(const EncodeJob& j, const TileInfo& ti, uint32_t npix, uint32_t q, uint32_t b) {
+  uint32_t L = 0;
+  while (q + L < npix && L < 259 && tile_px(j, ti, q + L) == tile_px(j, ti, q + L - b)) L++;
+  return L;
+}
+
+// greedy scan (lz.hpp:32-95) over the candidates, one wave per tile, + the four LZ streams
+__global__ __launch_bounds__(64) void k_lzscan(EncodeJob j, int limit) {
+  const int t = blockIdx.x, lane = threadIdx.x;
+  TileInfo ti = j.tiles[t];
+  const uint32_t npix = (uint32_t)ti.w * ti.h, nwords = (npix + 63) / 64, w = ti.w;
+  const uint64_t* bits = j.candbits + (size_t)t * (j.npix_cap / 64);
+  const uint32_t* F = j.fpb + (size_t)t * j.npix_cap;
+  uint32_t* mt = j.matches + (size_t)t * 3 * (j.lz_cap + 1);
+  int bonus = 0;                                                      // choh.cpp:139-154
+  if (ti.colours != -1) {
+    if (ti.colours <= 4) bonus = 32;
+    else if (ti.colours <= 8) bonus = 20;
+    else if (ti.colours <= 16) bonus = 10;
+    else if (ti.colours <= 32) bonus = 2;
+  }
+  const uint32_t thr = 4 + bonus;
+  uint32_t nm = 0, pos = 0;
+  bool overflow = false;
+  while (ti.ncand && pos < npix) {
+    uint32_t q = 0xffffffffu;
+    for (uint32_t wi = pos >> 6; wi < nwords; wi += 64) {
+      uint64_t wv = (wi + lane < nwords) ? bits[wi + lane] : 0;
+      if (wi + lane == (pos >> 6)) wv &= ~0ull << (pos & 63);
+      const uint64_t bal = __ballot(wv != 0);
+      if (bal) {
+        const int l = __ffsll((unsigned long long)bal) - 1;
+        const uint64_t word = __shfl(wv, l);
+        q = (wi + l) * 64 + (__ffsll((unsigned long long)word) - 1);
+        break;
+      }
+    }
+    if (q == 0xffffffffu) break;
+    const uint32_t f = F[q];
+    // horizontal: b = 1 .. min(limit, q), longest first, then the smallest b; stop at 259
+    const uint32_t bm = q < (uint32_t)limit ? q : (uint32_t)limit;
+    uint64_t best = 0;                                                // (L << 32) | (~b)
+    for (uint32_t b0 = 1; b0 <= bm; b0 += 64) {
+      const uint32_t b = b0 + lane;
+      uint64_t key = 0;
+      if (b <= bm && F[q - b] == f) {
+        const uint32_t L = run_len(j, ti, npix, q, b);
+        key = ((uint64_t)L << 32) | (uint32_t)(~b);
+      }
+      key = wmax64(key);
+      if (key > best) best = key;
+      if ((best >> 32) == 259) break;
+    }
+    // vertical (lz.hpp:54-74): whole rows up to 65536 back, strictly longer only
+    if ((best >> 32) < 259) {
+      uint64_t vb = 0;
+      for (uint32_t k0 = 1; k0 * w <= 65536u && k0 * w <= q; k0 += 64) {
+        const uint32_t k = k0 + lane, b = k * w;
+        uint64_t key = 0;
+        if (b <= 65536u && b <= q && F[q - b] == f) {
+          const uint32_t L = run_len(j, ti, npix, q, b);
+          key = ((uint64_t)L << 32) | (uint32_t)(~b);
+        }
+        key = wmax64(key);
+        if (key > vb) vb = key;
+      }
+      if ((vb >> 32) > (best >> 32)) best = vb;
+    }
+    const uint32_t longest = (uint32_t)(best >> 32), bb = ~(uint32_t)best;
+    if (longest >= thr) {
+      if (nm < j.lz_cap) {
+        if (lane == 0) { mt[3 * nm] = q; mt[3 * nm + 1] = longest; mt[3 * nm + 2] = bb; }
+      } else {
+        overflow = true;
+      }
+      nm++;
+      pos = q + longest;
+    } else {
+      pos = q + 1;
+    }
+  }
+  // streams (lz.hpp:75-95): future, length - 4, back % 256, back / 256 (as u8)
+  uint16_t* lz0 = j.sym + lz_sym_off_s(j, t, 0);
+  uint16_t* lz1 = j.sym + lz_sym_off_s(j, t, 1);
+  uint16_t* lz2 = j.sym + lz_sym_off_s(j, t, 2);
+  uint16_t* lz3 = j.sym + lz_sym_off_s(j, t, 3);
+  uint32_t nf = 0, prev_end = 0;
+  const uint32_t nmk = nm < j.lz_cap ? nm : j.lz_cap;
+  for (uint32_t m = 0; m <= nmk; m++) {
+    const bool tail = m == nmk;
+    const uint32_t mpos = tail ? npix : mt[3 * m];
+    const uint32_t g = mpos - prev_end, n255 = g / 255;
+    if (nf + n255 + 1 > j.lz_cap) { overflow = true; break; }
+    for (uint32_t k = lane; k < n255; k += 64) lz0[nf + k] = 255;
+    nf += n255;
+    if (!tail) {
+      if (lane == 0) {
+        lz0[nf] = (uint16_t)(g % 255);
+        lz1[m] = (uint16_t)(mt[3 * m + 1] - 4);
+        lz2[m] = (uint16_t)(mt[3 * m + 2] % 256);
+        lz3[m] = (uint16_t)(uint8_t)(mt[3 * m + 2] / 256);
+      }
+      nf++;
+      prev_end = mpos + mt[3 * m + 1];
+    }
+  }
+  uint32_t nk = 0;
+  for (uint32_t m = lane; m < nmk; m += 64) nk += mt[3 * m + 1];
+  for (int o = 32; o > 0; o >>= 1) nk += __shfl_xor(nk, o);
+  if (lane == 0) {
+    if (overflow) ti.flags |= TF_OVERFLOW;
+    ti.nmatch = nm;
+    ti.nfut = nf;
+    ti.nclean = (overflow || !nmk) ? npix : npix - nk;
+    j.tiles[t] = ti;
+  }
+}
+
+// ---------------------------------------------------------------- stream set-up and choices
+
+__global__ __launch_bounds__(128) void k_setup_s(EncodeJob j) {
+  const int t = blockIdx.x, k = threadIdx.x;
+  if (k >= SPT_S) return;
+  const TileInfo ti = j.tiles[t];
+  const uint32_t nclean = ti.nclean;
+  const uint32_t nmk = ti.nmatch < j.lz_cap ? ti.nmatch : j.lz_cap;
+  const uint32_t sid = t * SPT_S + k;
+  StreamInfo st;
+  memset(&st, 0, sizeof(st));
+  st.mode = SM_EMPTY;
+  if (k < KS_MED) {                                                   // LZ (lz.hpp:100-142)
+    st.sym_off = lz_sym_off_s(j, t, k);
+    st.slab_off = lz_slab_off_s(j, t, k);
+    st.slab_cap = j.lz_cap + 8;
+    st.n = k == 0 ? ti.nfut : nmk;
+    st.range = 256;
+    st.pb = 10;
+  } else {
+    int p, kind;
+    if (k < KS_FIN) { kind = KS_MED; p = k - KS_MED; }
+    else if (k < KS_MAP) { kind = KS_FIN; p = k - KS_FIN; }
+    else if (k < KS_VAR) { kind = KS_MAP; p = k - KS_MAP; }
+    else { kind = KS_VAR; p = (k - KS_VAR) / 8; }
+    const PlaneInfo pi = j.pinfo[(size_t)t * HOH_NPLANE_S + p];
+    if (pi.present) {
+      const uint32_t range = 1u << pi.depth;
+      if (kind == KS_MED) {
+        st.sym_off = med_plane_off(j, t, p);
+        st.slab_off = plane_slab_off_s(j, t, p);
+        st.slab_cap = j.npix_cap + 8;
+        st.n = nclean; st.range = range; st.pb = 15; st.fast = 1;
+        st.hist_src = sid + 1;
+      } else if (kind == KS_MAP) {
+        if (pi.xt) {
+          st.sym_off = map_sym_off(j, t, p);
+          st.slab_off = map_slab_off_s(j, t, p);
+          st.slab_cap = HOH_MAPCAP + 8;
+          st.n = pi.xt * pi.yt; st.range = pi.used; st.pb = 8;        // layer_encode.hpp:308-315
+        }
+      } else if (kind == KS_VAR) {
+        st.sym_off = fin_plane_off(j, t, p);
+        st.n = nclean; st.range = range; st.pb = kVarPb[(k - KS_VAR) % 8];
+        st.sizeonly = 1;
+        st.hist_src = t * SPT_S + KS_FIN + p + 1;
+      }
+      // KS_FIN stays absent until k_choose_s activates it
+    }
+  }
+  j.streams[sid] = st;
+}
+
+// layer_encode.hpp:22, :115-120, :326-398 on the stream sizes
+__global__ __launch_bounds__(64) void k_choose_s(EncodeJob j) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= j.ntiles * HOH_NPLANE_S) return;
+  const int t = i / HOH_NPLANE_S, p = i % HOH_NPLANE_S;
+  PlaneInfo pi = j.pinfo[i];
+  if (!pi.present) return;
+  const TileInfo ti = j.tiles[t];
+  const StreamInfo* st = j.streams + (size_t)t * SPT_S;
+  const uint64_t n = (uint64_t)ti.w * ti.h;
+  uint64_t possible = (pi.depth * n + (pi.depth * n) % 8 + 1024) / 8;
+  uint32_t valid = 0, fin = 0, fin_pb = 0;
+  const uint64_t sm = st[KS_MED + p].size;
+  if (sm < possible) { possible = sm; valid = 1; }
+  const StreamInfo* v = st + KS_VAR + p * 8;
+  const uint64_t t1 = v[0].size, t2 = v[1].size;
+  if (t1 < t2) {
+    if (t1 < possible) possible = t1;                                 // not swapped (Q14)
+    for (int k = 2; k < 5; k++) if (v[k].size < possible) { possible = v[k].size; valid = 1; fin = 1; fin_pb = v[k].pb; }
+  } else {
+    if (t2 < possible) possible = t2;
+    for (int k = 5; k < 8; k++) if (v[k].size < possible) { possible = v[k].size; valid = 1; fin = 1; fin_pb = v[k].pb; }
+  }
+  pi.possible = (uint32_t)possible;
+  pi.valid = valid;
+  pi.perm_final = fin;
+  pi.size = pi.fixed_len + (pi.xt ? st[KS_MAP + p].size : 0) + (uint32_t)possible;
+  pi.limit = pi.size;
+  j.pinfo[i] = pi;
+  if (fin) {
+    StreamInfo f = v[0];
+    f.pb = fin_pb;
+    f.sizeonly = 0;
+    f.slab_off = plane_slab_off_s(j, t, p);                          // the MED stream's slab: unused now
+    f.slab_cap = j.npix_cap + 8;
+    f.mode = SM_EMPTY; f.words = 0; f.size = 0; f.err = 0;
+    j.streams[(size_t)t * SPT_S + KS_FIN + p] = f;
+  }
+}
+
+// ---------------------------------------------------------------- tile layout and fixed bytes
+
+// byte ranges of one layer in the file: [fixed header][map stream][permanent prefix], clipped to
+// the layer's limit (the Q15 prefix of an indexed layer)
+__device__ void place_layer(const EncodeJob& j, int t, int p, uint64_t off, uint32_t limit) {
+  PlaneInfo& pi = j.pinfo[(size_t)t * HOH_NPLANE_S + p];
+  StreamInfo* st = j.streams + (size_t)t * SPT_S;
+  pi.out_off = off;
+  pi.limit = limit;
+  uint64_t o = pi.fixed_len;
+  StreamInfo& mp = st[KS_MAP + p];
+  if (pi.xt) {
+    mp.out_off = off + o;
+    if (o >= limit) mp.drop = 1;
+    else if (o + mp.size > limit) mp.clip = (uint32_t)(limit - o);
+    o += mp.size;
+  }
+  StreamInfo& pm = st[(pi.perm_final ? KS_FIN : KS_MED) + p];
+  pm.out_off = off + o;
+  const uint64_t want = pi.possible;
+  const uint64_t room = limit > o ? limit - o : 0;
+  const uint64_t keep = want < room ? want : room;
+  if (keep == 0) pm.drop = 1;
+  else pm.clip = (uint32_t)keep;
+  st[(pi.perm_final ? KS_MED : KS_FIN) + p].drop = 1;
+}
+
+__global__ __launch_bounds__(1024) void k_layout_s(EncodeJob j) {
+  __shared__ uint64_t part[1024];
+  __shared__ uint64_t tot_size, tot_vlen;
+  const int tid = threadIdx.x;
+  if (tid == 0) { tot_size = 0; tot_vlen = 0; }
+  __syncthreads();
+  for (int base = 0; base < j.ntiles; base += 1024) {
+    const int t = base + tid;
+    uint64_t sz = 0, vl = 0;
+    if (t < j.ntiles) {
+      TileInfo ti = j.tiles[t];
+      StreamInfo* st = j.streams + (size_t)t * SPT_S;
+      const PlaneInfo* pi = j.pinfo + (size_t)t * HOH_NPLANE_S;
+      uint32_t bad = ti.flags & (TF_UNREPRODUCIBLE | TF_UNSUPPORTED | TF_OVERFLOW);
+      for (int k = 0; k < SPT_S; k++) if (st[k].err) bad |= TF_OVERFLOW;
+      const uint32_t lzb = 1 + st[0].size + st[1].size + st[2].size + st[3].size;   // lz.hpp:98-142
+      uint64_t s64 = 2 + 1 + lzb;
+      if (ti.flags & TF_GREY) {
+        ti.mode = 0;                                              // bitimage (non-binary grey: flagged)
+      } else {
+        for (int p = 0; p < HOH_NPLANE_S; p++) if (pi[p].present && !pi[p].valid) bad |= TF_UNREPRODUCIBLE;
+        const uint64_t L1 = pi[0].size, L2 = pi[1].size, L3 = pi[2].size;
+        uint64_t best = L1 + L2 + L3 + lzb;                        // choh.cpp:295
+        uint32_t mode = 128, ch1 = 0, c2 = 1, c3 = 2;
+        if (pi[3].present && pi[3].size + 3ull * ti.colours + 1 + lzb < best) {   // :298-308
+          best = pi[3].size + 3ull * ti.colours + 1 + lzb;
+          mode = 127; ch1 = 3;
+        }
+        if (pi[4].present && pi[4].size + L1 + pi[5].size + lzb < best) {         // :309-325
+          mode = 2; c2 = 4; c3 = 5;
+        }
+        if (ch1 == 3 && pi[3].size < L1) bad |= TF_UNREPRODUCIBLE;   // Q15 prefix past the layer
+        ti.mode = mode;
+        if (mode == 127) s64 += L1;
+        else s64 += 1 + hoh_varint_len(L1) + hoh_varint_len(pi[c2].size) + L1 + pi[c2].size + pi[c3].size;
+        ti.chmap = ch1 | (c2 << 4) | (c3 << 8);
+      }
+      if (bad) atomicOr(j.gerr, bad << 8);
+      ti.lz_bytes = lzb;
+      ti.size = (uint32_t)s64;
+      j.tiles[t] = ti;
+      sz = s64;
+      if (j.tile_sizes) j.tile_sizes[t] = (uint32_t)s64;
+      if (j.write_table && t + 1 < j.ntiles) vl = hoh_varint_len(s64);
+    }
+    if (sz) atomicAdd((unsigned long long*)&tot_size, (unsigned long long)sz);
+    if (vl) atomicAdd((unsigned long long*)&tot_vlen, (unsigned long long)vl);
+  }
+  __syncthreads();
+  const uint64_t first = j.prefix + tot_vlen;
+  uint64_t carry_s = 0, carry_v = 0;
+  for (int base = 0; base < j.ntiles; base += 1024) {
+    const int t = base + tid;
+    uint64_t sz = 0, vl = 0;
+    if (t < j.ntiles) {
+      sz = j.tiles[t].size;
+      if (j.write_table && t + 1 < j.ntiles) vl = hoh_varint_len(sz);
+    }
+    part[tid] = sz;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) { const uint64_t u = tid >= o ? part[tid - o] : 0; __syncthreads(); part[tid] += u; __syncthreads(); }
+    const uint64_t es = part[tid] - sz, chunk_s = part[1023];
+    __syncthreads();
+    part[tid] = vl;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) { const uint64_t u = tid >= o ? part[tid - o] : 0; __syncthreads(); part[tid] += u; __syncthreads(); }
+    const uint64_t ev = part[tid] - vl, chunk_v = part[1023];
+    __syncthreads();
+    if (t < j.ntiles) {
+      TileInfo ti = j.tiles[t];
+      ti.off = first + carry_s + es;
+      ti.pad = (uint32_t)(j.prefix + carry_v + ev);
+      j.tiles[t] = ti;
+      StreamInfo* st = j.streams + (size_t)t * SPT_S;
+      uint64_t o = ti.off + 3 + 1;
+      for (int k = 0; k < 4; k++) { st[k].out_off = o; o += st[k].size; }
+      for (int p = 0; p < HOH_NPLANE_S; p++) {                  // everything not placed below is dropped
+        st[KS_MED + p].drop = 1; st[KS_FIN + p].drop = 1; st[KS_MAP + p].drop = 1;
+        for (int v = 0; v < 8; v++) st[KS_VAR + p * 8 + v].drop = 1;
+      }
+      if (!(ti.flags & TF_GREY)) {
+        const PlaneInfo* pi = j.pinfo + (size_t)t * HOH_NPLANE_S;
+        const uint32_t ch1 = ti.chmap & 15, c2 = (ti.chmap >> 4) & 15, c3 = (ti.chmap >> 8) & 15;
+        const uint32_t L1 = pi[0].size;
+        for (int k = KS_MED; k < KS_VAR; k++) st[k].drop = 0;
+        if (ti.mode == 127) {
+          place_layer(j, t, ch1, o, L1);
+        } else {
+          o += 1 + hoh_varint_len(L1) + hoh_varint_len(pi[c2].size);
+          place_layer(j, t, ch1, o, L1);
+          o += L1;
+          place_layer(j, t, c2, o, pi[c2].size);
+          o += pi[c2].size;
+          place_layer(j, t, c3, o, pi[c3].size);
+        }
+        // layers that are not part of the tile
+        for (int p = 0; p < HOH_NPLANE_S; p++) {
+          if (p == (int)ch1 || (ti.mode != 127 && (p == (int)c2 || p == (int)c3))) continue;
+          st[KS_MED + p].drop = 1; st[KS_FIN + p].drop = 1; st[KS_MAP + p].drop = 1;
+        }
+      }
+    }
+    carry_s += chunk_s;
+    carry_v += chunk_v;
+  }
+  if (tid == 0) *j.total = first + tot_size;
+}
+
+// fixed bytes: tile framing (choh.cpp:115-116, :328, :351-356), LZ flags (lz.hpp:98) and every
+// placed layer's header (layer_encode.hpp:57, :276-297 or :320-325), clipped to its limit
+__global__ __launch_bounds__(64) void k_tilebytes_s(EncodeJob j) {
+  const int t = blockIdx.x * 64 + threadIdx.x;
+  if (t >= j.ntiles || *j.total > j.cap || *j.gerr) return;
+  const TileInfo ti = j.tiles[t];
+  uint8_t* o = j.out + ti.off;
+  o[0] = 0; o[1] = 0;
+  o[2] = (uint8_t)ti.mode;
+  o[3] = 0x03;
+  if (j.write_table && t + 1 < j.ntiles) hoh_write_varint(j.out, ti.pad, ti.size);
+  if (ti.flags & TF_GREY) return;
+  const PlaneInfo* pi = j.pinfo + (size_t)t * HOH_NPLANE_S;
+  const uint32_t ch1 = ti.chmap & 15, c2 = (ti.chmap >> 4) & 15, c3 = (ti.chmap >> 8) & 15;
+  if (ti.mode != 127) {
+    uint32_t p = 3 + ti.lz_bytes;
+    o[p++] = 0x24;
+    p = hoh_write_varint(o, p, pi[0].size);
+    p = hoh_write_varint(o, p, pi[c2].size);
+  }
+  const uint32_t layers[3] = {ch1, c2, c3};
+  for (int k = 0; k < (ti.mode == 127 ? 1 : 3); k++) {
+    const PlaneInfo& L = pi[layers[k]];
+    uint8_t hb[32];
+    uint32_t n = 0;
+    hb[n++] = 0x10;
+    if (L.xt) {
+      hb[n++] = (uint8_t)(L.xt - 1);
+      hb[n++] = (uint8_t)(L.yt - 1);
+      hb[n++] = (uint8_t)L.used;
+      for (int m = 0; m < 14; m++) {
+        if (!((L.used_bits >> m) & 1)) continue;
+        hb[n++] = (uint8_t)(kMasks[m] >> 8);
+        hb[n++] = (uint8_t)(kMasks[m] & 255);
+      }
+    } else {
+      hb[n++] = 0; hb[n++] = 0; hb[n++] = 0x00; hb[n++] = 0x10;
+    }
+    uint8_t* d = j.out + L.out_off;
+    for (uint32_t i = 0; i < n && i < L.limit; i++) d[i] = hb[i];
+  }
+}
+
+// ---------------------------------------------------------------- orchestration
+
+void encode_speed_s(const EncodeJob& j, hipStream_t s, void (*mark)(void*, const char*), void* mc) {
+  const int dist = j.speed == 1 ? 10 : j.speed == 2 ? 11 : j.speed == 3 ? 12 : 14;   // choh.cpp:125-137
+  const int limit = 1 << dist;
+  int ring = 1;
+  while (ring < limit + NT) ring <<= 1;
+  if (j.speed >= 3) hipLaunchKernelGGL(k_rawmed, dim3(j.ntiles), dim3(NT), 0, s, j);
+  hipLaunchKernelGGL(k_search, dim3(j.ntiles * HOH_NPLANE_S), dim3(NT), sizeof(SearchLds), s, j);
+  mark(mc, "search");
+  hipLaunchKernelGGL(k_lzfp, dim3(16, j.ntiles), dim3(NT), 0, s, j);
+  hipLaunchKernelGGL(k_lzcand, dim3(j.ntiles), dim3(NT), (size_t)ring * 4, s, j, limit, ring);
+  hipLaunchKernelGGL(k_lzscan, dim3(j.ntiles), dim3(64), 0, s, j, limit);
+  launch_nuke(j, s);
+  mark(mc, "lz");
+  hipLaunchKernelGGL(k_setup_s, dim3(j.ntiles), dim3(128), 0, s, j);
+  const int S = j.ntiles * SPT_S;
+  launch_tables(j, S, s);
+  mark(mc, "tables");
+  launch_rans_fast(j, j.ntiles * 6, s, SidMap{3, KS_MED}, j.ntiles * 3, SidMap{3, KS_MED + 3});
+  launch_rans_gen(j, S, s);
+  launch_finalize(j, S, s);
+  mark(mc, "rans_enc");
+  hipLaunchKernelGGL(k_choose_s, dim3((j.ntiles * HOH_NPLANE_S + 63) / 64), dim3(64), 0, s, j);
+  const SidMap fin{HOH_NPLANE_S, KS_FIN};
+  launch_tables(j, j.ntiles * HOH_NPLANE_S, s, fin);
+  launch_rans_gen(j, j.ntiles * HOH_NPLANE_S, s, fin);
+  launch_finalize(j, j.ntiles * HOH_NPLANE_S, s, fin);
+  mark(mc, "rans_enc_final");
+  hipLaunchKernelGGL(k_layout_s, dim3(1), dim3(1024), 0, s, j);
+  hipLaunchKernelGGL(k_tilebytes_s, dim3((j.ntiles + 63) / 64), dim3(64), 0, s, j);
+  launch_streambytes(j, S, s);
+  mark(mc, "assemble");
+}

@@ -188,14 +188,15 @@ class Index:
             pass
 
 
-def encode_image(rgb_dev, W, H, out_dev=None, ctx=None, index=None):
-    """rgb_dev: uint8 torch tensor (W*H*3) in HBM.  Returns (out tensor, size, printed)."""
+def encode_image(rgb_dev, W, H, out_dev=None, ctx=None, index=None, speed=0):
+    """rgb_dev: uint8 torch tensor (W*H*3) in HBM; speed = choh's -sN.  Returns (out tensor, size,
+    printed).  -s1..-s4 files carry no side index (they are undecodable by construction, Q14)."""
     import torch
     ctx = ctx or default_ctx()
     if out_dev is None:
         out_dev = torch.empty(lib().hoh_encode_bound(W, H), dtype=torch.uint8, device=rgb_dev.device)
     n, printed = C.c_size_t(0), C.c_size_t(0)
-    r = lib().hoh_encode_image_ix(ctx.h, vp(rgb_dev.data_ptr()), W, H, 0, vp(out_dev.data_ptr()),
+    r = lib().hoh_encode_image_ix(ctx.h, vp(rgb_dev.data_ptr()), W, H, speed, vp(out_dev.data_ptr()),
                                   out_dev.numel(), C.byref(n), C.byref(printed),
                                   index.h if index is not None else None, _stream_ptr(torch))
     check(r, "hoh_encode_image")
@@ -273,13 +274,13 @@ def synth_rgb_dev(W, H, seed=1, noise=4, ctx=None, device="cuda", row0=0):
 
 # ------------------------------------------------------------------ host-buffer API (reference names)
 
-def choh(rgb, ctx=None):
-    """`choh in out W H -s0` on an (H, W, 3) uint8 array -> (file bytes, printed size)."""
+def choh(rgb, ctx=None, speed=0):
+    """`choh in out W H -sN` on an (H, W, 3) uint8 array -> (file bytes, printed size)."""
     import torch
     rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
     H, W, _ = rgb.shape
     d = torch.from_numpy(rgb.reshape(-1)).cuda()
-    out, n, printed = encode_image(d, W, H, ctx=ctx)
+    out, n, printed = encode_image(d, W, H, ctx=ctx, speed=speed)
     torch.cuda.synchronize()
     return out[:n].cpu().numpy().tobytes(), printed
 
