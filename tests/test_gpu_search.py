@@ -55,3 +55,25 @@ def test_choh_speed_parity(hoh, orc, name, sp, img):
     assert printed == ref_printed
     assert len(data) == len(ref)
     assert data == ref
+
+
+def test_choh_8192_speed_golden(hoh):
+    """config 5: 8192^2 at -s1/-s2/-s3 against the reference choh's own output (size + SHA-256)"""
+    import hashlib
+    import json
+    import os
+    import time
+    import torch
+    g = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden_speed.json")))
+    for f in g["files"]:
+        sp = f["spec"]
+        d = hoh.synth_rgb_dev(sp["W"], sp["H"], sp["seed"], sp["noise"])
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        out, n, printed = hoh.encode_image(d, sp["W"], sp["H"], speed=sp["speed"])
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t
+        print("-s%d 8192^2: %d B in %.1f ms" % (sp["speed"], n, el * 1e3))
+        assert n == f["out"]["len"]
+        assert printed == f["printed"]
+        assert hashlib.sha256(out[:n].cpu().numpy().tobytes()).hexdigest() == f["out"]["sha256"]
