@@ -33,9 +33,9 @@ extern "C" {
 #define HOH_E_UNREPRODUCIBLE 5  /* the reference writes uninitialised bytes for this input
                                    (grey non-binary tiles, choh.cpp:196-205; palette prefix
                                    longer than the indexed layer, choh.cpp:301-308)             */
-#define HOH_E_UNSUPPORTED 6     /* valid but not implemented on this path (-s1..-s4 predictor
-                                   search, 4-channel formats); decoder: indexed (mode 127)
-                                   tiles, which carry no palette                   */
+#define HOH_E_UNSUPPORTED 6     /* valid but not implemented on this path (4-channel formats);
+                                   decoder: indexed (mode 127) tiles, which carry no palette
+                                   (SURVEY Q15), and -s>=1 layers (Q14)                         */
 #define HOH_E_CORRUPT 7         /* decoder: malformed or undecodable bitstream (incl. the
                                    reference's lossy raw tables)                     */
 #define HOH_E_NODEV 8           /* no GPU / HIP device unavailable                              */
@@ -54,15 +54,17 @@ int hoh_get_kernel_ms(hoh_ctx* ctx, const char** names, float* ms, int max);
 int hoh_get_kernel_stats(hoh_ctx* ctx, const char** names, double* total_ms, uint64_t* count, int max);
 void hoh_reset_kernel_stats(hoh_ctx* ctx);
 
-/* ---- image level: `choh in out W H -s0` / `dhoh in out` -------------------------------- */
+/* ---- image level: `choh in out W H -sN` / `dhoh in out` -------------------------------- */
 
 /* Worst-case .hoh size for a W x H image (stored planes + LZ streams + framing). */
 size_t hoh_encode_bound(int W, int H);
 
-/* Replaces choh.cpp:394-527 at cruncher_mode 0 (-s0).  Reads W*H*3 interleaved RGB bytes from
- * d_rgb, writes the exact bytes choh writes (header-only for untiled images) to
- * d_out.  *out_size = bytes written; *printed (optional) = the number choh prints
- * (choh.cpp:522).  speed must be 0. */
+/* Replaces choh.cpp:394-527.  speed = cruncher_mode (-s0 .. -s4; choh.cpp:408-427).  Reads
+ * W*H*3 interleaved RGB bytes from d_rgb, writes the exact bytes choh writes (header-only for
+ * untiled images) to d_out.  *out_size = bytes written; *printed (optional) = the
+ * number choh prints (choh.cpp:522).  -s1..-s4 run the predictor search, seek-distance LZ and
+ * prob_bits ladder (layer_encode.hpp:122-392); their files are undecodable by construction
+ * (SURVEY Q14), so they get no side index. */
 int hoh_encode_image(hoh_ctx* ctx, const uint8_t* d_rgb, int W, int H, int speed,
                      uint8_t* d_out, size_t cap, size_t* out_size, size_t* printed, void* stream);
 

@@ -39,11 +39,17 @@ def test_choh_dhoh_cli(tmp_path, W, H):
         assert (tmp_path / "back.rgb").read_bytes() == img.tobytes()
 
 
-def test_choh_rejects_other_speeds(tmp_path):
+@pytest.mark.parametrize("speed", [1, 3])
+def test_choh_speeds(tmp_path, speed):
+    from hoh_ans.synth import synth_rgb
+    img = synth_rgb(512, 256, 30 + speed, 3)
     src = tmp_path / "in.rgb"
-    src.write_bytes(bytes(768 * 512 * 3))
-    r = _run([os.path.join(BIN, "choh"), str(src), str(tmp_path / "o.hoh"), "768", "512", "-s1"])
-    assert r.returncode == 6
+    src.write_bytes(img.tobytes())
+    r = _run([os.path.join(BIN, "choh"), str(src), str(tmp_path / "o.hoh"), "512", "256", "-s%d" % speed])
+    assert r.returncode == 0, r.stderr
+    want, printed = oracle.choh(img, speed)
+    assert (tmp_path / "o.hoh").read_bytes() == want
+    assert int(r.stdout.strip().splitlines()[-1]) == printed
 
 
 def test_dropin_headers_roundtrip():

@@ -1,7 +1,8 @@
-// choh drop-in (choh.cpp:394-527): `choh in.rgb out.hoh width height [-s0]` on the GPU.
+// choh drop-in (choh.cpp:394-527): `choh in.rgb out.hoh width height [-sN]` on the GPU.
 // Writes the bytes the reference writes and prints the size it prints (header +
-// tile size for untiled images, of which only the header is written).  Only -s0 is implemented;
-// without a speed argument the reference would use -s1, here -s0 is used and a note printed.
+// tile size for untiled images, of which only the header is written).  Speeds -s0..-s4 as in the
+// reference (choh.cpp:408-427): default and unknown settings mean -s1 (the reference reads
+// argv[5] unchecked when it is missing; here that is the documented default).
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -31,11 +32,14 @@ int main(int argc, char** argv) {
     std::printf("invalid width or height\n");
     return 2;
   }
-  if (argc > 5 && std::strcmp(argv[5], "-s0") != 0) {
-    std::fprintf(stderr, "choh (GPU): only -s0 is implemented\n");
-    return HOH_E_UNSUPPORTED;
+  int speed = 1;
+  if (argc > 5) {
+    static const char* names[5] = {"-s0", "-s1", "-s2", "-s3", "-s4"};
+    int k = 0;
+    while (k < 5 && std::strcmp(argv[5], names[k]) != 0) k++;
+    if (k < 5) speed = k;
+    else std::printf("invalid speed setting\nusage: choh infile.rgb outfile.hoh width height -sN\n");
   }
-  if (argc == 5) std::fprintf(stderr, "choh (GPU): no speed given, using -s0\n");
   std::vector<uint8_t> in;
   if (!read_file(argv[1], in)) { std::printf("could not read %s\n", argv[1]); return 3; }
   const size_t raw = (size_t)W * H * 3;
@@ -48,7 +52,7 @@ int main(int argc, char** argv) {
   if (hipMalloc(&d_in, raw) != hipSuccess || hipMalloc(&d_out, cap) != hipSuccess) return HOH_E_HIP;
   if (hipMemcpy(d_in, in.data(), raw, hipMemcpyHostToDevice) != hipSuccess) return HOH_E_HIP;
   size_t n = 0, printed = 0;
-  r = hoh_encode_image(ctx, d_in, W, H, 0, d_out, cap, &n, &printed, nullptr);
+  r = hoh_encode_image(ctx, d_in, W, H, speed, d_out, cap, &n, &printed, nullptr);
   if (r != HOH_OK) { std::fprintf(stderr, "choh: %s\n", hoh_strerror(r)); return r; }
   std::vector<uint8_t> out(n);
   if (n && hipMemcpy(out.data(), d_out, n, hipMemcpyDeviceToHost) != hipSuccess) return HOH_E_HIP;
