@@ -21,6 +21,8 @@ void launch_unpredict_serial(const uint16_t* res, size_t nres, const uint16_t* b
 void launch_green(const uint8_t* rgb, size_t n, uint16_t* G, uint16_t* R, uint16_t* B, hipStream_t s);
 void launch_addgreen(const uint16_t* G, const uint16_t* R, const uint16_t* B, size_t n, uint8_t* o, hipStream_t s);
 void launch_compact(const uint16_t* in, const uint8_t* nuke, size_t n, uint16_t* out, uint64_t* count, hipStream_t s);
+int layer_encode_search(hoh_ctx* c, const uint16_t* data, size_t n, int w, int h, int depth, int cruncher,
+                        const uint8_t* nuke, uint8_t* out, size_t cap, size_t* written);
 
 namespace {
 
@@ -162,8 +164,9 @@ int hoh_layer_encode(hoh_ctx* c, const uint16_t* data, size_t size, int w, int h
                      const uint8_t* nuke, uint8_t* out, size_t cap, size_t* written) {
   if (!c || !data || !out || !written || w <= 0 || h <= 0 || (size_t)w * h != size || depth < 1 || depth > 12)
     return HOH_E_ARG;
-  if (cruncher != 0) return HOH_E_UNSUPPORTED;                          // -s>=1 predictor search
   (void)hipSetDevice(ctx_device(c));
+  if (cruncher > 4) return HOH_E_ARG;
+  if (cruncher != 0) return layer_encode_search(c, data, size, w, h, depth, (int)cruncher, nuke, out, cap, written);
   hipStream_t s = ctx_stream(c, nullptr);
   const size_t bound = hoh_entropy_bound(size, (size_t)1 << depth, 15);
   DevMem a(size * 2), res(size * 2 + 16), cl(size * 2 + 16), nk(nuke ? size : 16), cnt(16), eout(bound);
@@ -189,20 +192,53 @@ int hoh_layer_encode(hoh_ctx* c, const uint16_t* data, size_t size, int w, int h
   return HOH_OK;
 }
 
-// layer_decode.hpp:128-278 for -s0 layers; returns the full-depth plane (no u8 truncation, Q10)
+// layer_decode.hpp:128-278; returns the full-depth plane (no u8 truncation, Q10).  Layers with a
+// predictor map (-s>=1) go through the general unpredict_all; the 1x1 MED map of -s0 layers through
+// the fast path with MED on every row (Q9 fixed).
 int hoh_layer_decode(hoh_ctx* c, const uint8_t* in, size_t in_size, size_t bp, int w, int h, int depth,
                      const uint16_t* backref, uint16_t* out) {
-  if (!c || !in || !out || w <= 0 || h <= 0 || bp + 5 > in_size) return HOH_E_ARG;
-  if (in[bp] != 0x10) return HOH_E_UNSUPPORTED;                        // compaction / no prediction
-  if (in[bp + 1] != 0 || in[bp + 2] != 0) return HOH_E_UNSUPPORTED;    // predictor tiles (-s>=1)
-  if (in[bp + 3] != 0x00 || in[bp + 4] != 0x10) return HOH_E_UNSUPPORTED;
-  size_t cnt = 0;
-  int r = hoh_entropy_count(in, in_size, bp + 5, &cnt);
-  if (r) return r;
-  std::vector<uint16_t> res(cnt + 1);
-  size_t p = bp + 5, n = 0;
-  if ((r = hoh_decode_entropy(c, in, in_size, &p, res.data(), cnt, &n))) return r;
-  return hoh_unpredict_fastpath(c, res.data(), n, backref, w, h, depth, out);
+  if (!c || !in || !out || w <= 0 || h <= 0 || bp + 1 > in_size) return HOH_E_ARG;
+  const uint8_t tr = in[bp];
+  if (tr & 0xe0) return HOH_E_UNSUPPORTED;                             // compaction modes 1-7 (:141-195)
+  size_t p = bp + 1, cnt = 0, n = 0;
+  int r;
+  auto stream = [&](std::vector<uint16_t>& v) -> int {
+    int e = hoh_entropy_count(in, in_size, p, &cnt);
+    if (e) return e;
+    v.resize(cnt + 1);
+    return hoh_decode_entropy(c, in, in_size, &p, v.data(), cnt, &n);
+  };
+  std::vector<uint16_t> res;
+  if (!(tr & 0x10)) {                                                  // no prediction (:265-276)
+    if ((r = stream(res))) return r;
+    if (n != (size_t)w * h) return HOH_E_CORRUPT;
+    memcpy(out, res.data(), n * 2);
+    return HOH_OK;
+  }
+  if (p + 2 > in_size) return HOH_E_CORRUPT;
+  const int xt = in[p] + 1, yt = in[p + 1] + 1;                        // :198-199
+  p += 2;
+  std::vector<uint16_t> map((size_t)xt * yt);
+  if (xt == 1 && yt == 1) {                                            // :203-209
+    if (p + 2 > in_size) return HOH_E_CORRUPT;
+    map[0] = (uint16_t)((in[p] << 8) | in[p + 1]);
+    p += 2;
+  } else {                                                             // :210-229
+    if (p + 1 > in_size) return HOH_E_CORRUPT;
+    const int used = in[p++];
+    if (p + 2 * (size_t)used > in_size) return HOH_E_CORRUPT;
+    std::vector<uint16_t> comb(used);
+    for (int i = 0; i < used; i++, p += 2) comb[i] = (uint16_t)((in[p] << 8) | in[p + 1]);
+    std::vector<uint16_t> sym;
+    if ((r = stream(sym))) return r;
+    if (n != map.size()) return HOH_E_CORRUPT;
+    for (size_t i = 0; i < n; i++) {
+      if (sym[i] >= used) return HOH_E_CORRUPT;
+      map[i] = comb[sym[i]];
+    }
+  }
+  if ((r = stream(res))) return r;
+  return hoh_unpredict_all(c, res.data(), n, backref, w, h, depth, xt, yt, map.data(), out);
 }
 
 }  // extern "C"

@@ -327,6 +327,141 @@ __global__ __launch_bounds__(NT) void k_search(EncodeJob j) {
   }
 }
 
+// ---------------------------------------------------------------- plane-level entry points
+
+// channelpredict_section (prediction.hpp:46-151) of one cell, one thread: the cell-local top row
+// and best-predictor state live in the caller's scratch (the cell may be a whole plane)
+__global__ void k_section_one(const uint16_t* D, int w, int h, int depth, int xt, int yt, int cx, int cy,
+                              uint32_t mask, uint16_t* out, uint64_t* count, uint16_t* top, uint8_t* bp) {
+  if (threadIdx.x || blockIdx.x) return;
+  const int c = 1 << depth, half = c >> 1;
+  const int tw = (w + xt - 1) / xt, th = (h + yt - 1) / yt;
+  const int x0 = cx * tw, y0 = cy * th;
+  for (int i = 0; i < tw; i++) {
+    bp[i] = 4;
+    top[i] = cy ? D[(long)y0 * w + x0 + i - w] : (uint16_t)half;
+  }
+  uint64_t k = 0;
+  for (int ym = 0; ym < th && y0 + ym < h; ym++) {
+    uint32_t L, TL;
+    if (cx) {
+      L = D[(long)(y0 + ym) * w + x0 - 1];
+      TL = (ym || cy) ? D[(long)(y0 + ym - 1) * w + x0 - 1] : (uint32_t)half;
+    } else {
+      L = TL = half;
+    }
+    for (int xm = 0; xm < tw && x0 + xm < w; xm++) {
+      const uint32_t v = D[(long)(y0 + ym) * w + x0 + xm];
+      const uint32_t T = top[xm], TR = top[xm + 1 == tw ? 0 : xm + 1];
+      Preds p;
+      preds16(L, T, TL, TR, false, p);
+      const uint32_t pr = midp(pick(p, bp[xm]), pick(p, bp[xm == 0 ? tw - 1 : xm - 1]));
+      out[k++] = (uint16_t)(((int)v - (int)pr + half + c) % c);
+      TL = T;
+      top[xm] = (uint16_t)v;
+      L = v;
+      bp[xm] = (uint8_t)best_pred(v, p, mask, c);
+    }
+  }
+  *count = k;
+}
+
+// channelpredict_all (prediction.hpp:153-229), one thread per pixel
+__global__ __launch_bounds__(NT) void k_all_plane(const uint16_t* D, int w, int h, int depth, int xt, int yt,
+                                                  const uint16_t* map, uint16_t* out) {
+  const int c = 1 << depth;
+  const AllCtx a{D, w, h, (w + xt - 1) / xt, (h + yt - 1) / yt, xt, c, c >> 1, map};
+  const uint64_t n = (uint64_t)w * h;
+  for (uint64_t q = (uint64_t)blockIdx.x * NT + threadIdx.x; q < n; q += (uint64_t)gridDim.x * NT) {
+    const int y = (int)(q / (uint64_t)w), x = (int)(q - (uint64_t)y * w);
+    out[q] = (uint16_t)resid_all(a, x, y);
+  }
+}
+
+// unpredict_all (unprediction.hpp:6-91) with any predictor map: the exact inverse of
+// channelpredict_all including LZ copies (LEMPEL_BACKREF).  Row y's first pixel needs the best
+// predictor of row y-1's last pixel, so the recurrence is serial: one thread per plane.
+__global__ void k_unpredict_all(const uint16_t* res, uint64_t nres, const uint16_t* backref, int w, int h,
+                                int depth, int xt, int yt, const uint16_t* map, uint16_t* out,
+                                uint16_t* top, uint8_t* bp, uint32_t* err) {
+  if (threadIdx.x || blockIdx.x) return;
+  const int c = 1 << depth, half = c >> 1;
+  const int tw = (w + xt - 1) / xt, th = (h + yt - 1) / yt;
+  for (int i = 0; i < w; i++) { bp[i] = 4; top[i] = (uint16_t)half; }
+  uint64_t k = 0;
+  for (int y = 0; y < h; y++) {
+    uint32_t L = half, TL = half;
+    for (int x = 0; x < w; x++) {
+      const uint64_t loc = (uint64_t)y * w + x;
+      const uint32_t T = top[x], TR = top[x + 1 == w ? 0 : x + 1];
+      Preds p;
+      preds16(L, T, TL, TR, true, p);
+      uint32_t v;
+      if (backref && backref[loc]) {
+        if (backref[loc] > loc) { *err = 1; return; }
+        v = out[loc - backref[loc]];
+      } else {
+        if (k >= nres) { *err = 1; return; }
+        const uint32_t pr = midp(pick(p, bp[x]), pick(p, bp[x == 0 ? w - 1 : x - 1]));
+        v = (uint32_t)((res[k++] - c - half + pr) & 0xffffu) % (uint32_t)c;   // :67-68 in uint16
+      }
+      out[loc] = (uint16_t)v;
+      TL = T;
+      top[x] = (uint16_t)v;
+      L = v;
+      bp[x] = y + 1 < h ? (uint8_t)best_pred(v, p, map[((y + 1) / th) * xt + x / tw], c) : (uint8_t)0;
+    }
+  }
+  *err = 0;
+}
+
+// grid search of layer_encode.hpp:176-203 on a whole plane: costs per (cell, mask) ...
+__global__ __launch_bounds__(NT) void k_search_costs(const uint16_t* D, int w, int h, int depth, int xt, int yt,
+                                                     int npred, const double* ent, double* cost) {
+  __shared__ uint16_t top[NT][40];
+  __shared__ uint8_t bp[NT][40];
+  const int k = blockIdx.x * NT + threadIdx.x;
+  if (k >= xt * yt * npred) return;
+  const int cell = k / npred, m = k % npred;
+  cost[cell * 14 + m] = cell_cost(D, w, h, depth, xt, yt, cell % xt, cell / xt, kMasks[m], ent,
+                                  top[threadIdx.x], bp[threadIdx.x]);
+}
+
+// ... and the first mask of least cost per cell (strict <, :196-200)
+__global__ __launch_bounds__(NT) void k_search_pick(int ncell, int npred, const double* cost, uint16_t* plist,
+                                                    uint8_t* pidx) {
+  const int cell = blockIdx.x * NT + threadIdx.x;
+  if (cell >= ncell) return;
+  double best = 99999999999.0;
+  int bi = 0;
+  for (int m = 0; m < npred; m++) if (cost[cell * 14 + m] < best) { best = cost[cell * 14 + m]; bi = m; }
+  plist[cell] = kMasks[bi];
+  pidx[cell] = (uint8_t)bi;
+}
+
+void launch_section_one(const uint16_t* D, int w, int h, int depth, int xt, int yt, int cx, int cy, uint32_t mask,
+                        uint16_t* out, uint64_t* count, uint16_t* top, uint8_t* bp, hipStream_t s) {
+  hipLaunchKernelGGL(k_section_one, dim3(1), dim3(64), 0, s, D, w, h, depth, xt, yt, cx, cy, mask, out, count, top, bp);
+}
+void launch_all_plane(const uint16_t* D, int w, int h, int depth, int xt, int yt, const uint16_t* map, uint16_t* out,
+                      hipStream_t s) {
+  const uint64_t n = (uint64_t)w * h;
+  const int blocks = (int)((n + NT - 1) / NT < 4096 ? (n + NT - 1) / NT : 4096);
+  hipLaunchKernelGGL(k_all_plane, dim3(blocks > 0 ? blocks : 1), dim3(NT), 0, s, D, w, h, depth, xt, yt, map, out);
+}
+void launch_unpredict_all(const uint16_t* res, uint64_t nres, const uint16_t* backref, int w, int h, int depth,
+                          int xt, int yt, const uint16_t* map, uint16_t* out, uint16_t* top, uint8_t* bp,
+                          uint32_t* err, hipStream_t s) {
+  hipLaunchKernelGGL(k_unpredict_all, dim3(1), dim3(64), 0, s, res, nres, backref, w, h, depth, xt, yt, map, out,
+                     top, bp, err);
+}
+void launch_search_plane(const uint16_t* D, int w, int h, int depth, int xt, int yt, int npred, const double* ent,
+                         double* cost, uint16_t* plist, uint8_t* pidx, hipStream_t s) {
+  const int n = xt * yt * npred;
+  hipLaunchKernelGGL(k_search_costs, dim3((n + NT - 1) / NT), dim3(NT), 0, s, D, w, h, depth, xt, yt, npred, ent, cost);
+  hipLaunchKernelGGL(k_search_pick, dim3((xt * yt + NT - 1) / NT), dim3(NT), 0, s, xt * yt, npred, cost, plist, pidx);
+}
+
 // ---------------------------------------------------------------- LZ at seek distance 10..14
 
 __device__ __forceinline__ uint32_t tile_px(const EncodeJob& j, const TileInfo& ti, uint32_t q) {
@@ -823,4 +958,15 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, void (*mark)(void*, const
   hipLaunchKernelGGL(k_tilebytes_s, dim3((j.ntiles + 63) / 64), dim3(64), 0, s, j);
   launch_streambytes(j, S, s);
   mark(mc, "assemble");
+}
+
+// histogram of a u16 plane (entropy estimate of layer_encode.hpp:133-147)
+__global__ __launch_bounds__(NT) void k_hist16(const uint16_t* in, uint64_t n, uint32_t* hist) {
+  for (uint64_t q = (uint64_t)blockIdx.x * NT + threadIdx.x; q < n; q += (uint64_t)gridDim.x * NT)
+    atomicAdd(&hist[in[q]], 1u);
+}
+
+void launch_hist16(const uint16_t* in, uint64_t n, uint32_t* hist, hipStream_t s) {
+  const uint64_t b = (n + NT - 1) / NT;
+  hipLaunchKernelGGL(k_hist16, dim3(b < 1024 ? (b ? (unsigned)b : 1u) : 1024u), dim3(NT), 0, s, in, n, hist);
 }

@@ -87,6 +87,10 @@ def lib():
             ("hoh_layer_decode", [vp, vp, sz, sz, C.c_int, C.c_int, C.c_int, vp, vp]),
             ("hoh_predict_fastpath", [vp, vp, C.c_int, C.c_int, C.c_int, vp]),
             ("hoh_unpredict_fastpath", [vp, vp, sz, vp, C.c_int, C.c_int, C.c_int, vp]),
+            ("hoh_predict_section", [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                     C.c_uint16, vp, szp]),
+            ("hoh_predict_all", [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp]),
+            ("hoh_unpredict_all", [vp, vp, sz, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp]),
             ("hoh_subtract_green", [vp, vp, sz, vp, vp, vp]),
             ("hoh_add_green", [vp, vp, vp, vp, sz, vp]),
         ):
@@ -316,17 +320,64 @@ def decode_entropy(data, byte_pointer=0, ctx=None):
     return out[:n.value], bp.value
 
 
-def layer_encode(plane, depth, nuke=None, ctx=None):
+def layer_encode(plane, depth, nuke=None, ctx=None, speed=0):
+    """layer_encode (layer_encode.hpp:11-412) at cruncher_mode `speed` -> layer bytes."""
     ctx = ctx or default_ctx()
     p = np.ascontiguousarray(plane, dtype=np.uint16)
     h, w = p.shape
     nk = None if nuke is None else np.ascontiguousarray(nuke, dtype=np.uint8)
-    cap = lib().hoh_entropy_bound(p.size, 1 << depth, 15) + 16
+    cap = lib().hoh_entropy_bound(p.size, 1 << depth, 31) + 4096
     out = np.empty(cap, np.uint8)
     n = C.c_size_t(0)
-    check(lib().hoh_layer_encode(ctx.h, _p(p), p.size, w, h, depth, 0, None if nk is None else _p(nk),
+    check(lib().hoh_layer_encode(ctx.h, _p(p), p.size, w, h, depth, speed, None if nk is None else _p(nk),
                                  _p(out), cap, C.byref(n)), "hoh_layer_encode")
     return out[:n.value].tobytes()
+
+
+def layer_decode(data, w, h, depth, backref=None, pos=0, ctx=None):
+    """decode_layer (layer_decode.hpp:128-278) -> (h, w) u16 plane (full depth)."""
+    ctx = ctx or default_ctx()
+    b = np.frombuffer(bytes(data), dtype=np.uint8).copy()
+    br = None if backref is None else np.ascontiguousarray(backref, dtype=np.uint16)
+    out = np.empty((h, w), np.uint16)
+    check(lib().hoh_layer_decode(ctx.h, _p(b), b.size, pos, w, h, depth, None if br is None else _p(br), _p(out)),
+          "hoh_layer_decode")
+    return out
+
+
+def predict_section(plane, depth, xt, yt, cx, cy, mask, ctx=None):
+    """channelpredict_section (prediction.hpp:46-151) -> residuals of one cell."""
+    ctx = ctx or default_ctx()
+    p = np.ascontiguousarray(plane, dtype=np.uint16)
+    h, w = p.shape
+    out = np.empty(p.size + 64, np.uint16)
+    k = C.c_size_t(0)
+    check(lib().hoh_predict_section(ctx.h, _p(p), w, h, depth, xt, yt, cx, cy, mask, _p(out), C.byref(k)),
+          "hoh_predict_section")
+    return out[:k.value].copy()
+
+
+def predict_all(plane, depth, xt, yt, tile_map, ctx=None):
+    """channelpredict_all (prediction.hpp:153-229) -> residual plane (flat)."""
+    ctx = ctx or default_ctx()
+    p = np.ascontiguousarray(plane, dtype=np.uint16)
+    tm = np.ascontiguousarray(tile_map, dtype=np.uint16)
+    h, w = p.shape
+    out = np.empty(p.size, np.uint16)
+    check(lib().hoh_predict_all(ctx.h, _p(p), w, h, depth, xt, yt, _p(tm), _p(out)), "hoh_predict_all")
+    return out
+
+
+def unpredict_all(res, w, h, depth, xt, yt, tile_map, backref=None, ctx=None):
+    """unpredict_all (unprediction.hpp:6-91) for any predictor map -> (h, w) plane."""
+    ctx = ctx or default_ctx()
+    r = np.ascontiguousarray(res, dtype=np.uint16)
+    tm = np.ascontiguousarray(tile_map, dtype=np.uint16)
+    br = None if backref is None else np.ascontiguousarray(backref, dtype=np.uint16)
+    out = np.empty((h, w), np.uint16)
+    check(lib().hoh_unpredict_all(ctx.h, _p(r), r.size, None if br is None else _p(br), w, h, depth, xt, yt, _p(tm),
+                                  _p(out)), "hoh_unpredict_all")
+    return out
 
 
 def channelpredict_fastpath(plane, depth, ctx=None):

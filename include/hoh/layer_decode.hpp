@@ -1,7 +1,7 @@
 // Drop-in for decode_layer (layer_decode.hpp:128-136): returns a new[]'d width*height plane as
 // uint8_t like the reference (9-bit planes are truncated to 8 bits there too; the caller's
-// inverse subtract-green works modulo 256).  MED is inverted on every row (SURVEY Q9 fixed).
-// Returns nullptr on error.
+// inverse subtract-green works modulo 256).  Predictor-map layers are inverted by
+// unpredict_all; the -s0 MED layer with MED on every row (SURVEY Q9 fixed).  nullptr on error.
 #pragma once
 #include <cstddef>
 #include <cstdint>

@@ -143,12 +143,14 @@ int hoh_encode_entropy_batch(hoh_ctx* ctx, const uint16_t* d_syms, const uint64_
 /* ---- plane level ------------------------------------------------------------------------ */
 
 /* Replaces layer_encode(uint16_t*, size_t, int, int, int, size_t, uint8_t*, uint8_t*)
- * (layer_encode.hpp:11-20) for cruncher_mode 0.  nuke may be NULL (no LZ). */
+ * (layer_encode.hpp:11-20), cruncher_mode 0..4 (1..4: grid predictor search and prob_bits ladder,
+ * with the reference's stale-prefix output).  nuke may be NULL (no LZ). */
 int hoh_layer_encode(hoh_ctx* ctx, const uint16_t* data, size_t size, int width, int height,
                      int depth, size_t cruncher_mode, const uint8_t* nuke, uint8_t* out,
                      size_t cap, size_t* written);
 /* Replaces decode_layer (layer_decode.hpp:128-136), returning the full-depth plane (u16: the
- * reference truncates 9-bit planes to u8).  backref may be NULL. */
+ * reference truncates 9-bit planes to u8).  Predictor-map layers use unpredict_all;
+ * the -s0 MED layer uses MED on every row (Q9 fixed).  backref may be NULL. */
 int hoh_layer_decode(hoh_ctx* ctx, const uint8_t* in, size_t in_size, size_t byte_pointer,
                      int width, int height, int depth, const uint16_t* backref, uint16_t* out);
 /* Replaces channelpredict_fastpath (prediction.hpp:6-13; reached via channelpredict_section
@@ -160,6 +162,19 @@ int hoh_predict_fastpath(hoh_ctx* ctx, const uint16_t* data, int width, int heig
  * NULL. */
 int hoh_unpredict_fastpath(hoh_ctx* ctx, const uint16_t* res, size_t nres, const uint16_t* backref,
                            int width, int height, int depth, uint16_t* out);
+/* Replaces channelpredict_section (prediction.hpp:46-151): residuals of cell (cx, cy) of an
+ * xt x yt grid with one predictor mask, in the cell's raster order; *count = residuals written
+ * (out must hold the cell's pixel count). */
+int hoh_predict_section(hoh_ctx* ctx, const uint16_t* data, int width, int height, int depth, int x_tiles,
+                        int y_tiles, int x, int y, uint16_t predictor, uint16_t* out, size_t* count);
+/* Replaces channelpredict_all (prediction.hpp:153-229): whole plane, one mask per grid cell. */
+int hoh_predict_all(hoh_ctx* ctx, const uint16_t* data, int width, int height, int depth, int x_tiles,
+                    int y_tiles, const uint16_t* tile_map, uint16_t* out);
+/* Replaces unpredict_all (unprediction.hpp:6-91) for any predictor map: the exact inverse of
+ * channelpredict_all with LZ copies (backref may be NULL).  A 1x1 {0x0010} map is the -s0 layer
+ * and is inverted with MED on every row (SURVEY Q9 fixed), as hoh_unpredict_fastpath. */
+int hoh_unpredict_all(hoh_ctx* ctx, const uint16_t* res, size_t nres, const uint16_t* backref, int width,
+                      int height, int depth, int x_tiles, int y_tiles, const uint16_t* tile_map, uint16_t* out);
 /* Replaces subtract_green (channel.hpp:73-79) and provides its inverse. */
 int hoh_subtract_green(hoh_ctx* ctx, const uint8_t* rgb, size_t npix, uint16_t* G, uint16_t* R, uint16_t* B);
 int hoh_add_green(hoh_ctx* ctx, const uint16_t* G, const uint16_t* R, const uint16_t* B, size_t npix, uint8_t* rgb);

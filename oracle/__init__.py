@@ -80,6 +80,8 @@ def lib():
         L.or_predict_section.argtypes = [u16p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                          C.c_uint16, u16p]
         L.or_predict_all.argtypes = [u16p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, u16p, u16p]
+        L.or_unpredict_all.restype = C.c_long
+        L.or_unpredict_all.argtypes = [u16p, C.c_size_t, u16p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, u16p, u16p]
         L.or_choh_bound.restype = C.c_size_t
         L.or_choh_bound.argtypes = [C.c_int, C.c_int]
         L.or_dhoh.restype = C.c_long
@@ -109,6 +111,7 @@ def ref():
         R.ref_channelpredict_section.restype = C.c_size_t
         R.ref_channelpredict_section.argtypes = [u16p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                                  C.c_int, C.c_uint16, u16p]
+        R.ref_unpredict_map.argtypes = [u16p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, u16p, u16p, u16p]
         R.ref_channelpredict_all.argtypes = [u16p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, u16p, u16p]
         R.ref_subtract_green.argtypes = [u8p, C.c_size_t, u16p, u16p, u16p]
         R.ref_count_colours.restype = C.c_int
@@ -237,6 +240,18 @@ def predict_all(plane, depth, xt, yt, tile_map):
     h, w = plane.shape
     out = np.empty(w * h, np.uint16)
     lib().or_predict_all(_p(plane, u16p), w, h, depth, xt, yt, _p(tm, u16p), _p(out, u16p))
+    return out
+
+
+def unpredict_all(res, w, h, depth, xt, yt, tile_map, backref=None):
+    r = np.ascontiguousarray(res, dtype=np.uint16)
+    tm = np.ascontiguousarray(tile_map, dtype=np.uint16)
+    br = None if backref is None else np.ascontiguousarray(backref, dtype=np.uint16)
+    out = np.empty((h, w), np.uint16)
+    k = lib().or_unpredict_all(_p(r, u16p), r.size, None if br is None else _p(br, u16p), w, h, depth, xt, yt,
+                               _p(tm, u16p), _p(out, u16p))
+    if k < 0:
+        raise OracleError(k)
     return out
 
 

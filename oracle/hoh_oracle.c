@@ -537,6 +537,43 @@ void or_predict_all(const uint16_t* d, int w, int h, int depth, int xt, int yt, 
   free(top);
 }
 
+/* unprediction.hpp:6-91 (unpredict_all) for any predictor map: the inverse of or_predict_all,
+ * LZ copies from backref (may be NULL).  Returns residuals consumed or OR_E_CORRUPT. */
+long or_unpredict_all(const uint16_t* res, size_t nres, const uint16_t* backref, int w, int h, int depth, int xt,
+                      int yt, const uint16_t* map, uint16_t* o) {
+  int c = 1 << depth, half = c / 2;
+  int tw = (w + xt - 1) / xt, th = (h + yt - 1) / yt;
+  int* bp = (int*)malloc(sizeof(int) * w);
+  uint16_t* top = (uint16_t*)malloc(2 * (size_t)w);
+  for (int i = 0; i < w; i++) { bp[i] = 4; top[i] = (uint16_t)half; }
+  size_t k = 0;
+  long ret = 0;
+  for (int y = 0; y < h && ret == 0; y++) {
+    uint16_t L = (uint16_t)half, TL = (uint16_t)half;
+    for (int x = 0; x < w; x++) {
+      size_t loc = (size_t)y * w + x;
+      uint16_t T = top[x], TR = top[(x + w + 1) % w], p[16];
+      preds16(L, T, TL, TR, 1, p);
+      if (backref && backref[loc]) {
+        if (backref[loc] > loc) { ret = OR_E_CORRUPT; break; }
+        o[loc] = o[loc - backref[loc]];
+      } else {
+        if (k >= nres) { ret = OR_E_CORRUPT; break; }
+        uint16_t v = (uint16_t)(res[k++] - c - half + midp16(p[bp[x]], p[bp[(x + w - 1) % w]]));
+        o[loc] = (uint16_t)(v % c);
+      }
+      TL = top[x];
+      top[x] = o[loc];
+      L = o[loc];
+      bp[x] = 0;
+      if (y + 1 < h) bp[x] = best_pred(o[loc], p, map[((y + 1) / th) * xt + x / tw], c);
+    }
+  }
+  free(bp);
+  free(top);
+  return ret ? ret : (long)k;
+}
+
 /* ------------------------------------------------------------------ colour */
 
 void or_subtract_green(const uint8_t* s, size_t npix, uint16_t* G, uint16_t* R, uint16_t* B) {

@@ -78,6 +78,9 @@ size_t or_predict_section(const uint16_t* data, int w, int h, int depth, int xt,
                           uint16_t mask, uint16_t* out);
 void or_predict_all(const uint16_t* data, int w, int h, int depth, int xt, int yt, const uint16_t* map,
                     uint16_t* out);
+long or_unpredict_all(const uint16_t* res, size_t nres, const uint16_t* backref, int w, int h, int depth, int xt,
+                      int yt, const uint16_t* map, uint16_t* out);
+
 /* layer_encode.hpp:11-412 / choh.cpp:104-383 / choh.cpp:394-527 at any cruncher_mode (-sN) */
 long or_layer_encode(const uint16_t* data, size_t n, int w, int h, int depth, int cruncher,
                      const uint8_t* nuke, uint8_t* out);

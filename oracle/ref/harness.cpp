@@ -98,6 +98,14 @@ void ref_channelpredict_all(const uint16_t* data, int w, int h, int depth, int x
   delete[] r;
 }
 
+void ref_unpredict_map(const uint16_t* res, int w, int h, int depth, int xt, int yt, const uint16_t* tile_map,
+                       const uint16_t* backref, uint16_t* out) {
+  uint16_t* r = unpredict_all((uint16_t*)res, (size_t)w * h, w, h, depth, xt, yt, (uint16_t*)tile_map,
+                              (uint16_t*)backref);                // unprediction.hpp:6
+  memcpy(out, r, (size_t)w * h * 2);
+  delete[] r;
+}
+
 void ref_subtract_green(const uint8_t* rgb, size_t npix, uint16_t* G, uint16_t* R, uint16_t* B) {
   subtract_green((uint8_t*)rgb, npix * 3, G, R, B);                // channel.hpp:73
 }

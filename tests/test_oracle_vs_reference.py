@@ -186,3 +186,32 @@ def test_choh_speeds_vs_reference_binary(tmp_path):
         mine, printed = O.choh(img, sp)
         assert (tmp_path / "a.hoh").read_bytes() == mine, (W, H, sp)
         assert int(r.stdout.split()[-1]) == printed
+
+
+def test_unpredict_all_maps_vs_reference():
+    """unpredict_all (unprediction.hpp:6-91) with predictor maps and LZ back references; and the
+    round trip channelpredict_all -> unpredict_all"""
+    rs = np.random.RandomState(8)
+    R = O.ref()
+    masks = [1, 2, 0x20, 0x10, 0xffbf, 3, 0xfffd, 0xffff]
+    for it in range(60):
+        w, h, depth = int(rs.randint(1, 90)), int(rs.randint(1, 90)), int(rs.choice([8, 9]))
+        xt, yt = int(rs.randint(1, 4)), int(rs.randint(1, 4))
+        tm = rs.choice(masks, xt * yt).astype(np.uint16)
+        d = _smooth(rs, h, w, depth, int(rs.choice([0, 3, 20])))
+        res = O.predict_all(d, depth, xt, yt, tm)
+        assert np.array_equal(O.unpredict_all(res, w, h, depth, xt, yt, tm), d), it
+        br = np.zeros(w * h, np.uint16)
+        if it % 2:
+            for _ in range(5):
+                i, L, b = int(rs.randint(0, w * h)), int(rs.randint(1, 20)), int(rs.randint(1, 60))
+                for k in range(i, min(w * h, i + L)):
+                    if k >= b:
+                        br[k] = b
+        r2 = rs.randint(0, 1 << depth, w * h).astype(np.uint16)
+        nres = int((br == 0).sum())
+        out = np.empty(w * h, np.uint16)
+        R.ref_unpredict_map(r2.ctypes.data_as(O.u16p), w, h, depth, xt, yt, tm.ctypes.data_as(O.u16p),
+                            br.ctypes.data_as(O.u16p), out.ctypes.data_as(O.u16p))
+        mine = O.unpredict_all(r2[:nres], w, h, depth, xt, yt, tm, br)
+        assert np.array_equal(mine.reshape(-1), out), it
