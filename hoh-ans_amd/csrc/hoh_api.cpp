@@ -409,13 +409,20 @@ int hoh_encode_tiles(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int t0, int
 
 int hoh_encode_tiles_ix(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int t0, int ntiles, uint8_t* d_out,
                         size_t cap, uint32_t* d_tile_sizes, size_t* out_size, hoh_index* idx, void* stream) {
-  if (!c || !d_rgb || !d_out || !out_size || W <= 0 || H <= 0) return HOH_E_ARG;
+  return hoh_encode_tiles_speed(c, d_rgb, W, H, 0, t0, ntiles, d_out, cap, d_tile_sizes, out_size, idx, stream);
+}
+
+int hoh_encode_tiles_speed(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int speed, int t0, int ntiles,
+                           uint8_t* d_out, size_t cap, uint32_t* d_tile_sizes, size_t* out_size, hoh_index* idx,
+                           void* stream) {
+  if (!c || !d_rgb || !d_out || !out_size || W <= 0 || H <= 0 || speed < 0 || speed > 4) return HOH_E_ARG;
+  if (speed && idx) idx->nstreams = 0;
   (void)hipSetDevice(c->device);
   int xt, yt, tw, th;
   if (!hoh_tiling(W, H, &xt, &yt, &tw, &th)) return HOH_E_ARG;
   uint64_t total = 0;
-  int r = encode_tiles_impl(c, d_rgb, W, H, t0, ntiles, d_out, cap, 0, 0, d_tile_sizes, &total, idx,
-                            pick(c, stream));
+  int r = encode_tiles_impl(c, d_rgb, W, H, t0, ntiles, d_out, cap, 0, 0, d_tile_sizes, &total, speed ? nullptr : idx,
+                            pick(c, stream), speed);
   *out_size = (size_t)total;
   return r;
 }

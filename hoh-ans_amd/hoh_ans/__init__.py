@@ -76,6 +76,8 @@ def lib():
         L.hoh_synth_rgb.argtypes = [vp, vp, C.c_int, C.c_int, C.c_uint64, C.c_int, vp]
         L.hoh_synth_rgb_rows.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int, vp]
         L.hoh_encode_tiles_ix.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, sz, vp, szp, vp, vp]
+        L.hoh_encode_tiles_speed.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, sz, vp, szp,
+                                             vp, vp]
         L.hoh_decode_tiles.argtypes = [vp, vp, sz, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp]
         for name, args in (
             ("hoh_decode_image", [vp, vp, sz, vp, sz, ip, ip, vp]),
@@ -223,7 +225,7 @@ def decode_image(hoh_dev, size, out_dev=None, ctx=None, index=None):
     return out_dev, w.value, h.value
 
 
-def encode_tiles(rgb_dev, W, H, t0, ntiles, out_dev, sizes_dev, ctx=None, index=None, row0=0):
+def encode_tiles(rgb_dev, W, H, t0, ntiles, out_dev, sizes_dev, ctx=None, index=None, row0=0, speed=0):
     """Encode tiles [t0, t0+ntiles) of a W x H image into a blob (concatenated tile byte strings).
     rgb_dev holds image rows from row0 on (a shard); only the named tiles' pixels are read.
     Returns the blob size; sizes_dev (uint32, device) receives each tile's size."""
@@ -231,9 +233,9 @@ def encode_tiles(rgb_dev, W, H, t0, ntiles, out_dev, sizes_dev, ctx=None, index=
     ctx = ctx or default_ctx()
     n = C.c_size_t(0)
     base = rgb_dev.data_ptr() - row0 * W * 3
-    r = lib().hoh_encode_tiles_ix(ctx.h, vp(base), W, H, t0, ntiles, vp(out_dev.data_ptr()),
-                                  out_dev.numel(), vp(sizes_dev.data_ptr()), C.byref(n),
-                                  index.h if index is not None else None, _stream_ptr(torch))
+    r = lib().hoh_encode_tiles_speed(ctx.h, vp(base), W, H, speed, t0, ntiles, vp(out_dev.data_ptr()),
+                                     out_dev.numel(), vp(sizes_dev.data_ptr()), C.byref(n),
+                                     index.h if index is not None else None, _stream_ptr(torch))
     check(r, "hoh_encode_tiles")
     return n.value
 

@@ -104,6 +104,10 @@ int hoh_encode_tiles(hoh_ctx* ctx, const uint8_t* d_rgb, int W, int H, int t0, i
 int hoh_encode_tiles_ix(hoh_ctx* ctx, const uint8_t* d_rgb, int W, int H, int t0, int ntiles,
                         uint8_t* d_out, size_t cap, uint32_t* d_tile_sizes, size_t* out_size,
                         hoh_index* idx, void* stream);
+/* The same at any speed (-s0..-s4; -s>=1 tiles get no side index). */
+int hoh_encode_tiles_speed(hoh_ctx* ctx, const uint8_t* d_rgb, int W, int H, int speed, int t0, int ntiles,
+                           uint8_t* d_out, size_t cap, uint32_t* d_tile_sizes, size_t* out_size,
+                           hoh_index* idx, void* stream);
 /* Decodes tiles [t0, t0+ntiles) from d_blob (their byte strings concatenated, sizes in
  * h_tile_sizes) into the W x H image at d_rgb (only those tiles' pixels are written; d_rgb is
  * the base of the whole image).  idx may be the index hoh_encode_tiles_ix recorded. */

@@ -61,3 +61,29 @@ def test_synth_rows_match_numpy():
     for y0, y1 in [(0, 300), (17, 200), (299, 300)]:
         d = hoh_ans.synth_rgb_dev(W, y1 - y0, 9, 3, row0=y0).cpu().numpy().reshape(y1 - y0, W, 3)
         assert np.array_equal(d, full[y0:y1])
+
+
+@pytest.mark.parametrize("speed", [1, 3])
+def test_shards_speed_assemble_to_file(speed):
+    """config 5 on N GPUs: -s>=1 tiles sharded by bands of tile rows, prefix + concatenation is
+    the single-call file (and the oracle's)"""
+    import torch
+    import hoh_ans
+    from hoh_ans import dist as hd
+    W, H, world, seed = 1024, 768, 3, 5
+    img = synth.synth_rgb(W, H, seed, 4)
+    L = hoh_ans.lib()
+    blobs, sizes = [], []
+    for r in range(world):
+        t0, nt, y0, y1 = hd.shard(W, H, r, world)
+        rgb = torch.from_numpy(img[y0:y1].reshape(-1).copy()).cuda()
+        out = torch.empty(L.hoh_encode_bound(W, y1 - y0), dtype=torch.uint8, device="cuda")
+        sz = torch.empty(nt, dtype=torch.int32, device="cuda")
+        n = hoh_ans.encode_tiles(rgb, W, H, t0, nt, out, sz, row0=y0, speed=speed)
+        ts = sz.cpu().numpy().astype(np.uint32)
+        assert int(ts.sum()) == n
+        blobs.append(out[:n].cpu().numpy().tobytes())
+        sizes.append(ts)
+    f = hoh_ans.file_prefix(W, H, np.concatenate(sizes)) + b"".join(blobs)
+    assert f == hoh_ans.choh(img, speed=speed)[0]
+    assert f == oracle.choh(img, speed)[0]
