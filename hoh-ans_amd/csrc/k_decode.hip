@@ -362,13 +362,8 @@ __device__ __forceinline__ uint32_t skew_pos(uint32_t x, uint32_t y, uint32_t w)
   return ((y >> 6) * (w + 63) + x + r) * 64 + r;
 }
 
-// skewed-layout width of stream sid (0: flat).  Only complete planes (n == w*h, i.e. no LZ
-// nukes) are skewed; the single-stream decoder has no tiles.
-__device__ __forceinline__ uint32_t skew_w(const DecJob& j, int sid, uint32_t n) {
-  if (!j.tiles || sid % SK_PER_TILE < 3 || (j.dbg & 1)) return 0;
-  const DecTile& t = j.tiles[sid / SK_PER_TILE];
-  return n == (uint32_t)(t.w * t.h) ? (uint32_t)t.w : 0u;
-}
+// Decoded planes are flat (raster order); OutCursor keeps the skewed variant for reference only.
+__device__ __forceinline__ uint32_t skew_w(const DecJob&, int, uint32_t) { return 0u; }
 
 struct OutCursor {
   uint16_t* out;
@@ -416,7 +411,8 @@ __device__ bool dec_run(const DecJob& j, const DecStream& d, const uint32_t* cum
 // exact slot -> symbol table (a byte per slot: the symbol's offset from the first symbol of its
 // 32-slot bucket, plus that first symbol per bucket) and the whole payload, so the per-symbol
 // chain is two LDS round trips and no global load; the symbol stores are never awaited.
-// Dynamic LDS: cum (514 u32) | bucket symbols (u16) | slot table (u8) | payload words | 4 rings.
+// Dynamic LDS: cum (514 u32) | bucket symbols (u16) | slot table (u8) | payload words.  Output is
+// the flat plane: each thread stores its segment 8 symbols (16 B) at a time.
 __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams, uint32_t wcap) {
   extern __shared__ __attribute__((aligned(16))) uint32_t dr_lds[];
   const int tid = threadIdx.x;
@@ -512,10 +508,6 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams, uint32_t
   const uint32_t nseg = (d.n + DSEG - 1) / DSEG;
   bool bad = false;
   const bool fast = staged && !wide;
-  // rows of HOH_SEG pixels: thread = row, wave = 64-row band, so the skewed layout's line
-  // (band, st) collects over 64 steps in an LDS ring and leaves as one coalesced 128-B store
-  const bool ringmode = fast && sw == DSEG;
-  uint16_t* ring = (uint16_t*)(pw + wcap) + (tid >> 6) * 4096;
   for (uint32_t sg0 = 0; sg0 < nseg; sg0 += DR_T) {
     const uint32_t sg = sg0 + tid;
     const bool act = sg < nseg;
@@ -529,25 +521,26 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams, uint32_t
       s1 = min(d.n, s0 + DSEG);
       if (sg + 1 < nseg) { const Checkpoint c2 = j.ck[xs.ckpt_off + sg + 1]; want = (uint64_t)c2.xl | ((uint64_t)c2.xh << 32); }
     }
-    if (ringmode) {
-      const uint32_t lane = tid & 63;
-      const uint32_t band = (sg0 >> 6) + (tid >> 6);
-      if (band * 64 >= nseg) continue;                      // whole wave past the last row
-      uint16_t* bo = out + (size_t)band * (DSEG + 63) * 64 + lane;
-      for (uint32_t xx = 0; xx < DSEG; xx++) {
-        if (act) {
+    if (fast && act && s1 - s0 == DSEG) {
+      // a whole segment: 8 symbols per 16-B store of the lane's own (flat) output range; the
+      // stores are never awaited, and nothing but the chain touches LDS
+      uint4* o4 = (uint4*)(out + s0);
+      for (uint32_t g = 0; g < DSEG / 8; g++) {
+        uint32_t pk[4];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
           const uint32_t nw = pw[min(wi, wcap - 1)];
           const uint32_t slot = (uint32_t)x & mask;
           const uint32_t sym = sy_s[slot >> bsh] + tb[slot];
           const uint32_t cc = cum_s[sym], f = cum_s[sym + 1] - cc;
-          ring[((xx + lane) & 63) * 64 + lane] = (uint16_t)sym;
+          if (u & 1) pk[u >> 1] |= sym << 16; else pk[u >> 1] = sym;
           x = (uint64_t)f * (x >> pb) + (slot - cc);       // Rans64DecAdvance
           if (x < (1ull << 31)) { x = (x << 32) | nw; wi++; }
         }
-        bo[xx * 64] = ring[(xx & 63) * 64 + lane];          // line xx is complete (lane 0 wrote last)
+        if (!(j.dbg & 32)) o4[g] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+        else if (pk[0] == 0xffffffffu) bad = true;           // keep the chain live (measurement)
       }
-      for (uint32_t st = DSEG; st < DSEG + 63; st++) bo[st * 64] = ring[(st & 63) * 64 + lane];
-      if (act && (x != want || wi > d.words)) bad = true;
+      if (x != want || wi > d.words) bad = true;
       continue;
     }
     if (!act) continue;
@@ -666,68 +659,113 @@ __device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
   return max(min(a, b), min(max(a, b), c));
 }
 
-#define UP_P 8   // residual prefetch group (steps)
+#define UP_P 8   // steps per residual group (one 16-B chunk pair per lane and plane)
+
+// LDS row pitch (bytes) of the output column ring: 128 columns of RGB, odd dword count
+#define ORING_PITCH 388
+
+// 16-bit elements off .. off+7 of the 16 in w[0..7] (off lane-constant, 0..7): a 4-way select
+// of the word pairs, then a funnel shift by a half word
+__device__ __forceinline__ void win8(const uint32_t* w, uint32_t off, uint32_t* o) {
+  const uint32_t q = off >> 1, sh = (off & 1) * 16;
+  uint32_t sel[5];
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    const uint32_t a0 = (q & 1) ? w[i + 1] : w[i];
+    const uint32_t a1 = (q & 1) ? w[i + 3] : w[i + 2];
+    sel[i] = (q & 2) ? a1 : a0;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) o[i] = __builtin_amdgcn_alignbit(sel[i + 1], sel[i], sh);
+}
 
 // Wavefront MED inverse (prediction.hpp:26-41 inverted on every row, Q9 fixed) of the three
 // planes of one tile + inverse subtract-green (channel.hpp:73-79), one wave per tile.
 // Lane r owns row 64b + r of band b and decodes x = st - r at step st; T and TL come from lane
 // r-1 through DPP (its values at steps st-1 and st-2), row -1 of a band from LDS.  The three
-// planes are independent chains interleaved in one instruction stream.
-// LDS row pitch (bytes) of the output staging band: whole dwords, odd dword count (bank spread)
-__host__ __device__ __forceinline__ uint32_t ostage_pitch(uint32_t tw) {
-  uint32_t dw = (tw * 3 + 3) / 4;
-  return (dw | 1u) * 4;
-}
-
+// planes are independent chains interleaved in one instruction stream.  Residual planes are
+// flat (raster order): every UP_P steps a lane loads the two aligned 16-B chunks holding its
+// next UP_P residuals per plane (issued one group ahead) and funnel-shifts them into place.
+// RGB goes to a 128-column LDS ring; each 64-column chunk leaves as coalesced row segments once
+// all 64 rows have passed it.
 __global__ __launch_bounds__(64) void k_dunpred_fast(DecJob j) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int t = blockIdx.x;
   const DecTile ti = j.tiles[t];
   if (ti.err || !unpred_fast(j, t, ti)) return;
-  const uint32_t opitch = ostage_pitch(j.tw);
-  uint8_t* ob = lds;                                   // [64][opitch] RGB bytes of the band
-  uint16_t* lastG = (uint16_t*)(lds + 64 * opitch);
+  uint8_t* ring = lds;                                        // [64][ORING_PITCH]
+  uint16_t* lastG = (uint16_t*)(lds + 64 * ORING_PITCH);
   uint16_t* lastR = lastG + j.tw;
   uint16_t* lastB = lastR + j.tw;
   const int lane = threadIdx.x;
   const int w = ti.w, h = ti.h, nst = w + 63;
-  const uint16_t* skG = j.dsym + (size_t)(t * 3) * j.plane_cap + lane;
-  const uint16_t* skR = skG + j.plane_cap;
-  const uint16_t* skB = skR + j.plane_cap;
+  const uint16_t* plG = j.dsym + (size_t)(t * 3) * j.plane_cap;
   const size_t pitch = (size_t)j.W * 3;
   uint8_t* obase = j.rgb + ((size_t)ti.y0 * j.W + ti.x0) * 3;
   const bool dw_ok = ((pitch | ((size_t)ti.x0 * 3) | (size_t)j.rgb) & 3) == 0;
+  uint8_t* orow = ring + (size_t)lane * ORING_PITCH;
   for (int r0 = 0; r0 < h; r0 += 64) {
     const int y = r0 + lane;
     const int last = min(63, h - r0 - 1);
     const bool rowok = y < h;
-    const size_t bo = (size_t)(r0 >> 6) * nst * 64;
-    // residuals of the next UP_P steps are loaded one group ahead into nG/nR/nB and landed at
-    // the group start (the asm operand pins the wait there, so the compiler never parks a
-    // pending load across the loop latch)
-    uint32_t nG[UP_P], nR[UP_P], nB[UP_P];
-#pragma unroll
-    for (int u = 0; u < UP_P; u++) { nG[u] = skG[bo + u * 64]; nR[u] = skR[bo + u * 64]; nB[u] = skB[bo + u * 64]; }
+    const long F = (long)min(y, h - 1) * w - lane;            // flat index of this lane at step 0
+    const uint32_t off = (uint32_t)(F & 7);
+    const long F0 = F - off;                                   // 16-B aligned
+    // flush chunk k (columns 64k .. 64k+63, all rows of the band) from the ring
+    auto flush = [&](int k) {
+      const int c0 = 64 * k, nc = min(64, w - c0), rows = last + 1;
+      const uint8_t* src0 = ring + (c0 & 127) * 3;
+      uint8_t* dst0 = obase + (size_t)r0 * pitch + (size_t)c0 * 3;
+      if (dw_ok && nc == 64) {
+        for (int e = lane; e < rows * 48; e += 64) {
+          const int rr = e / 48, d = e - rr * 48;
+          ((uint32_t*)(dst0 + (size_t)rr * pitch))[d] = ((const uint32_t*)(src0 + (size_t)rr * ORING_PITCH))[d];
+        }
+      } else {
+        const int nb = nc * 3;
+        for (int e = lane; e < rows * nb; e += 64) {
+          const int rr = e / nb, d = e - rr * nb;
+          dst0[(size_t)rr * pitch + d] = src0[(size_t)rr * ORING_PITCH + d];
+        }
+      }
+    };
+    auto chunk = [&](const uint16_t* pl, long f) -> uint4 {
+      return *(const uint4*)(pl + (f < 0 ? 0 : f));
+    };
+    uint4 nG0, nG1, nR0, nR1, nB0, nB1;
+    {
+      nG0 = chunk(plG, F0); nG1 = chunk(plG, F0 + 8);
+      nR0 = chunk(plG + j.plane_cap, F0); nR1 = chunk(plG + j.plane_cap, F0 + 8);
+      nB0 = chunk(plG + 2 * (size_t)j.plane_cap, F0); nB1 = chunk(plG + 2 * (size_t)j.plane_cap, F0 + 8);
+    }
     uint32_t cG = 0, cR = 0, cB = 0;      // this lane's value at the previous step (L)
     uint32_t pG = 128, pR = 256, pB = 256; // T of the previous step (TL)
-    uint8_t* orow = ob + (size_t)lane * opitch;
+    int flushed = 0;
     for (int s0 = 0; s0 < nst; s0 += UP_P) {
-      uint32_t qG[UP_P], qR[UP_P], qB[UP_P];
-#pragma unroll
-      for (int u = 0; u < UP_P; u++) {
-        asm volatile("" ::"v"(nG[u]), "v"(nR[u]), "v"(nB[u]));
-        qG[u] = nG[u]; qR[u] = nR[u]; qB[u] = nB[u];
+      // land this group's chunks (issued one group ahead), then issue the next group's
+      asm volatile("" ::"v"(nG0.x), "v"(nG0.y), "v"(nG0.z), "v"(nG0.w), "v"(nG1.x), "v"(nG1.y), "v"(nG1.z), "v"(nG1.w));
+      asm volatile("" ::"v"(nR0.x), "v"(nR0.y), "v"(nR0.z), "v"(nR0.w), "v"(nR1.x), "v"(nR1.y), "v"(nR1.z), "v"(nR1.w));
+      asm volatile("" ::"v"(nB0.x), "v"(nB0.y), "v"(nB0.z), "v"(nB0.w), "v"(nB1.x), "v"(nB1.y), "v"(nB1.z), "v"(nB1.w));
+      uint32_t qG[4], qR[4], qB[4];
+      {
+        const uint32_t wg[8] = {nG0.x, nG0.y, nG0.z, nG0.w, nG1.x, nG1.y, nG1.z, nG1.w};
+        const uint32_t wr[8] = {nR0.x, nR0.y, nR0.z, nR0.w, nR1.x, nR1.y, nR1.z, nR1.w};
+        const uint32_t wb[8] = {nB0.x, nB0.y, nB0.z, nB0.w, nB1.x, nB1.y, nB1.z, nB1.w};
+        win8(wg, off, qG); win8(wr, off, qR); win8(wb, off, qB);
       }
-#pragma unroll
-      for (int u = 0; u < UP_P; u++) {
-        const size_t nx = bo + (size_t)(s0 + UP_P + u) * 64;
-        nG[u] = skG[nx]; nR[u] = skR[nx]; nB[u] = skB[nx];
+      {
+        const long fn = F0 + s0 + UP_P;
+        nG0 = chunk(plG, fn); nG1 = chunk(plG, fn + 8);
+        nR0 = chunk(plG + j.plane_cap, fn); nR1 = chunk(plG + j.plane_cap, fn + 8);
+        nB0 = chunk(plG + 2 * (size_t)j.plane_cap, fn); nB1 = chunk(plG + 2 * (size_t)j.plane_cap, fn + 8);
       }
 #pragma unroll
       for (int u = 0; u < UP_P; u++) {
         const int st = s0 + u;
         const int x = st - lane;
-        const uint32_t rG = qG[u], rR = qR[u], rB = qB[u];
+        const uint32_t rG = (qG[u >> 1] >> ((u & 1) * 16)) & 0xffffu;
+        const uint32_t rR = (qR[u >> 1] >> ((u & 1) * 16)) & 0xffffu;
+        const uint32_t rB = (qB[u >> 1] >> ((u & 1) * 16)) & 0xffffu;
         uint32_t oG = 128, oR = 256, oB = 256;        // lane 0: row above the band
         if (r0 > 0 && lane == 0 && x < w) { oG = lastG[x]; oR = lastR[x]; oB = lastB[x]; }
         const uint32_t TG = wave_shr1(cG, oG), TR = wave_shr1(cR, oR), TB = wave_shr1(cB, oB);
@@ -740,30 +778,17 @@ __global__ __launch_bounds__(64) void k_dunpred_fast(DecJob j) {
         pG = TG; pR = TR; pB = TB;
         cG = vG; cR = vR; cB = vB;
         if (rowok && x >= 0 && x < w) {
-          uint8_t* o = orow + x * 3;
+          uint8_t* o = orow + (x & 127) * 3;
           o[0] = (uint8_t)(vR + vG); o[1] = (uint8_t)vG; o[2] = (uint8_t)(vB + vG);
           if (lane == last) { lastG[x] = (uint16_t)vG; lastR[x] = (uint16_t)vR; lastB[x] = (uint16_t)vB; }
         }
       }
+      // columns < s0 + UP_P - 63 are complete in every row: flush whole 64-column chunks before
+      // the ring slot is reused (column 64k + 128 arrives at step 64k + 128 at the earliest)
+      const int done = s0 + UP_P - 63;
+      while (64 * (flushed + 1) <= done && 64 * flushed < w) { flush(flushed); flushed++; }
     }
-    __syncthreads();
-    // coalesced flush of the band (rows r0 .. r0+last)
-    const int rows = last + 1, rb = w * 3;
-    if (dw_ok) {
-      const int dpr = rb >> 2;
-      for (int rr = 0; rr < rows; rr++) {
-        const uint32_t* src = (const uint32_t*)(ob + (size_t)rr * opitch);
-        uint32_t* dst = (uint32_t*)(obase + (size_t)(r0 + rr) * pitch);
-        for (int e = lane; e < dpr; e += 64) dst[e] = src[e];
-        for (int e = dpr * 4 + lane; e < rb; e += 64) ((uint8_t*)dst)[e] = ((const uint8_t*)src)[e];
-      }
-    } else {
-      for (int rr = 0; rr < rows; rr++) {
-        const uint8_t* src = ob + (size_t)rr * opitch;
-        uint8_t* dst = obase + (size_t)(r0 + rr) * pitch;
-        for (int e = lane; e < rb; e += 64) dst[e] = src[e];
-      }
-    }
+    while (64 * flushed < w) { flush(flushed); flushed++; }
     __syncthreads();
   }
 }
@@ -1040,8 +1065,8 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   j.npix_cap = (uint32_t)(((size_t)j.tw * j.th + 63) / 64 * 64);
   j.lz_cap = (uint32_t)((j.npix_cap / 4 + j.npix_cap / 255 + 16 + 7) / 8 * 8);
   {
-    const size_t skew = (size_t)((j.th + 63) / 64) * (j.tw + 63) * 64 + (size_t)2 * UP_P * 64;
-    j.plane_cap = (uint32_t)((std::max((size_t)j.npix_cap, skew) + 63) / 64 * 64);
+    // flat planes + slack for k_dunpred_fast's chunk reads one group past the end
+    j.plane_cap = (uint32_t)(((size_t)j.npix_cap + 4 * UP_P + 64 + 63) / 64 * 64);
   }
   const int S = j.ntiles * SK_PER_TILE;
   DecWork& w = ctx_dec(c);
@@ -1078,7 +1103,7 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   const uint32_t maxw = (uint32_t)(pin[0] >> 32);
   if (indexed) {
     // payload stage sized to the largest stream when it fits next to the tables (<= 128 KB)
-    const size_t fixed = (514 + 512 + 8192) * 4 + 4 * 4096 * 2;   // tables + 4 output rings
+    const size_t fixed = (514 + 512 + 8192) * 4;                      // cum + bucket symbols + slot table
     const uint32_t wcap = (uint32_t)std::min<size_t>(std::max<uint32_t>(maxw, 1), (150 * 1024 - fixed) / 4);
     hipLaunchKernelGGL(k_dmatch, dim3((S + 255) / 256), dim3(256), 0, s, j, S);
     hipLaunchKernelGGL(k_drans, dim3(S), dim3(DR_T), fixed + (size_t)wcap * 4, s, j, S, wcap);
@@ -1089,7 +1114,7 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   hipLaunchKernelGGL(k_dstored, dim3(S), dim3(256), 0, s, j, S);
   hipLaunchKernelGGL(k_dlz, dim3((j.ntiles + 63) / 64), dim3(64), 0, s, j);
   ctx_mark(c, s, "dlz", false);
-  hipLaunchKernelGGL(k_dunpred_fast, dim3(j.ntiles), dim3(64), (size_t)64 * ostage_pitch(j.tw) + (size_t)3 * j.tw * 2, s, j);
+  hipLaunchKernelGGL(k_dunpred_fast, dim3(j.ntiles), dim3(64), (size_t)64 * ORING_PITCH + (size_t)3 * j.tw * 2, s, j);
   j.lzband = (int)std::min<size_t>(64, (160 * 1024 - (size_t)j.tw * 4) / ((size_t)j.tw * 8));
   hipLaunchKernelGGL(k_dunpred_lz, dim3(j.ntiles), dim3(64), (size_t)(2 * j.lzband + 1) * j.tw * 4, s, j);
   hipLaunchKernelGGL(k_dunpred_serial, dim3(j.ntiles), dim3(192), 0, s, j);
