@@ -10,6 +10,8 @@
 #include <string.h>
 #include <stdlib.h>
 #include <vector>
+#include <algorithm>
+#include <stdio.h>
 #include <string>
 
 void launch_synth(uint8_t* rgb, int W, int H, int y0, uint64_t seed, int noise, hipStream_t s);
@@ -47,6 +49,7 @@ struct hoh_ctx {
   int device = 0;
   hipStream_t own = nullptr;
   Buf idx8, fpb, pinfo, lg;     // -s>=1 workspaces
+  Buf dbgb;                     // measurement stamps
   uint32_t lg_key[4] = {0, 0, 0, 0};
   uint64_t lg_off[4] = {0, 0, 0, 0};
   Buf sym, hist, candbits, matches, pal, streams, tiles, hdr, tab_fast, tab_gen, slabs, ckpt, misc, tsizes;
@@ -143,7 +146,7 @@ static void freebuf(Buf& b) { if (b.p) (void)hipFree(b.p); b.p = nullptr; b.n = 
 void hoh_ctx_destroy(hoh_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  Buf* all[] = {&c->idx8, &c->fpb, &c->pinfo, &c->lg, &c->sym, &c->hist, &c->candbits, &c->matches, &c->pal, &c->streams, &c->tiles, &c->hdr,
+  Buf* all[] = {&c->dbgb, &c->idx8, &c->fpb, &c->pinfo, &c->lg, &c->sym, &c->hist, &c->candbits, &c->matches, &c->pal, &c->streams, &c->tiles, &c->hdr,
                 &c->tab_fast, &c->tab_gen, &c->slabs, &c->ckpt, &c->misc, &c->tsizes};
   for (Buf* b : all) freebuf(*b);
   dec_free(c->dec);
@@ -372,14 +375,43 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
     if (hipGetLastError() != hipSuccess) return HOH_E_HIP;
     idx = nullptr;
   } else {
-  launch_lz(j, s);
-  launch_nuke(j, s);             prof.mark("lz");
-  launch_tables(j, (int)S, s);   prof.mark("tables");
-  launch_rans_fast(j, ntiles * 4, s, SidMap{3, SK_G}, ntiles * 3, SidMap{1, SK_I}); prof.mark("rans_enc_fast");
-  launch_rans_gen(j, (int)S, s); prof.mark("rans_enc_gen");
-  launch_finalize(j, (int)S, s); prof.mark("finalize");
-  launch_layout(j, s);           prof.mark("layout");
-  launch_assemble(j, (int)S, s); prof.mark("assemble");
+  // (HOH_ENC_DBG bits 16..19 stop after a stage: pipelined cost per stage, output invalid)
+  do {
+    if (j.dbg & 0x10000) break;
+    launch_lz(j, s);
+    launch_nuke(j, s);             prof.mark("lz");
+    if (j.dbg & 0x20000) break;
+    launch_tables(j, (int)S, s);   prof.mark("tables");
+    if (j.dbg & 0x40000) break;
+    if (j.dbg & 0x200000) {
+      if ((e = ensure(c->dbgb, (size_t)ntiles * 4 * 16))) return e;
+      j.dbgbuf = (uint64_t*)c->dbgb.p;
+      (void)hipMemsetAsync(j.dbgbuf, 0, (size_t)ntiles * 4 * 16, s);
+    }
+    launch_rans_fast(j, ntiles * 4, s, SidMap{3, SK_G}, ntiles * 3, SidMap{1, SK_I}); prof.mark("rans_enc_fast");
+    if (j.dbg & 0x200000) {
+      // per workgroup: start / end (100 MHz); print the spread of one launch
+      const int nb = (ntiles * 4 + 63) / 64;
+      std::vector<uint64_t> h((size_t)nb * 2);
+      (void)hipMemcpyAsync(h.data(), j.dbgbuf, h.size() * 8, hipMemcpyDeviceToHost, s);
+      (void)hipStreamSynchronize(s);
+      uint64_t b0 = ~0ull, e1 = 0, dsum = 0, dmax = 0;
+      int n = 0;
+      for (int i = 0; i < nb; i++) {
+        if (!h[2 * i]) continue;
+        b0 = std::min(b0, h[2 * i]); e1 = std::max(e1, h[2 * i + 1]);
+        const uint64_t d = h[2 * i + 1] - h[2 * i];
+        dsum += d; dmax = std::max(dmax, d); n++;
+      }
+      if (n) fprintf(stderr, "rans_fast: %d WGs, span %.0f us, mean %.0f us, max %.0f us, last start +%.0f us\n", n,
+                     (e1 - b0) / 100.0, dsum / 100.0 / n, dmax / 100.0, 0.0);
+    }
+    launch_rans_gen(j, (int)S, s); prof.mark("rans_enc_gen");
+    if (j.dbg & 0x80000) break;
+    launch_finalize(j, (int)S, s); prof.mark("finalize");
+    launch_layout(j, s);           prof.mark("layout");
+    launch_assemble(j, (int)S, s); prof.mark("assemble");
+  } while (0);
   }
   if (hipGetLastError() != hipSuccess) return HOH_E_HIP;
   if (idx) {
