@@ -92,6 +92,8 @@ __global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane, SidMa
   // chains of images in flight land on different CUs instead of sharing the first ones
   const int blk = (int)((blockIdx.x + gridDim.x - rot) % gridDim.x);
   if (blk >= nblk) return;
+  // the chain is the critical path of an image: win issue arbitration against co-resident waves
+  if (!(j.dbg & 0x400000)) __builtin_amdgcn_s_setprio(3);
   uint64_t t_beg = 0;
   if (j.dbgbuf && lane == 0) t_beg = __builtin_amdgcn_s_memrealtime();
   const int pi = blk * LANES + lane;
