@@ -15,7 +15,7 @@ One step = one pass of the hot path over the workload, inputs resident in HBM:
          .hoh is assembled (prefix + concatenation; byte-identical to a 1-GPU encode), and
          decode the shard (hoh_decode_tiles).
 value = raw RGB bytes of all ranks x K / max-over-ranks(time of the K steps) / 1e6.
-Images in flight (--inflight, default 8): each GPU keeps D images in flight, one library context,
+Images in flight (--inflight, default 12): each GPU keeps D images in flight, one library context,
 HIP stream and hardware queue per slot (GPU_MAX_HW_QUEUES raised to D), steps dealt round-robin
 to the slots.  The serial rANS chain of one image (65,536 dependent steps per tile-plane) leaves
 most CUs idle; the other images' kernels fill them.  detail.latency_ms_* is the per-image latency
@@ -125,15 +125,15 @@ def pmc_traffic(kernel, W, H):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=64)
-    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=96)
+    ap.add_argument("--warmup", type=int, default=12)
     ap.add_argument("--size", type=int, default=8192, help="image width; height per GPU")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--noise", type=int, default=4)
     ap.add_argument("--cpu-tiles", type=int, default=512)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-index", action="store_true", help="decode without the side index (serial rANS)")
-    ap.add_argument("--inflight", type=int, default=8,
+    ap.add_argument("--inflight", type=int, default=12,
                     help="images in flight per GPU (each with its own context/stream); 1 = one at a time")
     args = ap.parse_args()
     # one hardware queue per in-flight image (HIP reads this at runtime init; <= 32 allowed here)
