@@ -522,13 +522,13 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams, uint32_t
       if (sg + 1 < nseg) { const Checkpoint c2 = j.ck[xs.ckpt_off + sg + 1]; want = (uint64_t)c2.xl | ((uint64_t)c2.xh << 32); }
     }
     if (fast && act && s1 - s0 == DSEG) {
-      // a whole segment: 8 symbols per 16-B store of the lane's own (flat) output range; the
+      // a whole segment: 16 symbols per 32-B store of the lane's own (flat) output range; the
       // stores are never awaited, and nothing but the chain touches LDS
       uint4* o4 = (uint4*)(out + s0);
-      for (uint32_t g = 0; g < DSEG / 8; g++) {
-        uint32_t pk[4];
+      for (uint32_t g = 0; g < DSEG / 16; g++) {
+        uint32_t pk[8];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
+        for (int u = 0; u < 16; u++) {
           const uint32_t nw = pw[min(wi, wcap - 1)];
           const uint32_t slot = (uint32_t)x & mask;
           const uint32_t sym = sy_s[slot >> bsh] + tb[slot];
@@ -537,8 +537,10 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams, uint32_t
           x = (uint64_t)f * (x >> pb) + (slot - cc);       // Rans64DecAdvance
           if (x < (1ull << 31)) { x = (x << 32) | nw; wi++; }
         }
-        if (!(j.dbg & 32)) o4[g] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-        else if (pk[0] == 0xffffffffu) bad = true;           // keep the chain live (measurement)
+        if (!(j.dbg & 32)) {                                 // 32 contiguous bytes per thread
+          o4[2 * g] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+          o4[2 * g + 1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
+        } else if (pk[0] == 0xffffffffu) bad = true;         // keep the chain live (measurement)
       }
       if (x != want || wi > d.words) bad = true;
       continue;
@@ -732,32 +734,31 @@ __global__ __launch_bounds__(64) void k_dunpred_fast(DecJob j) {
     auto chunk = [&](const uint16_t* pl, long f) -> uint4 {
       return *(const uint4*)(pl + (f < 0 ? 0 : f));
     };
-    uint4 nG0, nG1, nR0, nR1, nB0, nB1;
-    {
-      nG0 = chunk(plG, F0); nG1 = chunk(plG, F0 + 8);
-      nR0 = chunk(plG + j.plane_cap, F0); nR1 = chunk(plG + j.plane_cap, F0 + 8);
-      nB0 = chunk(plG + 2 * (size_t)j.plane_cap, F0); nB1 = chunk(plG + 2 * (size_t)j.plane_cap, F0 + 8);
-    }
+    // residual chunks: R[k] holds the aligned 16-B chunk A_g = F0 + 8g of each plane; group g
+    // uses A_g and A_{g+1} and issues A_{g+2}, so each chunk is loaded once, one group ahead
+    // (three buffers rotate through an unroll by three: no pending load is ever copied)
+    const uint16_t* plR = plG + j.plane_cap;
+    const uint16_t* plB = plG + 2 * (size_t)j.plane_cap;
+    uint4 g0 = chunk(plG, F0), r0c = chunk(plR, F0), b0c = chunk(plB, F0);
+    uint4 g1 = chunk(plG, F0 + 8), r1c = chunk(plR, F0 + 8), b1c = chunk(plB, F0 + 8);
+    uint4 g2, r2c, b2c;
     uint32_t cG = 0, cR = 0, cB = 0;      // this lane's value at the previous step (L)
     uint32_t pG = 128, pR = 256, pB = 256; // T of the previous step (TL)
     int flushed = 0;
-    for (int s0 = 0; s0 < nst; s0 += UP_P) {
-      // land this group's chunks (issued one group ahead), then issue the next group's
-      asm volatile("" ::"v"(nG0.x), "v"(nG0.y), "v"(nG0.z), "v"(nG0.w), "v"(nG1.x), "v"(nG1.y), "v"(nG1.z), "v"(nG1.w));
-      asm volatile("" ::"v"(nR0.x), "v"(nR0.y), "v"(nR0.z), "v"(nR0.w), "v"(nR1.x), "v"(nR1.y), "v"(nR1.z), "v"(nR1.w));
-      asm volatile("" ::"v"(nB0.x), "v"(nB0.y), "v"(nB0.z), "v"(nB0.w), "v"(nB1.x), "v"(nB1.y), "v"(nB1.z), "v"(nB1.w));
+    auto group = [&](int s0, const uint4& ga, const uint4& gb, uint4& gn, const uint4& ra, const uint4& rb, uint4& rn,
+                     const uint4& ba, const uint4& bb, uint4& bn) {
+      asm volatile("" ::"v"(gb.x), "v"(gb.y), "v"(gb.z), "v"(gb.w), "v"(rb.x), "v"(rb.y), "v"(rb.z), "v"(rb.w));
+      asm volatile("" ::"v"(bb.x), "v"(bb.y), "v"(bb.z), "v"(bb.w));
       uint32_t qG[4], qR[4], qB[4];
       {
-        const uint32_t wg[8] = {nG0.x, nG0.y, nG0.z, nG0.w, nG1.x, nG1.y, nG1.z, nG1.w};
-        const uint32_t wr[8] = {nR0.x, nR0.y, nR0.z, nR0.w, nR1.x, nR1.y, nR1.z, nR1.w};
-        const uint32_t wb[8] = {nB0.x, nB0.y, nB0.z, nB0.w, nB1.x, nB1.y, nB1.z, nB1.w};
+        const uint32_t wg[8] = {ga.x, ga.y, ga.z, ga.w, gb.x, gb.y, gb.z, gb.w};
+        const uint32_t wr[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
+        const uint32_t wb[8] = {ba.x, ba.y, ba.z, ba.w, bb.x, bb.y, bb.z, bb.w};
         win8(wg, off, qG); win8(wr, off, qR); win8(wb, off, qB);
       }
       {
-        const long fn = F0 + s0 + UP_P;
-        nG0 = chunk(plG, fn); nG1 = chunk(plG, fn + 8);
-        nR0 = chunk(plG + j.plane_cap, fn); nR1 = chunk(plG + j.plane_cap, fn + 8);
-        nB0 = chunk(plG + 2 * (size_t)j.plane_cap, fn); nB1 = chunk(plG + 2 * (size_t)j.plane_cap, fn + 8);
+        const long fn = F0 + s0 + 2 * UP_P;
+        gn = chunk(plG, fn); rn = chunk(plR, fn); bn = chunk(plB, fn);
       }
 #pragma unroll
       for (int u = 0; u < UP_P; u++) {
@@ -787,6 +788,13 @@ __global__ __launch_bounds__(64) void k_dunpred_fast(DecJob j) {
       // the ring slot is reused (column 64k + 128 arrives at step 64k + 128 at the earliest)
       const int done = s0 + UP_P - 63;
       while (64 * (flushed + 1) <= done && 64 * flushed < w) { flush(flushed); flushed++; }
+    };
+    for (int s0 = 0; s0 < nst; s0 += 3 * UP_P) {
+      group(s0, g0, g1, g2, r0c, r1c, r2c, b0c, b1c, b2c);
+      if (s0 + UP_P >= nst) break;
+      group(s0 + UP_P, g1, g2, g0, r1c, r2c, r0c, b1c, b2c, b0c);
+      if (s0 + 2 * UP_P >= nst) break;
+      group(s0 + 2 * UP_P, g2, g0, g1, r2c, r0c, r1c, b2c, b0c, b1c);
     }
     while (64 * flushed < w) { flush(flushed); flushed++; }
     __syncthreads();
@@ -1066,7 +1074,7 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   j.lz_cap = (uint32_t)((j.npix_cap / 4 + j.npix_cap / 255 + 16 + 7) / 8 * 8);
   {
     // flat planes + slack for k_dunpred_fast's chunk reads one group past the end
-    j.plane_cap = (uint32_t)(((size_t)j.npix_cap + 4 * UP_P + 64 + 63) / 64 * 64);
+    j.plane_cap = (uint32_t)(((size_t)j.npix_cap + 6 * UP_P + 64 + 63) / 64 * 64);
   }
   const int S = j.ntiles * SK_PER_TILE;
   DecWork& w = ctx_dec(c);
