@@ -5,7 +5,7 @@ import sys, os, time, threading
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "hoh-ans_amd"))
 mode, D, K = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
 W = H = int(sys.argv[4]) if len(sys.argv) > 4 else 8192
-os.environ["GPU_MAX_HW_QUEUES"] = str(max(4, D))
+os.environ.setdefault("GPU_MAX_HW_QUEUES", str(max(4, D)))
 import torch, hoh_ans
 rgb = hoh_ans.synth_rgb_dev(W, H, 1, 4)
 L = hoh_ans.lib()
