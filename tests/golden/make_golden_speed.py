@@ -1,9 +1,10 @@
-"""Golden whole-file vectors for choh -s1..-s3 on the 8192^2 bench image (SURVEY §8(d) config 5:
-compressed-size parity at -s>=1), made by running the reference's own choh, compiled in place by
-oracle/ref/Makefile, on the deterministic synthetic image.  Stores size, printed size and SHA-256
-only (the files are ~95 MB).  Takes ~5 / 7 / 20 minutes per speed on one core.
+"""Golden whole-file vectors made by running the reference's own choh (compiled in place by
+oracle/ref/Makefile) on the deterministic synthetic image: choh -s1..-s4 on the 8192^2 bench
+image (compressed-size parity at -s>=1) and choh -s0 on 16384^2 (config 4,
+the sharded size).  Stores size, printed size and SHA-256 only (the files are 86-400 MB).  Takes
+~5 / 7 / 20 / 90 minutes per speed at 8192^2 and ~1 minute for 16384^2 -s0 on one core.
 
-    python tests/golden/make_golden_speed.py [speeds...]     (needs /root/reference)
+    python tests/golden/make_golden_speed.py [--size S --seed K] [speeds...]   (needs /root/reference)
 """
 import hashlib
 import json
@@ -22,11 +23,20 @@ def main():
     from hoh_ans.synth import synth_rgb
     exe = O.ref_bin("choh")
     assert exe, "reference choh not built (oracle/ref/Makefile)"
-    speeds = [int(a) for a in sys.argv[1:]] or [1, 2, 3]
-    path = os.path.join(HERE, "golden_speed.json")
-    out = json.load(open(path)) if os.path.exists(path) else {"files": []}
+    args = sys.argv[1:]
     W = H = 8192
     seed, noise = 1, 4
+    if "--size" in args:
+        i = args.index("--size")
+        W = H = int(args[i + 1])
+        del args[i:i + 2]
+    if "--seed" in args:
+        i = args.index("--seed")
+        seed = int(args[i + 1])
+        del args[i:i + 2]
+    speeds = [int(a) for a in args] or [1, 2, 3]
+    path = os.path.join(HERE, "golden_speed.json")
+    out = json.load(open(path)) if os.path.exists(path) else {"files": []}
     d = tempfile.mkdtemp()
     src = os.path.join(d, "img.rgb")
     with open(src, "wb") as f:
@@ -38,9 +48,9 @@ def main():
         rec = {"spec": {"W": W, "H": H, "seed": seed, "noise": noise, "speed": sp},
                "out": {"len": len(data), "sha256": hashlib.sha256(data).hexdigest()},
                "printed": int(r.stdout.split()[-1])}
-        out["files"] = [f for f in out["files"] if f["spec"]["speed"] != sp] + [rec]
+        out["files"] = [f for f in out["files"] if (f["spec"]["speed"], f["spec"]["W"]) != (sp, W)] + [rec]
         print(rec, flush=True)
-    out["files"].sort(key=lambda f: f["spec"]["speed"])
+    out["files"].sort(key=lambda f: (f["spec"]["W"], f["spec"]["speed"]))
     out["generator"] = "tests/golden/make_golden_speed.py (reference choh built by oracle/ref/Makefile)"
     json.dump(out, open(path, "w"), indent=1)
 

@@ -87,3 +87,41 @@ def test_shards_speed_assemble_to_file(speed):
     f = hoh_ans.file_prefix(W, H, np.concatenate(sizes)) + b"".join(blobs)
     assert f == hoh_ans.choh(img, speed=speed)[0]
     assert f == oracle.choh(img, speed)[0]
+
+
+def test_16384_golden_single_and_sharded():
+    """config 4: 16384^2 -s0, one call and as 4 shards (bands of tile rows) + prefix, against the
+    reference choh's own file (tests/golden/golden_speed.json)"""
+    import hashlib
+    import json
+    import os
+    import torch
+    import hoh_ans
+    from hoh_ans import dist as hd
+    g = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden_speed.json")))
+    recs = [f for f in g["files"] if f["spec"]["W"] == 16384 and f["spec"]["speed"] == 0]
+    if not recs:
+        pytest.skip("no 16384^2 golden")
+    sp = recs[0]["spec"]
+    W = H = 16384
+    rgb = hoh_ans.synth_rgb_dev(W, H, sp["seed"], sp["noise"])
+    out, n, printed = hoh_ans.encode_image(rgb, W, H)
+    torch.cuda.synchronize()
+    assert n == recs[0]["out"]["len"] and printed == recs[0]["printed"]
+    assert hashlib.sha256(out[:n].cpu().numpy().tobytes()).hexdigest() == recs[0]["out"]["sha256"]
+    del out
+    L = hoh_ans.lib()
+    h = hashlib.sha256()
+    blobs, sizes = [], []
+    for r in range(4):
+        t0, nt, y0, y1 = hd.shard(W, H, r, 4)
+        o = torch.empty(L.hoh_encode_bound(W, y1 - y0), dtype=torch.uint8, device="cuda")
+        sz = torch.empty(nt, dtype=torch.int32, device="cuda")
+        nb = hoh_ans.encode_tiles(rgb[y0 * W * 3:y1 * W * 3], W, H, t0, nt, o, sz, row0=y0)
+        blobs.append(o[:nb].cpu().numpy().tobytes())
+        sizes.append(sz.cpu().numpy().astype(np.uint32))
+        del o
+    h.update(hoh_ans.file_prefix(W, H, np.concatenate(sizes)))
+    for b in blobs:
+        h.update(b)
+    assert h.hexdigest() == recs[0]["out"]["sha256"]
