@@ -5,7 +5,9 @@ import sys, os, time, threading
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "hoh-ans_amd"))
 mode, D, K = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
 W = H = int(sys.argv[4]) if len(sys.argv) > 4 else 8192
-os.environ.setdefault("GPU_MAX_HW_QUEUES", str(max(4, D)))
+# one hardware queue per image in flight, as bench.py does (the GPU box exports 4); an explicit
+# PIPE_QUEUES overrides for queue-count experiments
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("PIPE_QUEUES", str(min(32, max(4, D))))
 import torch, hoh_ans
 rgb = hoh_ans.synth_rgb_dev(W, H, 1, 4)
 L = hoh_ans.lib()
