@@ -133,6 +133,9 @@ def main():
     ap.add_argument("--cpu-tiles", type=int, default=512)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-index", action="store_true", help="decode without the side index (serial rANS)")
+    ap.add_argument("--threads", action="store_true",
+                    help="N=1: one host thread per lane with synchronous calls (the N>1 mode) instead of "
+                         "enqueue-only calls from one thread")
     ap.add_argument("--inflight", type=int, default=12,
                     help="images in flight per GPU (each with its own context/stream); 1 = one at a time")
     args = ap.parse_args()
@@ -214,9 +217,34 @@ def main():
             for _ in range(count):
                 self.step()
 
+        def enqueue(self, status):
+            """One step without any host wait: encode and decode enqueued on the lane's stream;
+            their status words land in `status` (4 x int64, device); events bracket the two
+            halves for the per-image latency."""
+            with torch.cuda.stream(self.stream):
+                e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+                e0.record()
+                hoh_ans.encode_image_async(rgb, W, H, self.out, status[0:2], ctx=self.ctx, index=self.index)
+                e1.record()
+                hoh_ans.decode_image_async(self.out, self.out.numel(), W, H, self.dec, status[2:4], ctx=self.ctx,
+                                           index=self.index)
+                e2.record()
+            self.events.append((e0, e1, e2))
+
     lanes = [Lane(k) for k in range(D)]
+    for ln in lanes:
+        ln.events = []
+    # N = 1: enqueue-only -- one host thread deals the steps round-robin to the lanes and never
+    # waits inside the timed region (statuses are checked afterwards).  N > 1 needs the tile sizes
+    # on the host for the gather, so each lane is a host thread running synchronous steps.
+    use_async = world == 1 and not args.threads
+    status = torch.zeros((max(args.steps, args.warmup, D), 4), dtype=torch.int64, device=dev)
 
     def run_all(total):
+        if use_async:
+            for i in range(total):
+                lanes[i % D].enqueue(status[i])
+            return
         # steps are dealt round-robin to the lanes; each lane runs its share back to back
         shares = [total // D + (1 if k < total % D else 0) for k in range(D)]
         if D == 1:
@@ -228,12 +256,23 @@ def main():
         for x in th:
             x.join()
 
+    def check_status(total):
+        st = status[:total].cpu().numpy()
+        for i in range(total):
+            hoh_ans.check_status(st[i, 0:2], "encode (step %d)" % i)
+            hoh_ans.check_status(st[i, 2:4], "decode (step %d)" % i)
+        return int(st[total - 1, 1])
+
     for ln in lanes:
         ln.ctx.profiling(True)
     run_all(max(args.warmup, D))
+    torch.cuda.synchronize()
+    if use_async:
+        check_status(max(args.warmup, D))
     for ln in lanes:
         ln.ctx.reset_stats()
         ln.t_enc = ln.t_dec = 0.0
+        ln.events = []
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -249,6 +288,13 @@ def main():
             a0, c0 = stats.get(k, (0.0, 0))
             stats[k] = (a0 + tot, c0 + cnt)
         ln.ctx.profiling(False)
+    if use_async:
+        n_async = check_status(args.steps)
+        for ln in lanes:
+            ln.n = n_async
+            for e0, e1, e2 in ln.events:
+                ln.t_enc += e0.elapsed_time(e1) * 1e-3
+                ln.t_dec += e1.elapsed_time(e2) * 1e-3
     t_enc = sum(ln.t_enc for ln in lanes)
     t_dec = sum(ln.t_dec for ln in lanes)
     # per-kernel durations of one image alone (no other image in flight), for the record

@@ -15,6 +15,8 @@
 #include <string>
 
 void launch_synth(uint8_t* rgb, int W, int H, int y0, uint64_t seed, int noise, hipStream_t s);
+void launch_put_bytes(uint8_t* dst, const uint8_t* b, int n, hipStream_t s);
+void launch_status_enc(const uint32_t* gerr, const uint64_t* total, uint64_t cap, uint64_t* out, hipStream_t s);
 
 namespace {
 
@@ -76,6 +78,7 @@ static void prof_fold(hoh_ctx* c) {
   if (c->nmark >= 2) {
     (void)hipEventSynchronize(c->kev[c->nmark - 1]);
     for (size_t i = 1; i < c->nmark; i++) {
+      if (c->knames[i] == "start") continue;
       float v = 0;
       (void)hipEventElapsedTime(&v, c->kev[i - 1], c->kev[i]);
       size_t k = 0;
@@ -104,7 +107,9 @@ static void prof_mark(hoh_ctx* c, hipStream_t s, const char* name, bool reset) {
 struct Prof {
   hoh_ctx* c;
   hipStream_t s;
-  explicit Prof(hoh_ctx* c_, hipStream_t s_) : c(c_), s(s_) { prof_mark(c, s, "start", true); }
+  // an enqueue-only call must not wait for the previous call's events: it appends its marks
+  // (the interval ending at its "start" mark spans the gap between calls and is not counted)
+  Prof(hoh_ctx* c_, hipStream_t s_, bool async = false) : c(c_), s(s_) { prof_mark(c, s, "start", !async); }
   void mark(const char* name) { prof_mark(c, s, name, false); }
 };
 
@@ -289,15 +294,18 @@ static int ensure_log2_tables(hoh_ctx* c, int W, int H, EncodeJob& j) {
   return HOH_OK;
 }
 
+// d_status == nullptr: synchronous (the host waits and maps the status word).  Otherwise
+// enqueue-only: {status code, total bytes} are written to d_status by the stream.
 static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int t0, int ntiles,
                              uint8_t* d_out, size_t cap, uint64_t prefix, int write_table,
                              uint32_t* d_tile_sizes, uint64_t* total_out, hoh_index* idx,
-                             hipStream_t s, int speed = 0) {
+                             hipStream_t s, int speed = 0, uint64_t* d_status = nullptr) {
+  const bool async = d_status != nullptr;
   int xt, yt, tw, th;
   hoh_tiling(W, H, &xt, &yt, &tw, &th);
   if (tw > HOH_MAX_TILE_W || (size_t)tw * th > (1u << 24)) return HOH_E_UNSUPPORTED;
   if (t0 < 0 || ntiles <= 0 || t0 + ntiles > xt * yt) return HOH_E_ARG;
-  Prof prof(c, s);
+  Prof prof(c, s, async);
   EncodeJob j;
   memset(&j, 0, sizeof(j));
   {
@@ -357,6 +365,7 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   j.tab_fast = (EncFast*)c->tab_fast.p;
   j.tab_gen = (EncGen*)c->tab_gen.p;
   j.slabs = (uint32_t*)c->slabs.p;
+  j.slab_words = nslab;
   j.ckpt = speed ? nullptr : (Checkpoint*)c->ckpt.p;      // -s>=1 files get no side index
   j.gerr = (uint32_t*)c->misc.p;
   j.total = (uint64_t*)((uint8_t*)c->misc.p + 8);
@@ -383,13 +392,13 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
     if (j.dbg & 0x20000) break;
     launch_tables(j, (int)S, s);   prof.mark("tables");
     if (j.dbg & 0x40000) break;
-    if (j.dbg & 0x200000) {
+    if ((j.dbg & 0x200000) && !async) {
       if ((e = ensure(c->dbgb, (size_t)ntiles * 4 * 16))) return e;
       j.dbgbuf = (uint64_t*)c->dbgb.p;
       (void)hipMemsetAsync(j.dbgbuf, 0, (size_t)ntiles * 4 * 16, s);
     }
     launch_rans_fast(j, ntiles * 4, s, SidMap{3, SK_G}, ntiles * 3, SidMap{1, SK_I}); prof.mark("rans_enc_fast");
-    if (j.dbg & 0x200000) {
+    if ((j.dbg & 0x200000) && !async) {
       // per workgroup: start / end (100 MHz); print the spread of one launch
       const int nb = (ntiles * 4 + 63) / 64;
       std::vector<uint64_t> h((size_t)nb * 2);
@@ -418,6 +427,10 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
     int r = index_capture(idx, j, s);
     if (r) return r;
     prof.mark("index");
+  }
+  if (async) {
+    launch_status_enc(j.gerr, j.total, cap, d_status, s);
+    return hipGetLastError() == hipSuccess ? HOH_OK : HOH_E_HIP;
   }
   if (hipMemcpyAsync(c->pinned, c->misc.p, 16, hipMemcpyDeviceToHost, s) != hipSuccess) return HOH_E_HIP;
   if (hipStreamSynchronize(s) != hipSuccess) return HOH_E_HIP;
@@ -474,10 +487,9 @@ int hoh_encode_image_ix(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int spee
   uint64_t total = 0;
   int r;
   if (tiled) {
+    launch_put_bytes(d_out, hb, (int)hl, s);      // the header, ahead of the tiles (one host sync per call)
     r = encode_tiles_impl(c, d_rgb, W, H, 0, xt * yt, d_out, cap, hl, 1, nullptr, &total, idx, s, speed);
     if (speed && idx) idx->nstreams = 0;
-    if (r == HOH_OK && hipMemcpyAsync(d_out, hb, hl, hipMemcpyHostToDevice, s) != hipSuccess) r = HOH_E_HIP;
-    if (r == HOH_OK && hipStreamSynchronize(s) != hipSuccess) r = HOH_E_HIP;
     *out_size = (size_t)total;
     if (printed) *printed = (size_t)total;
   } else {
@@ -494,6 +506,25 @@ int hoh_encode_image_ix(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int spee
     if (idx) idx->nstreams = 0;
   }
   return r;
+}
+
+int hoh_encode_image_async(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int speed, uint8_t* d_out, size_t cap,
+                           hoh_index* idx, uint64_t* d_status, void* stream) {
+  if (!c || !d_rgb || !d_out || !d_status || W <= 0 || H <= 0 || speed < 0 || speed > 4) return HOH_E_ARG;
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick(c, stream);
+  uint8_t hb[32];
+  int xt, yt, tw, th;
+  if (!hoh_tiling(W, H, &xt, &yt, &tw, &th)) return HOH_E_UNSUPPORTED;  // header-only files: use the sync call
+  size_t hl = header_fixed(W, H, hb);
+  hb[hl++] = (uint8_t)(xt - 1);
+  hb[hl++] = (uint8_t)(yt - 1);
+  if (cap < hl) return HOH_E_CAP;
+  if (speed && idx) idx->nstreams = 0;
+  launch_put_bytes(d_out, hb, (int)hl, s);
+  uint64_t total = 0;
+  return encode_tiles_impl(c, d_rgb, W, H, 0, xt * yt, d_out, cap, hl, 1, nullptr, &total, speed ? nullptr : idx, s,
+                           speed, d_status);
 }
 
 int hoh_encode_image(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int speed, uint8_t* d_out, size_t cap,

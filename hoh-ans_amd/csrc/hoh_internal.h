@@ -173,6 +173,7 @@ struct EncodeJob {
   uint32_t gen_stride;    // entries per stream in tab_gen (>= range)
   uint32_t hdr_cap;       // bytes per stream in hdr
   uint32_t* slabs;        // rANS words
+  uint64_t slab_words;    // words in slabs (bounds of the encoder's indexed stores; 0 = unchecked)
   Checkpoint* ckpt;
   uint32_t* gerr;         // global error word
   uint64_t* total;        // total bytes of the tile blob

@@ -89,11 +89,30 @@ __device__ uint64_t block_scan_1024(uint64_t v, uint64_t* wsum, uint64_t* total)
   return v;
 }
 
+// Enqueue-only decodes have no host check between kernels: every kernel returns at once when an
+// earlier kernel (or the header check) recorded an error.  Block-uniform: one read, one barrier
+// (a block of the same kernel may set the word meanwhile).
+__device__ __forceinline__ bool dec_abort(const DecJob& j) {
+  __shared__ uint32_t g_abort;
+  if (threadIdx.x == 0) g_abort = *(volatile const uint32_t*)j.gerr;
+  __syncthreads();
+  return g_abort != 0;
+}
+
+// the .hoh prefix the caller's W, H imply (async decode): magic .. tiling bytes, <= 16 bytes
+__global__ void k_dhdr(DecJob j, uint64_t lo, uint64_t hi, int n) {
+  const int i = threadIdx.x;
+  if (i >= n) return;
+  const uint8_t want = (uint8_t)((i < 8 ? lo >> (8 * i) : hi >> (8 * (i - 8))) & 255);
+  if ((uint64_t)i >= j.size || j.in[i] != want) atomicOr(j.gerr, 1u);
+}
+
 // Tile table (dhoh.cpp:42-65): n-1 varints after the header give tile sizes.  Parallel parse:
 // a varint ends at a byte < 0x80, unless a run of >= 3 bytes >= 0x80 occurs (varint.hpp reads a
 // third byte whole), in which case thread 0 re-parses serially.  Shard decode (tsizes set)
 // takes the sizes from the caller instead.  Sizes are parked in tiles[i+1].off, then scanned.
 __global__ __launch_bounds__(1024) void k_dtable(DecJob j) {
+  if (dec_abort(j)) return;
   __shared__ uint64_t wsum[17];
   __shared__ uint64_t tend;
   __shared__ int serial;
@@ -288,6 +307,7 @@ __device__ bool parse_stream(const DecJob& j, uint64_t& p, int sid, uint64_t out
 }
 
 __global__ __launch_bounds__(64) void k_dparse(DecJob j) {
+  if (dec_abort(j)) return;
   const int t = blockIdx.x, lane = threadIdx.x;
   DecTile ti = j.tiles[t];
   uint64_t p = ti.off;
@@ -335,6 +355,7 @@ __global__ __launch_bounds__(64) void k_dparse(DecJob j) {
 
 // match the decoder's streams to the side index by payload position
 __global__ void k_dmatch(DecJob j, int nstreams) {
+  if (dec_abort(j)) return;
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nstreams || s >= j.nix) return;
   DecStream d = j.streams[s];
@@ -415,6 +436,7 @@ __device__ bool dec_run(const DecJob& j, const DecStream& d, const uint32_t* cum
 // the flat plane: each thread stores its segment 8 symbols (16 B) at a time.
 __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams, uint32_t wcap) {
   extern __shared__ __attribute__((aligned(16))) uint32_t dr_lds[];
+  if (dec_abort(j)) return;
   const int tid = threadIdx.x;
   const int sid = blockIdx.x;
   const DecStream d = j.streams[sid];
@@ -580,6 +602,7 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams, uint32_t
 
 // Without an index: one lane per stream, tables from the parse kernel (512 buckets).
 __global__ __launch_bounds__(64) void k_drans_serial(DecJob j, int nstreams) {
+  if (dec_abort(j)) return;
   const int sid = blockIdx.x * 64 + threadIdx.x;
   if (sid >= nstreams) return;
   const DecStream d = j.streams[sid];
@@ -596,6 +619,7 @@ __global__ __launch_bounds__(64) void k_drans_serial(DecJob j, int nstreams) {
 
 // stored streams: MSB-first fixed-width fields
 __global__ void k_dstored(DecJob j, int nstreams) {
+  if (dec_abort(j)) return;
   const int sid = blockIdx.x;
   const DecStream d = j.streams[sid];
   if (d.mode != SM_STORED) return;
@@ -609,6 +633,7 @@ __global__ void k_dstored(DecJob j, int nstreams) {
 
 // LZ streams -> matches (un_lz.hpp:150-170); one lane per tile
 __global__ void k_dlz(DecJob j) {
+  if (dec_abort(j)) return;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= j.ntiles) return;
   DecTile ti = j.tiles[t];
@@ -692,6 +717,7 @@ __device__ __forceinline__ void win8(const uint32_t* w, uint32_t off, uint32_t* 
 // all 64 rows have passed it.
 __global__ __launch_bounds__(64) void k_dunpred_fast(DecJob j) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  if (dec_abort(j)) return;
   const int t = blockIdx.x;
   const DecTile ti = j.tiles[t];
   if (ti.err || !unpred_fast(j, t, ti)) return;
@@ -832,6 +858,7 @@ __device__ __forceinline__ uint32_t unpred_px(uint32_t T, uint32_t L, uint32_t T
 // copied pixels) are staged in LDS first.  Needs w >= 64 (copies reach at most one row up).
 __global__ __launch_bounds__(64) void k_dunpred_lz(DecJob j) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lz_lds[];
+  if (dec_abort(j)) return;
   const int t = blockIdx.x;
   const DecTile ti = j.tiles[t];
   if (ti.err || unpred_fast(j, t, ti) || ti.w < 64) return;
@@ -930,6 +957,7 @@ __global__ __launch_bounds__(64) void k_dunpred_lz(DecJob j) {
 // Tiles with LZ copies narrower than 64 pixels (copies may reach two rows up): serial raster
 // walk per plane, one lane per plane, into dplane.
 __global__ __launch_bounds__(192) void k_dunpred_serial(DecJob j) {
+  if (dec_abort(j)) return;
   const int t = blockIdx.x;
   const DecTile ti = j.tiles[t];
   if (ti.err || unpred_fast(j, t, ti) || ti.w >= 64) return;
@@ -990,7 +1018,13 @@ static int dbuf(DecWork& w, int k, size_t bytes, void** p) {
   return 0;
 }
 
-static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s);
+struct AsyncDec {              // enqueue-only decode: expected header bytes and the status slot
+  uint64_t hdr[2];
+  int hl;
+  uint64_t* status;
+};
+static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s, const AsyncDec* as = nullptr);
+void launch_status_dec(const uint32_t* gerr, uint64_t bytes, uint64_t* out, hipStream_t s);
 
 int decode_image_impl(hoh_ctx* c, const uint8_t* d_in, size_t size, uint8_t* d_rgb, size_t cap, int* Wp, int* Hp,
                       const hoh_index* idx, hipStream_t s) {
@@ -1030,6 +1064,36 @@ int decode_image_impl(hoh_ctx* c, const uint8_t* d_in, size_t size, uint8_t* d_r
   return decode_run(c, j, idx, s);
 }
 
+// enqueue-only decode of a W x H file (the caller knows the dimensions; the header is checked on
+// the device); {status, W*H*3} land in d_status
+int decode_image_async_impl(hoh_ctx* c, const uint8_t* d_in, size_t size, int W, int H, uint8_t* d_rgb, size_t cap,
+                            const hoh_index* idx, uint64_t* d_status, hipStream_t s) {
+  if (!((W >= 512 || H >= 512) && W >= 256 && H >= 256)) return 6;   // header-only files: sync call
+  if ((size_t)W * H * 3 > cap) return 2;
+  DecJob j;
+  memset(&j, 0, sizeof(j));
+  j.W = W; j.H = H;
+  j.xt = W / 256; j.yt = H / 256;
+  j.tw = (W + j.xt - 1) / j.xt; j.th = (H + j.yt - 1) / j.yt;
+  uint8_t hb[16];
+  int p = 0;
+  hb[p++] = 153; hb[p++] = 72; hb[p++] = 79; hb[p++] = 72; hb[p++] = 2; hb[p++] = 8;   // choh.cpp:437-446
+  for (uint32_t v : {(uint32_t)W - 1, (uint32_t)H - 1}) p = (int)hoh_write_varint(hb, (uint32_t)p, v);
+  hb[p++] = (uint8_t)(j.xt - 1);
+  hb[p++] = (uint8_t)(j.yt - 1);
+  AsyncDec as;
+  as.hdr[0] = as.hdr[1] = 0;
+  for (int i = 0; i < p; i++) as.hdr[i / 8] |= (uint64_t)hb[i] << (8 * (i % 8));
+  as.hl = p;
+  as.status = d_status;
+  j.prefix = (uint64_t)p;
+  j.ntiles = j.xt * j.yt;
+  j.in = d_in;
+  j.size = size;
+  j.rgb = d_rgb;
+  return decode_run(c, j, idx, s, &as);
+}
+
 // shard decode: tiles [t0, t0+ntiles) of a W x H image, their bytes concatenated in d_blob
 int decode_tiles_impl(hoh_ctx* c, const uint8_t* d_blob, size_t size, int W, int H, int t0, int ntiles,
                       const uint32_t* h_sizes, uint8_t* d_rgb, const hoh_index* idx, hipStream_t s) {
@@ -1058,7 +1122,7 @@ int decode_tiles_impl(hoh_ctx* c, const uint8_t* d_blob, size_t size, int W, int
   return decode_run(c, j, idx, s);
 }
 
-static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s) {
+static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s, const AsyncDec* as) {
   {
     const char* e = getenv("HOH_DEC_DBG");
     j.dbg = e ? (uint32_t)atoi(e) : 0;
@@ -1095,20 +1159,24 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   const int indexed = j.ix && j.nix == S;
   if (hipMemsetAsync(j.gerr, 0, 64, s) != hipSuccess) return 3;
   if (hipMemsetAsync(j.streams, 0, (size_t)S * sizeof(DecStream), s) != hipSuccess) return 3;
-  ctx_mark(c, s, "start", true);
+  ctx_mark(c, s, "start", as == nullptr);
+  if (as) hipLaunchKernelGGL(k_dhdr, dim3(1), dim3(64), 0, s, j, as->hdr[0], as->hdr[1], as->hl);
   hipLaunchKernelGGL(k_dtable, dim3(1), dim3(1024), 0, s, j);
   ctx_mark(c, s, "dtable", false);
   hipLaunchKernelGGL(k_dparse, dim3(j.ntiles), dim3(64), 0, s, j);
   ctx_mark(c, s, "dparse", false);
   uint64_t* pin = ctx_pinned(c);
-  if (hipMemcpyAsync(pin, j.gerr, 8, hipMemcpyDeviceToHost, s) != hipSuccess) return 3;
-  if (hipStreamSynchronize(s) != hipSuccess) return 3;
-  {
+  // the largest payload sizes k_drans's LDS stage; an enqueue-only call cannot wait for it and
+  // stages streams of up to 40 KB (two workgroups per CU; larger streams decode unstaged)
+  uint32_t maxw = 10240;
+  if (!as) {
+    if (hipMemcpyAsync(pin, j.gerr, 8, hipMemcpyDeviceToHost, s) != hipSuccess) return 3;
+    if (hipStreamSynchronize(s) != hipSuccess) return 3;
     const uint32_t ge = (uint32_t)pin[0];
     if (ge & 2) return 6;
     if (ge) return 7;
+    maxw = (uint32_t)(pin[0] >> 32);
   }
-  const uint32_t maxw = (uint32_t)(pin[0] >> 32);
   if (indexed) {
     // payload stage sized to the largest stream when it fits next to the tables (<= 128 KB)
     const size_t fixed = (514 + 512 + 8192) * 4;                      // cum + bucket symbols + slot table
@@ -1128,6 +1196,10 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   hipLaunchKernelGGL(k_dunpred_serial, dim3(j.ntiles), dim3(192), 0, s, j);
   ctx_mark(c, s, "dunpred", false);
   if (hipGetLastError() != hipSuccess) return 3;
+  if (as) {
+    launch_status_dec(j.gerr, (uint64_t)j.W * j.H * 3, as->status, s);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+  }
   if (j.dbg & 16) {
     std::vector<uint64_t> h((size_t)S * 4);
     (void)hipMemcpyAsync(h.data(), j.dbgbuf, h.size() * 8, hipMemcpyDeviceToHost, s);

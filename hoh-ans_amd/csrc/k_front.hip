@@ -1,22 +1,33 @@
-// Encoder front end, one workgroup (4 waves) per 256x256 tile (choh.cpp:464-500 tiles are
-// independent), streaming the tile in raster blocks of 256 pixels (one barrier per block):
+// Encoder front end, one workgroup (4 waves) per tile (choh.cpp:464-500 tiles are independent),
+// streaming the tile in raster blocks of 256 positions:
 //  * subtract-green (channel.hpp:73-79) + MED fast-path residuals for the three planes
-//    (prediction.hpp:6-44), written to the residual arena, histograms in LDS;
+//    (prediction.hpp:6-44), written to the residual arena, histograms in LDS.  A pixel is kept
+//    as {R' | B' << 16, rgb}: the two 9-bit planes go through packed 16-bit arithmetic (the
+//    uint16 gradient wrap of Q8 is exactly the packed u16 wrap), G through SDWA byte selects;
 //  * grey test (channel.hpp:21-31) and distinct-colour count capped at 257 (choh.cpp:17-46);
 //  * LZ candidate detection for find_lz_rgb at -s0 (lz.hpp:32-53): a position q is a candidate
 //    iff some back distance b in [1, min(64, q)] gives 4 equal RGB pixels q..q+3 vs q-b..q-b+3.
 //    Each wave fingerprints the 4-pixel windows of its 64 positions and of the 64 before them,
-//    counts the 128 fingerprints in a wave-private LDS hash table, and checks exactly (b = 1..64,
-//    first hit wins) only the positions whose fingerprint occurs twice; equal windows have equal
-//    fingerprints, so the candidate set is exact.  The greedy selection runs in k_lz.hip over
-//    the (sparse) candidate bitmap.
+//    counts the 128 fingerprints in a wave-private LDS hash table and checks exactly
+//    (b = 1..64, first hit wins) only positions whose fingerprint occurs twice; equal windows
+//    have equal fingerprints, so the candidate set is exact.  The greedy selection runs in
+//    k_lz.hip over the (sparse) candidate bitmap.
 // Pixels live in an LDS ring (stored twice, so reads at q+k and q-d never wrap); every pixel is
-// read from HBM once, one block ahead of its use.
+// read from HBM once (one unaligned dword), one block ahead of its use.  Tiles wider than the
+// ring allows (only untiled images) read their neighbours from memory instead.
 #include "hoh_internal.h"
 
-#define RING 2048               // pixels: >= the 1024-pixel span [q - 512, q + 512) in use
+#define RING 2048               // positions; the span in use is [q - w - 1 - 256, q + 512)
+#define RING_MAX_W 1200
 #define WTAB 512                // slots of a wave's fingerprint table (128 keys)
+#define CSET 512                // colour set slots (<= 257 colours are counted)
 #define NT 256
+#define PF 4                    // blocks of HBM loads in flight per thread
+
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ us2 as_us2(uint32_t v) { return __builtin_bit_cast(us2, v); }
+__device__ __forceinline__ uint32_t as_u32(us2 v) { return __builtin_bit_cast(uint32_t, v); }
 
 __device__ __forceinline__ uint16_t med16(uint16_t a, uint16_t b, uint16_t c) {
   // predictor_operations.hpp:37-60, uint16_t overload (selected by overload resolution: Q8)
@@ -24,9 +35,10 @@ __device__ __forceinline__ uint16_t med16(uint16_t a, uint16_t b, uint16_t c) {
   return b < c ? b : (c > a ? c : a);
 }
 
-__device__ __forceinline__ uint32_t plane_val(uint32_t px, int k) {
-  uint32_t r = px & 255, g = (px >> 8) & 255, b = px >> 16;
-  return k == 0 ? g : k == 1 ? r - g + 256 : b - g + 256;
+// R' | B' << 16 of a packed pixel r | g << 8 | b << 16 (R' = r - g + 256, B' = b - g + 256)
+__device__ __forceinline__ uint32_t rb_form(uint32_t rgb) {
+  const uint32_t g = (rgb >> 8) & 255u;
+  return ((rgb & 0x00ff00ffu) | 0x01000100u) - g * 0x10001u;
 }
 
 __device__ __forceinline__ uint32_t fp32(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
@@ -41,7 +53,13 @@ __device__ __forceinline__ uint32_t fp32(uint32_t a, uint32_t b, uint32_t c, uin
 // inserted a second time sets the slot's duplicate bit
 __device__ __forceinline__ uint32_t wt_insert(uint32_t* key, uint32_t* dup, uint32_t k) {
   uint32_t sl = (k >> 1) & (WTAB - 1);
-  for (int probe = 0; probe < WTAB; probe++) {
+  {
+    const uint32_t old = atomicCAS(&key[sl], 0u, k);     // the common case: first probe
+    if (old == 0u) return sl;
+    if (old == k) { atomicOr(&dup[sl >> 5], 1u << (sl & 31)); return sl; }
+    sl = (sl + 1) & (WTAB - 1);
+  }
+  for (int probe = 1; probe < WTAB; probe++) {
     const uint32_t old = atomicCAS(&key[sl], 0u, k);
     if (old == 0u) return sl;
     if (old == k) { atomicOr(&dup[sl >> 5], 1u << (sl & 31)); return sl; }
@@ -50,13 +68,21 @@ __device__ __forceinline__ uint32_t wt_insert(uint32_t* key, uint32_t* dup, uint
   return WTAB;
 }
 
-__global__ __launch_bounds__(NT) void k_front(EncodeJob j) {
-  __shared__ uint32_t ring[2 * RING];
-  __shared__ uint32_t wkey[4][WTAB];
+// pixel at raster position q of a tile read from memory (tiles too wide for the ring)
+__device__ __forceinline__ uint32_t px_mem(const uint8_t* img, size_t pitch, int w, uint32_t npix, uint32_t q) {
+  if (q >= npix) return 0;                           // incl. positions before the tile (wrapped)
+  const uint32_t y = q / (uint32_t)w, x = q - y * (uint32_t)w;
+  const uint8_t* p = img + (size_t)y * pitch + (size_t)x * 3;
+  return p[0] | (p[1] << 8) | (p[2] << 16);
+}
+
+template <bool RINGED>
+__device__ __forceinline__ void front_tile(const EncodeJob& j, uint32_t* ring) {
+  __shared__ uint32_t wkey[4][WTAB + 1];
   __shared__ uint32_t wdup[4][WTAB / 32];
   __shared__ uint32_t hist[3][512];
-  __shared__ uint32_t hset[1024];
-  __shared__ uint32_t hpos[1024];                   // first raster position of each colour
+  __shared__ uint32_t hset[CSET];
+  __shared__ uint32_t hpos[CSET];                   // first raster position of each colour
   __shared__ int s_ncol, s_notgrey, s_ncand, s_np;
 
   const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -65,99 +91,159 @@ __global__ __launch_bounds__(NT) void k_front(EncodeJob j) {
   const int w = min(j.tw, j.W - x0), h = min(j.th, j.H - y0);
   const uint32_t npix = (uint32_t)w * h;
   for (int i = tid; i < 3 * 512; i += NT) (&hist[0][0])[i] = 0;
-  for (int i = tid; i < 1024; i += NT) { hset[i] = 0xffffffffu; hpos[i] = 0xffffffffu; }
-  for (int i = lane; i < WTAB; i += 64) wkey[wv][i] = 0;
+  for (int i = tid; i < CSET; i += NT) { hset[i] = 0xffffffffu; hpos[i] = 0xffffffffu; }
+  for (int i = lane; i <= WTAB; i += 64) wkey[wv][i] = 0;
   if (lane < WTAB / 32) wdup[wv][lane] = 0;
   if (tid == 0) { s_ncol = 0; s_notgrey = 0; s_ncand = 0; s_np = 0; }
 
-  uint16_t* res[3];
-  for (int k = 0; k < 3; k++) res[k] = j.sym + med_plane_off(j, t, k);
+  uint16_t* res0 = j.sym + med_plane_off(j, t, 0);
+  uint16_t* res1 = j.sym + med_plane_off(j, t, 1);
+  uint16_t* res2 = j.sym + med_plane_off(j, t, 2);
   uint64_t* cand = j.candbits + (size_t)t * (j.npix_cap / 64);
   const uint8_t* img = j.rgb + ((size_t)y0 * j.W + x0) * 3;
   const size_t pitch = (size_t)j.W * 3;
+  const bool lz = !(j.dbg & 4) && j.speed == 0;     // -s>=1: k_lzcand screens a longer window
 
-  // loader cursor: this thread's pixel of the block being loaded (raster blk*256 + tid)
-  int lx = tid, ly = 0;
-  while (lx >= w) { lx -= w; ly++; }
+  // loader cursor: this thread's pixel of the block being loaded (raster blk*256 + tid) as a
+  // byte offset from the tile origin
+  int lx = tid;
+  uint32_t loff = 0;
+  while (lx >= w) { lx -= w; loff += (uint32_t)pitch; }
+  loff += (uint32_t)lx * 3;
+  const uint32_t wrap = (uint32_t)pitch - (uint32_t)w * 3;
+  // branch-free pixel fetch: an unaligned dword whose top 3 bytes are the pixel (the image's
+  // very first pixel takes the dword at its own address instead); positions past the tile
+  // fetch the tile's first pixel and return 0
+  // Only the tile's own pixels may be read (a shard's buffer starts at its first row), so a
+  // pixel that starts a tile row reads the dword at itself (its 3 bytes + the next pixel's
+  // first), every other pixel the dword ending with it (the previous pixel's last byte + its 3);
+  // positions past the tile read the tile's first pixel and return 0.  1-pixel-wide tiles
+  // (untiled W = 1 images) read bytes.
   auto load_px = [&](uint32_t q) -> uint32_t {
-    if (q >= npix) return 0;
-    const uint8_t* p = img + (size_t)ly * pitch + (size_t)lx * 3;
-    return p[0] | (p[1] << 8) | (p[2] << 16);
+    const bool in = q < npix;
+    if (w < 2) return in ? (img[loff] | (img[loff + 1] << 8) | (img[loff + 2] << 16)) : 0u;
+    const bool at_self = !in || lx == 0;
+    const uint32_t a = !in ? 0u : (lx == 0 ? loff : loff - 1);
+    uint32_t v;
+    __builtin_memcpy(&v, img + a, 4);
+    v = at_self ? (v & 0xffffffu) : (v >> 8);
+    return in ? v : 0u;
   };
-  auto advance = [&]() { lx += NT; while (lx >= w) { lx -= w; ly++; } };
-  {
-    const uint32_t v0 = load_px(tid);
-    ring[tid & (RING - 1)] = v0;
-    ring[(tid & (RING - 1)) + RING] = v0;
+  const bool wide_rows = w >= NT;                    // a block advance wraps at most one row
+  auto advance = [&]() {
+    lx += NT;
+    loff += NT * 3;
+    if (wide_rows) {
+      const bool wr = lx >= w;
+      lx -= wr ? w : 0;
+      loff += wr ? wrap : 0u;
+    } else {
+      while (lx >= w) { lx -= w; loff += wrap; }
+    }
+  };
+  uint32_t own = 0, nv[PF];
+  if (RINGED) {
+    own = load_px(tid);
+    ring[tid & (RING - 1)] = own;
+    ring[(tid & (RING - 1)) + RING] = own;
     advance();
+#pragma unroll
+    for (int k = 1; k <= PF; k++) {
+      nv[k % PF] = load_px((uint32_t)k * NT + tid);
+      advance();
+    }
   }
-  uint32_t nextv = load_px(NT + tid);
-  advance();
   // compute cursor: (x, y) of position base + tid
   uint32_t cx = tid, cy = 0;
   while (cx >= (uint32_t)w) { cx -= w; cy++; }
   __syncthreads();
 
-  int notgrey = 0, ncand = 0;
+  uint32_t notgrey = 0;
+  int ncand = 0;
   const uint32_t nblk = (npix + NT - 1) / NT;
-  for (uint32_t blk = 0; blk < nblk; blk++) {
+  auto body = [&](const uint32_t blk, uint32_t& slot) {
     const uint32_t base = blk * NT;
-    {   // land block blk+1, issue block blk+2
-      const uint32_t qn = base + NT + tid;
-      ring[qn & (RING - 1)] = nextv;
-      ring[(qn & (RING - 1)) + RING] = nextv;
-      nextv = load_px(base + 2 * NT + tid);
-      advance();
-    }
-    __syncthreads();
     const uint32_t q = base + tid;
-    const bool act = q < npix;
+    uint32_t v;
+    if (RINGED) {   // land block blk+1, issue block blk+1+PF into its slot
+      const uint32_t qn = base + NT + tid;
+      ring[qn & (RING - 1)] = slot;
+      ring[(qn & (RING - 1)) + RING] = slot;
+      v = own;
+      own = slot;
+      slot = load_px(base + (1 + PF) * NT + tid);
+      advance();
+    } else {
+      v = px_mem(img, pitch, w, npix, q);
+    }
+    // forward / backward neighbours by raster distance: ring copies [ri] and [ri + RING] hold
+    // the same pixels, so q + k and q - d never wrap
     const uint32_t ri = q & (RING - 1);
-    const uint32_t* fwd = ring + ri;              // fwd[k] = pixel q + k
-    const uint32_t* bwd = ring + ri + RING;       // bwd[-d] = pixel q - d
-    const uint32_t v = fwd[0];
+    auto F = [&](uint32_t k) -> uint32_t { return RINGED ? ring[ri + k] : px_mem(img, pitch, w, npix, q + k); };
+    auto B = [&](uint32_t d) -> uint32_t { return RINGED ? ring[ri + RING - d] : px_mem(img, pitch, w, npix, q - d); };
+    __syncthreads();
+    const bool act = q < npix;
     if (act) {
-      const uint32_t pr = v & 255, pg = (v >> 8) & 255, pbb = v >> 16;
-      notgrey |= (pr != pg) | (pr != pbb);
-      if (s_ncol <= 256 && !(j.dbg & 1)) {         // distinct colours, stop past 256
-        uint32_t hsh = (v * 2654435761u) >> 22;
-        for (int probe = 0; probe < 1024; probe++) {
+      const uint32_t g = (v >> 8) & 255u;
+      notgrey |= (v ^ (g * 0x010101u)) & 0xffffffu;
+      if (__builtin_amdgcn_readfirstlane(s_ncol) <= 256 && !(j.dbg & 1)) {   // distinct colours, stop past 256
+        uint32_t hsh = (v * 2654435761u) >> 23;
+        for (int probe = 0; probe < CSET; probe++) {
           uint32_t old = atomicCAS(&hset[hsh], 0xffffffffu, v);
           if (old == 0xffffffffu) { atomicAdd(&s_ncol, 1); atomicMin(&hpos[hsh], q); break; }
           if (old == v) { atomicMin(&hpos[hsh], q); break; }
-          hsh = (hsh + 1) & 1023;
+          hsh = (hsh + 1) & (CSET - 1);
         }
       }
+      // neighbours; outside the tile the reference uses c/2 in every plane (prediction.hpp:21-28),
+      // i.e. the grey pixel 128,128,128 (G = 128, R' = B' = 256)
       const bool hasL = cx > 0, hasT = cy > 0;
-      const uint32_t vL = hasL ? bwd[-1] : 0;
-      const uint32_t vT = hasT ? bwd[-w] : 0;
-      const uint32_t vTL = (hasL && hasT) ? bwd[-w - 1] : 0;
-#pragma unroll
-      for (int k = 0; k < 3; k++) {
-        const int c = k ? 512 : 256, half = c / 2;
-        uint16_t L = hasL ? (uint16_t)plane_val(vL, k) : (uint16_t)half;
-        uint16_t T = hasT ? (uint16_t)plane_val(vT, k) : (uint16_t)half;
-        uint16_t TL = (hasL && hasT) ? (uint16_t)plane_val(vTL, k) : (uint16_t)half;
-        uint16_t p = med16(T, L, (uint16_t)(T + L - TL));
-        uint32_t r = ((int)plane_val(v, k) - (int)p + half + c) & (c - 1);
-        res[k][q] = (uint16_t)r;
-        if (!(j.dbg & 2)) atomicAdd(&hist[k][r], 1u);
+      const uint32_t bL = B(1), bT = B(w), bTL = B(w + 1);     // unconditional reads, then select
+      const uint32_t vL = hasL ? bL : 0x808080u;
+      const uint32_t vT = hasT ? bT : 0x808080u;
+      const uint32_t vTL = (hasL && hasT) ? bTL : 0x808080u;
+      // G: median of (T, L, (uint16)(T + L - TL))
+      const uint32_t gL = (vL >> 8) & 255u, gT = (vT >> 8) & 255u, gTL = (vTL >> 8) & 255u;
+      const uint32_t gg = (gT + gL - gTL) & 0xffffu;
+      const uint32_t pg = max(min(gT, gL), min(max(gT, gL), gg));
+      const uint32_t rg = (g - pg + 128u) & 255u;
+      // R', B' packed: the same median per 16-bit lane
+      const us2 tt = as_us2(rb_form(vT)), ll = as_us2(rb_form(vL)), tl = as_us2(rb_form(vTL));
+      const us2 gr = tt + ll - tl;
+      const us2 mn = __builtin_elementwise_min(tt, ll), mx = __builtin_elementwise_max(tt, ll);
+      const us2 pr = __builtin_elementwise_max(mn, __builtin_elementwise_min(mx, gr));
+      const uint32_t rrb = as_u32(as_us2(rb_form(v)) - pr + (us2)(256)) & 0x01ff01ffu;
+      const uint32_t rr = rrb & 0xffffu, rb = rrb >> 16;
+      res0[q] = (uint16_t)rg;
+      res1[q] = (uint16_t)rr;
+      res2[q] = (uint16_t)rb;
+      if (!(j.dbg & 2)) {
+        atomicAdd(&hist[0][rg], 1u);
+        atomicAdd(&hist[1][rr], 1u);
+        atomicAdd(&hist[2][rb], 1u);
       }
     }
     cx += NT;
-    while (cx >= (uint32_t)w) { cx -= w; cy++; }
-    // LZ screen (wave-private): windows at q and at q - 64
+    if (wide_rows) {
+      const bool wr = cx >= (uint32_t)w;
+      cx -= wr ? w : 0;
+      cy += wr ? 1 : 0;
+    } else {
+      while (cx >= (uint32_t)w) { cx -= w; cy++; }
+    }
+    if (!lz) return;
+    // LZ screen: this position's window, then (after the barrier) the window 64 back
     const bool win = q + 3 < npix;                 // a 4-pixel window starts here
-    const uint32_t hq = win ? fp32(v, fwd[1], fwd[2], fwd[3]) : 0u;
-    const bool winp = q >= 64 && q - 61 < npix;    // window at q - 64 lies in the tile
-    const uint32_t hp = winp ? fp32(bwd[-64], bwd[-63], bwd[-62], bwd[-61]) : 0u;
+    const uint32_t v1 = win ? F(1) : 0, v2 = win ? F(2) : 0, v3 = win ? F(3) : 0;
+    const uint32_t hq = win ? fp32(v, v1, v2, v3) : 0u;
+    // the window 64 back is another wave's: recomputing its fingerprint beats a second barrier
+    const bool winp = q >= 64 && q - 61 < npix;
+    const uint32_t hp = winp ? fp32(B(64), B(63), B(62), B(61)) : 0u;
     uint32_t* key = wkey[wv];
     uint32_t* dup = wdup[wv];
     uint32_t sq = WTAB, sp = WTAB;
-    if (!(j.dbg & 4) && j.speed == 0) {         // -s>=1: k_lzcand screens a longer window
-      if (hq) sq = wt_insert(key, dup, hq);
-      if (hp) sp = wt_insert(key, dup, hp);
-    }
+    if (hq) sq = wt_insert(key, dup, hq);
+    if (hp) sp = wt_insert(key, dup, hp);
     const bool hit = hq && sq < WTAB && ((dup[sq >> 5] >> (sq & 31)) & 1);
     const uint64_t flag = __ballot(hit);
     uint64_t word = 0;
@@ -166,18 +252,22 @@ __global__ __launch_bounds__(NT) void k_front(EncodeJob j) {
       bool c = false;
       if (hit) {
         const uint32_t bmax = q < 64 ? q : 64;
-        const uint32_t v1 = fwd[1], v2 = fwd[2], v3 = fwd[3];
         for (uint32_t b = 1; b <= bmax && !c; b++)
-          c = bwd[-(int)b] == v && bwd[1 - (int)b] == v1 && bwd[2 - (int)b] == v2 && bwd[3 - (int)b] == v3;
+          c = B(b) == v && B(b - 1) == v1 && B(b - 2) == v2 && B(b - 3) == v3;
       }
       word = __ballot(c);
     }
     // clear the slots this wave used (wave-ordered LDS: the reads above are done)
-    if (sq < WTAB) key[sq] = 0;
-    if (sp < WTAB) key[sp] = 0;
+    key[sq] = 0;                                    // slot WTAB is a spare: no branch
+    key[sp] = 0;
     if (lane < WTAB / 32) dup[lane] = 0;
     if (lane == 0 && (q >> 6) < (npix + 63) / 64) cand[q >> 6] = word;
     ncand += lane == 0 ? __popcll(word) : 0;
+  };
+  for (uint32_t blk = 0; blk < nblk; blk += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; u++)
+      if (blk + u < nblk) body(blk + u, nv[(u + 1) % PF]);
   }
   if (notgrey) atomicOr(&s_notgrey, 1);
   if (ncand) atomicAdd(&s_ncand, ncand);
@@ -188,10 +278,10 @@ __global__ __launch_bounds__(NT) void k_front(EncodeJob j) {
   }
   if (s_ncol <= 256 && s_notgrey) {
     // palette in first-occurrence order (choh.cpp:64-88): rank of a colour = number of colours
-    // whose first position is smaller (the ring is free now)
-    uint32_t* pc = ring;
-    uint32_t* pp = ring + 256;
-    for (int i = tid; i < 1024; i += NT) {
+    // whose first position is smaller
+    uint32_t* pc = &wkey[0][0];
+    uint32_t* pp = &wkey[0][0] + 256;
+    for (int i = tid; i < CSET; i += NT) {
       if (hset[i] != 0xffffffffu) {
         const int k = atomicAdd(&s_np, 1);
         pc[k] = hset[i];
@@ -224,6 +314,13 @@ __global__ __launch_bounds__(NT) void k_front(EncodeJob j) {
     j.tiles[t] = ti;
   }
 }
+
+__global__ __launch_bounds__(NT) void k_front(EncodeJob j) {
+  __shared__ uint32_t ring[2 * RING];
+  front_tile<true>(j, ring);
+}
+
+__global__ __launch_bounds__(NT) void k_front_wide(EncodeJob j) { front_tile<false>(j, nullptr); }
 
 // Indexed plane of a palette-candidate tile (choh.cpp:48-102 palette_encode + layer_encode -s0):
 // index = first-occurrence rank of the pixel's colour, then the MED fast-path residual at depth 8
@@ -290,5 +387,6 @@ void launch_palette(const EncodeJob& j, hipStream_t s) {
 }
 
 void launch_front(const EncodeJob& j, hipStream_t s) {
-  hipLaunchKernelGGL(k_front, dim3(j.ntiles), dim3(NT), 0, s, j);
+  if (j.tw <= RING_MAX_W) hipLaunchKernelGGL(k_front, dim3(j.ntiles), dim3(NT), 0, s, j);
+  else hipLaunchKernelGGL(k_front_wide, dim3(j.ntiles), dim3(NT), 0, s, j);
 }

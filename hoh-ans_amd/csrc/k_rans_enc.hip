@@ -1,19 +1,22 @@
 // rANS encoders (rans64.hpp:65-103, :262-278; entropy_encoding.hpp:206-238).
 //
 // Bit-exactness forces one serial coder state per stream (the reference never interleaves), so
-// the encoder is a latency-bound chain of 65,536 dependent steps per 256x256 tile plane.  The
-// fast kernel therefore spends all its effort on the length of that chain:
+// the encoder is a chain of 65,536 dependent steps per 256x256 tile plane, and one wave issues
+// one instruction every ~6 cycles: the chain's length is its instruction count.  The fast
+// kernel therefore spends all its effort on instructions per step:
 //  * one stream per lane, RF_LANES streams per wave; the symbol tables (16-B entries: 1/f as
 //    f64, f, c) are gathered from global memory (L2-resident, ~8 KB per stream) one 8-symbol
-//    block ahead, so the kernel needs only its 8-KB output window in LDS and leaves the CUs
-//    free for concurrent work;
+//    block ahead through 32-bit offsets from one scalar base (two symbol offsets per packed
+//    16-bit shift);
 //  * the quotient floor(x/f) of the reciprocal step is computed exactly with two f64
 //    multiplications by 1/f rounded up two ulps (the high word first, then remainder*2^32 +
 //    low word, both < 2^53: exact floors), which is mathematically identical to the Alverson
 //    reciprocal of Rans64EncPutSymbol; the new low word is x_lo + c + ql*(2^15 - f);
-//  * symbols are prefetched two 8-symbol blocks ahead and table entries one block ahead;
-//  * each step writes its speculative output word to an LDS window and records the renorm
-//    decision in a bit mask; once per 32 steps only the emitted words are copied to the slab.
+//  * each step writes its speculative output word to an LDS window and adds the renorm decision
+//    to a bit mask (one add-with-carry); once per 32 steps only the emitted words are copied to
+//    the slab.  (Storing every speculative word straight to the slab at the next output slot
+//    removes the mask and the flush loop but costs a scattered 64-lane store per step: measured
+//    40% slower.)
 // The generic kernel (LZ streams, other prob_bits) is the reference reciprocal step verbatim.
 // Both record decode checkpoints every HOH_SEG symbols (Recoil-style side index; the .hoh bytes
 // are unaffected).
@@ -23,6 +26,7 @@
 #include <atomic>
 
 #define WIN 32
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 
 // plane index -> stream: [0, na) through map a, then map b (e.g. the sub-green planes of every
 // tile first, the rarely present indexed planes after them, so idle lanes share few waves)
@@ -30,10 +34,27 @@ __device__ __forceinline__ uint32_t plane_sid(int pi, int spt, SidMap a, int na,
   return pi < na ? map_sid(a, spt, pi) : map_sid(b, spt, pi - na);
 }
 
-__device__ __forceinline__ void lookup8(EncFast* e, uint4 sy, const EncFast* tab) {
-  const uint32_t w[4] = {sy.x, sy.y, sy.z, sy.w};
+// byte offsets (from the table base) of the entries of 8 packed u16 symbols
+__device__ __forceinline__ void offs8(uint32_t* o, uint4 w, uint32_t base) {
+  const uint32_t d[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
-  for (int k = 0; k < 8; ++k) e[k] = tab[(k & 1) ? (w[k >> 1] >> 16) : (w[k >> 1] & 0xffffu)];
+  for (int k = 0; k < 4; k++) {
+    const uint32_t t = __builtin_bit_cast(uint32_t, __builtin_bit_cast(us2, d[k]) << (us2)(4));
+    uint32_t lo;
+    asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:DWORD"
+        : "=v"(lo) : "v"(t), "v"(base));        // base + low half: one instruction
+    o[2 * k] = lo;
+    o[2 * k + 1] = base + (t >> 16);
+  }
+}
+
+__device__ __forceinline__ EncFast ent(const char* tb, uint32_t off) { return *(const EncFast*)(tb + off); }
+
+__device__ __forceinline__ void lookup8(EncFast* e, uint4 sy, const char* tb, uint32_t base) {
+  uint32_t o[8];
+  offs8(o, sy, base);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) e[k] = ent(tb, o[k]);
 }
 
 struct Coder {
@@ -43,6 +64,7 @@ struct Coder {
   uint32_t* win;
 };
 
+// copy the window's emitted words to the slab (backwards, rans64 order)
 __device__ __forceinline__ void flush_win(Coder& c) {
   uint32_t m = c.mask;
   const uint32_t shift = WIN - c.slot;
@@ -55,13 +77,21 @@ __device__ __forceinline__ void flush_win(Coder& c) {
   c.slot = 0;
 }
 
-// one step, prob_bits 15 (x_max = f << 48)
+// one step, prob_bits 15 (x_max = f << 48): the low word goes to the LDS window speculatively,
+// the renormalisation decision into the mask
 __device__ __forceinline__ void step15(Coder& c, const EncFast& e) {
   c.win[c.slot] = c.xl;
   const uint32_t f = e.f;
-  const bool emit = (c.xh >> 16) >= f;
-  const uint32_t nh = emit ? 0u : c.xh;
-  const uint32_t nl = emit ? c.xh : c.xl;
+  // emit = x >= x_max, i.e. (x_hi >> 16) >= f; (nh, nl) = emit ? (0, x_hi) : (x_hi, x_lo); the
+  // decision is shifted into the mask by an add-with-carry of the compare itself: 4 instructions
+  uint32_t nh, nl;
+  asm("v_cmp_ge_u32_sdwa vcc, %[xh], %[f] src0_sel:WORD_1 src1_sel:DWORD\n\t"
+      "v_cndmask_b32_e64 %[nh], %[xh], 0, vcc\n\t"
+      "v_cndmask_b32_e32 %[nl], %[xl], %[xh], vcc\n\t"
+      "v_addc_co_u32_e32 %[m], vcc, %[m], %[m], vcc"
+      : [nh] "=&v"(nh), [nl] "=&v"(nl), [m] "+v"(c.mask)
+      : [xh] "v"(c.xh), [xl] "v"(c.xl), [f] "v"(f)
+      : "vcc");
   // all intermediate values are integers < 2^53, so every f64 operation below is exact; the
   // remainder stays in f64 (no int round trip on the dependent chain)
   const double nhd = (double)nh;
@@ -72,7 +102,6 @@ __device__ __forceinline__ void step15(Coder& c, const EncFast& e) {
   const uint32_t qh = (uint32_t)qhd;
   c.xl = nl + e.c + ql * (32768u - f);
   c.xh = __builtin_amdgcn_alignbit(qh, ql, 17);
-  c.mask = (c.mask << 1) | (emit ? 1u : 0u);
   c.slot++;
 }
 
@@ -102,7 +131,8 @@ __global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane, SidMa
   StreamInfo st = j.streams[sid];
   if (!st.fast || st.mode != SM_RANS || st.err || st.n == 0) return;
   const uint32_t n = st.n;
-  const EncFast* tab = j.tab_fast + (size_t)sid * HOH_FAST_RANGE;
+  const char* tb = (const char*)j.tab_fast;
+  const uint32_t tbase = sid * (uint32_t)(HOH_FAST_RANGE * sizeof(EncFast));
   Coder c;
   c.xh = 0; c.xl = 1u << 31; c.mask = 0; c.slot = 0;
   c.slab = j.slabs + st.slab_off;
@@ -112,11 +142,7 @@ __global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane, SidMa
   const uint16_t* sp = j.sym + st.sym_off;
   // prologue: the top n % 32 symbols one at a time (descending); the rest is whole windows
   const uint32_t r = n & 31, nb = (n - r) / 8;   // nb 8-symbol blocks, a multiple of 4
-  for (uint32_t i = n; i > n - r; i--) {
-    const uint32_t s = sp[i - 1];
-    const EncFast e = tab[s];
-    step15(c, e);
-  }
+  for (uint32_t i = n; i > n - r; i--) step15(c, ent(tb, tbase + (uint32_t)sp[i - 1] * 16u));
   flush_win(c);
   if (((nb * 8) % HOH_SEG) == 0 && nb * 8 < n) ckpt(c, ck, nb * 8 / HOH_SEG);
   if (nb) {
@@ -124,25 +150,25 @@ __global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane, SidMa
     EncFast eA[8], eB[8];
     uint4 s1 = sp4[nb - 2];
     uint4 s0 = sp4[nb - 3];
-    lookup8(eA, sp4[nb - 1], tab);
+    lookup8(eA, sp4[nb - 1], tb, tbase);
     for (int b = (int)nb - 1; b >= 3; b -= 4) {
       // entering: eA = entries of block b, s1 = symbols of b-1, s0 = symbols of b-2
-      lookup8(eB, s1, tab);
+      lookup8(eB, s1, tb, tbase);
       if (b - 3 >= 0) s1 = sp4[b - 3];
 #pragma unroll
       for (int k = 7; k >= 0; --k) step15(c, eA[k]);
       if ((b & (HOH_SEG / 8 - 1)) == 0) ckpt(c, ck, (uint32_t)b * 8 / HOH_SEG);
-      lookup8(eA, s0, tab);
+      lookup8(eA, s0, tb, tbase);
       if (b - 4 >= 0) s0 = sp4[b - 4];
 #pragma unroll
       for (int k = 7; k >= 0; --k) step15(c, eB[k]);
       if (((b - 1) & (HOH_SEG / 8 - 1)) == 0) ckpt(c, ck, (uint32_t)(b - 1) * 8 / HOH_SEG);
-      lookup8(eB, s1, tab);
+      lookup8(eB, s1, tb, tbase);
       if (b - 5 >= 0) s1 = sp4[b - 5];
 #pragma unroll
       for (int k = 7; k >= 0; --k) step15(c, eA[k]);
       if (((b - 2) & (HOH_SEG / 8 - 1)) == 0) ckpt(c, ck, (uint32_t)(b - 2) * 8 / HOH_SEG);
-      if (b - 4 >= 0) lookup8(eA, s0, tab);
+      if (b - 4 >= 0) lookup8(eA, s0, tb, tbase);
       if (b - 6 >= 0) s0 = sp4[b - 6];
 #pragma unroll
       for (int k = 7; k >= 0; --k) step15(c, eB[k]);
@@ -206,6 +232,11 @@ void launch_rans_fast(const EncodeJob& j, int nplane, hipStream_t s, SidMap a, i
   const int nblk = (nplane + lanes - 1) / lanes;
   const int grid = nblk >= 1024 || (j.dbg & 0x100000) ? nblk : 1024;
   const int rot = grid == nblk ? 0 : (int)((g_rot.fetch_add(1) * 8u * (unsigned)((nblk + 7) / 8)) % (unsigned)grid);
+  // The chain is issue-bound, so two chains on one SIMD run at half speed, and a launch ends
+  // with its slowest chain.  Asking for 56 KB of LDS (8 KB are used) caps the chains at
+  // two per CU (one per SIMD in practice) when several images are in flight.  dbg bits 24..31
+  // override the size in KB (measurement).
+  const size_t pad = (j.dbg >> 24) ? (size_t)((j.dbg >> 24) & 255) * 1024 : (size_t)56 * 1024;
   if (lanes == 16) {
     hipLaunchKernelGGL(k_rans_fast<16>, dim3(grid), dim3(64), 16 * WIN * 4, s, j, nplane, a, na, b, nblk, rot);
   } else if (lanes == 32) {
@@ -213,13 +244,7 @@ void launch_rans_fast(const EncodeJob& j, int nplane, hipStream_t s, SidMap a, i
   } else if (lanes == 8) {
     hipLaunchKernelGGL(k_rans_fast<8>, dim3(grid), dim3(64), 8 * WIN * 4, s, j, nplane, a, na, b, nblk, rot);
   } else {
-    // The chain is issue-bound, so two chains on one SIMD run at half speed, and a launch ends
-    // with its slowest chain.  Asking for 56 KB of LDS (only 8 KB are used) caps the chains at
-    // two per CU (one per SIMD in practice) when several images are in flight: +15% encode
-    // throughput at 8 in flight.  dbg bits 24..31 override the size in KB (measurement).
-    const size_t pad = (j.dbg >> 24) ? (size_t)((j.dbg >> 24) & 255) * 1024 : (size_t)56 * 1024;
-    hipLaunchKernelGGL(k_rans_fast<64>, dim3(grid), dim3(64), std::max<size_t>(64 * WIN * 4, pad), s, j, nplane, a, na, b,
-                       nblk, rot);
+    hipLaunchKernelGGL(k_rans_fast<64>, dim3(grid), dim3(64), std::max<size_t>(64 * WIN * 4, pad), s, j, nplane, a, na, b, nblk, rot);
   }
 }
 

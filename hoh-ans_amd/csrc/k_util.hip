@@ -31,3 +31,50 @@ void launch_synth(uint8_t* rgb, int W, int H, int y0, uint64_t seed, int noise, 
   const uint64_t salt = seed * 0x100000001B3ull;
   hipLaunchKernelGGL(k_synth, dim3(4096), dim3(256), 0, s, rgb, W, H, y0, salt, noise);
 }
+
+// ---- enqueue-only API support (hoh_*_async): results are written by the stream, not read back
+
+// up to 16 bytes from kernel arguments into device memory (the .hoh header of an async encode)
+__global__ void k_put_bytes(uint8_t* dst, uint64_t lo, uint64_t hi, int n) {
+  const int i = threadIdx.x;
+  if (i < n) dst[i] = (uint8_t)((i < 8 ? lo >> (8 * i) : hi >> (8 * (i - 8))) & 255);
+}
+
+// encoder status word -> {HOH status code, file bytes}: the mapping of encode_tiles_impl's
+// host epilogue (hoh_api.cpp), evaluated on the device
+__global__ void k_status_enc(const uint32_t* gerr, const uint64_t* total, uint64_t cap, uint64_t* out) {
+  if (threadIdx.x) return;
+  const uint32_t g = gerr[0];
+  const uint64_t t = total[0];
+  uint64_t code = 0;
+  if (g) {
+    const uint32_t tf = g >> 8;
+    code = (tf & TF_UNREPRODUCIBLE) ? 5 : (tf & TF_UNSUPPORTED) ? 6 : (g & 2) ? 4 : 3;
+  } else if (t > cap) {
+    code = 2;
+  }
+  out[0] = code;
+  out[1] = t;
+}
+
+// decoder error word -> {HOH status code, decoded bytes} (decode_run's epilogue)
+__global__ void k_status_dec(const uint32_t* gerr, uint64_t bytes, uint64_t* out) {
+  if (threadIdx.x) return;
+  const uint32_t g = gerr[0];
+  out[0] = g ? ((g & 2) ? 6 : 7) : 0;
+  out[1] = g ? 0 : bytes;
+}
+
+void launch_put_bytes(uint8_t* dst, const uint8_t* b, int n, hipStream_t s) {
+  uint64_t w[2] = {0, 0};
+  for (int i = 0; i < n && i < 16; i++) w[i / 8] |= (uint64_t)b[i] << (8 * (i % 8));
+  hipLaunchKernelGGL(k_put_bytes, dim3(1), dim3(64), 0, s, dst, w[0], w[1], n);
+}
+
+void launch_status_enc(const uint32_t* gerr, const uint64_t* total, uint64_t cap, uint64_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_status_enc, dim3(1), dim3(64), 0, s, gerr, total, cap, out);
+}
+
+void launch_status_dec(const uint32_t* gerr, uint64_t bytes, uint64_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_status_dec, dim3(1), dim3(64), 0, s, gerr, bytes, out);
+}

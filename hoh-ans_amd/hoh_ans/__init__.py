@@ -82,6 +82,8 @@ def lib():
         for name, args in (
             ("hoh_decode_image", [vp, vp, sz, vp, sz, ip, ip, vp]),
             ("hoh_decode_image_ix", [vp, vp, sz, vp, sz, ip, ip, vp, vp]),
+            ("hoh_encode_image_async", [vp, vp, C.c_int, C.c_int, C.c_int, vp, sz, vp, vp, vp]),
+            ("hoh_decode_image_async", [vp, vp, sz, C.c_int, C.c_int, vp, sz, vp, vp, vp]),
             ("hoh_encode_entropy", [vp, vp, sz, sz, C.c_uint32, vp, sz, szp]),
             ("hoh_decode_entropy", [vp, vp, sz, szp, vp, sz, szp]),
             ("hoh_entropy_count", [vp, sz, sz, szp]),
@@ -223,6 +225,37 @@ def decode_image(hoh_dev, size, out_dev=None, ctx=None, index=None):
                                   index.h if index is not None else None, _stream_ptr(torch))
     check(r, "hoh_decode_image")
     return out_dev, w.value, h.value
+
+
+def encode_image_async(rgb_dev, W, H, out_dev, status_dev, ctx=None, index=None, speed=0):
+    """Enqueue-only encode on the current stream (no host wait).  status_dev: int64 tensor of 2
+    (device) receiving {HOH status code, .hoh size}; read it after synchronising the stream and
+    pass it to check_status."""
+    import torch
+    ctx = ctx or default_ctx()
+    r = lib().hoh_encode_image_async(ctx.h, vp(rgb_dev.data_ptr()), W, H, speed, vp(out_dev.data_ptr()),
+                                     out_dev.numel(), index.h if index is not None else None,
+                                     vp(status_dev.data_ptr()), _stream_ptr(torch))
+    check(r, "hoh_encode_image_async")
+
+
+def decode_image_async(hoh_dev, size, W, H, out_dev, status_dev, ctx=None, index=None):
+    """Enqueue-only decode of a W x H .hoh (at most `size` bytes are read; a bound suffices) on
+    the current stream.  status_dev receives {HOH status code, W*H*3}."""
+    import torch
+    ctx = ctx or default_ctx()
+    r = lib().hoh_decode_image_async(ctx.h, vp(hoh_dev.data_ptr()), size, W, H, vp(out_dev.data_ptr()),
+                                     out_dev.numel(), index.h if index is not None else None,
+                                     vp(status_dev.data_ptr()), _stream_ptr(torch))
+    check(r, "hoh_decode_image_async")
+
+
+def check_status(status, what):
+    """status: the two u64 an async call wrote (any sequence); raises HohError on failure and
+    returns the size word."""
+    code, size = int(status[0]), int(status[1])
+    check(code, what)
+    return size
 
 
 def encode_tiles(rgb_dev, W, H, t0, ntiles, out_dev, sizes_dev, ctx=None, index=None, row0=0, speed=0):

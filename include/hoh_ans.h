@@ -88,6 +88,23 @@ int hoh_decode_image(hoh_ctx* ctx, const uint8_t* d_hoh, size_t size, uint8_t* d
 int hoh_decode_image_ix(hoh_ctx* ctx, const uint8_t* d_hoh, size_t size, uint8_t* d_rgb, size_t cap,
                         int* W, int* H, const hoh_index* idx, void* stream);
 
+/* ---- enqueue-only image path (no host synchronisation) ----------------------------------
+ * The work of hoh_encode_image_ix / hoh_decode_image_ix for tiled images, enqueued on `stream`
+ * with no host round trip, so one host thread keeps many images in flight on many streams (the
+ * reference's choh/dhoh loop over files, choh.cpp:464-500 / dhoh.cpp:297-396, without the
+ * per-file wait).  Results are written by the stream to d_status (device or pinned host memory,
+ * two u64): d_status[0] = HOH_OK or an HOH_E_* code, d_status[1] = the .hoh size (encode) or
+ * W*H*3 (decode).  Read it after synchronising the stream.  Calls on one stream run in order, so
+ * a context's workspaces, the index and the caller's buffers may be reused by the next call on
+ * the same stream.  The decoder takes W and H from the caller (the file header is checked on the
+ * device: a mismatch gives HOH_E_CORRUPT) and reads at most `size` bytes (a bound suffices, e.g.
+ * the encoder's cap).  Header-only (untiled) images return HOH_E_UNSUPPORTED here:
+ * use the synchronous calls. */
+int hoh_encode_image_async(hoh_ctx* ctx, const uint8_t* d_rgb, int W, int H, int speed, uint8_t* d_out,
+                           size_t cap, hoh_index* idx, uint64_t* d_status, void* stream);
+int hoh_decode_image_async(hoh_ctx* ctx, const uint8_t* d_hoh, size_t size, int W, int H, uint8_t* d_rgb,
+                           size_t cap, const hoh_index* idx, uint64_t* d_status, void* stream);
+
 /* Host-side header parse: W, H and tiling of a .hoh (dhoh.cpp:320-366). */
 int hoh_peek_header(const uint8_t* hoh, size_t size, int* W, int* H, int* x_tiles, int* y_tiles);
 

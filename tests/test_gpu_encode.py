@@ -32,6 +32,14 @@ def cases():
     out.append(("uniform", rs.randint(0, 256, (512, 768, 3)).astype(np.uint8)))   # stored planes
     out.append(("tiny2x2", np.array([[[255, 0, 0], [0, 255, 0]], [[255, 255, 0], [0, 0, 255]]], np.uint8)))
     out.append(("untiled300x200", synth_rgb(300, 200, 10, 4)))
+    # untiled and wider than k_front's pixel ring (neighbours read from memory); 1100 just fits it
+    out.append(("untiled2000x100", synth_rgb(2000, 100, 13, 4)))
+    out.append(("untiled1100x150", synth_rgb(1100, 150, 14, 3)))
+    img = synth_rgb(1500, 120, 15, 2)
+    for _ in range(100):
+        y, x, L, b = rs.randint(0, 120), rs.randint(70, 1400), rs.randint(4, 60), rs.randint(1, 65)
+        img[y, x:x + L] = img[y, x - b:x - b + L]
+    out.append(("untiled1500x120-repeats", img))
     out += palette_cases()
     return out
 

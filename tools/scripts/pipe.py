@@ -40,11 +40,26 @@ class Lane:
 
 
 lanes = [Lane() for _ in range(D)]
+ASYNC = os.environ.get("PIPE_ASYNC", "1") == "1"
+status = torch.zeros(4, dtype=torch.int64, device="cuda")
+
+
+def go_async(total):
+    # enqueue-only from one thread (statuses ignored: the knobs may break the output)
+    for i in range(total):
+        ln = lanes[i % D]
+        with torch.cuda.stream(ln.s):
+            if mode in ("enc", "both"):
+                hoh_ans.encode_image_async(rgb, W, H, ln.out, status[0:2], ctx=ln.ctx, index=ln.ix)
+            if mode in ("dec", "both"):
+                hoh_ans.decode_image_async(ln.out, ln.out.numel(), W, H, ln.dec, status[2:4], ctx=ln.ctx, index=ln.ix)
 os.environ["HOH_ENC_DBG"] = encdbg
 os.environ["HOH_DEC_DBG"] = decdbg
 
 
 def go(total):
+    if ASYNC:
+        return go_async(total)
     th = [threading.Thread(target=ln.run, args=(total // D,)) for ln in lanes]
     [x.start() for x in th]
     [x.join() for x in th]

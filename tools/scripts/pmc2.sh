@@ -1,0 +1,6 @@
+#!/bin/bash
+# two PMC passes (instruction mix; LDS/wait detail) over knobs.py KERNEL 0
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_BRANCH SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_SMEM --output-format csv -d gpurun_out/pmcA -o p -- python3 tools/scripts/knobs.py $1 0 > gpurun_out/pmcA.log 2>&1 &&
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES --output-format csv -d gpurun_out/pmcB -o p -- python3 tools/scripts/knobs.py $1 0 > gpurun_out/pmcB.log 2>&1
