@@ -26,33 +26,44 @@ def shard(W, H, rank, world):
     return r0 * xt, (r1 - r0) * xt, r0 * th, min(H, r1 * th)
 
 
-def gather_sizes(tile_sizes, device, group=None):
-    """All-gather every rank's per-tile sizes (variable count) -> list of np.uint32 arrays."""
+def shard_counts(W, H, world):
+    """Tile count of every rank's shard (known to all ranks without an exchange)."""
+    return [shard(W, H, r, world)[1] for r in range(world)]
+
+
+def gather_sizes(tile_sizes, device, group=None, counts=None):
+    """All-gather every rank's per-tile sizes -> list of np.uint32 arrays.  With `counts` (each
+    rank's tile count, e.g. shard_counts) one all_gather suffices; otherwise the counts are
+    exchanged first."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     ts = np.asarray(tile_sizes, dtype=np.int64)
-    n = torch.tensor([ts.size], dtype=torch.int64, device=device)
-    ns = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(ns, n, group=group)
-    ns = [int(x.item()) for x in ns]
-    m = max(ns)
+    if counts is None:
+        n = torch.tensor([ts.size], dtype=torch.int64, device=device)
+        ns = [torch.zeros_like(n) for _ in range(world)]
+        dist.all_gather(ns, n, group=group)
+        counts = [int(x.item()) for x in ns]
+    m = max(counts)
     buf = torch.zeros(m, dtype=torch.int64, device=device)
     buf[:ts.size] = torch.from_numpy(ts).to(device)
     bufs = [torch.zeros_like(buf) for _ in range(world)]
     dist.all_gather(bufs, buf, group=group)
-    return [b[:k].cpu().numpy().astype(np.uint32) for b, k in zip(bufs, ns)]
+    return [b[:k].cpu().numpy().astype(np.uint32) for b, k in zip(bufs, counts)]
 
 
 class FileGather:
-    """Gathers the ranks' tile blobs to rank 0 and assembles the .hoh there.
+    """Brings the ranks' tile blobs to rank 0 and assembles the .hoh there.
 
-    blob: uint8 tensor on this rank's device (capacity >= the largest rank's blob), size: bytes
-    used.  Workspaces are kept across calls (the bench calls it every step)."""
+    One all_gather of the per-tile sizes (every rank's tile count follows from the sharding),
+    then each rank r > 0 sends exactly its blob to rank 0, which receives it straight into its
+    place in the file buffer (after the header + tile table, hoh_file_prefix, and the blobs of
+    ranks < r): no padding to the largest shard and no assembly copy.  blob: uint8 tensor on
+    this rank's device, size: bytes used.  Workspaces are kept across calls (the bench calls it
+    every step).  Returns (file tensor, total bytes) on rank 0, (None, 0) elsewhere."""
 
     def __init__(self, W, H, device, group=None):
         self.W, self.H, self.device, self.group = W, H, device, group
-        self.slots = None
         self.file = None
 
     def __call__(self, blob, size, tile_sizes):
@@ -60,28 +71,28 @@ class FileGather:
         import torch.distributed as dist
         rank = dist.get_rank(self.group)
         world = dist.get_world_size(self.group)
-        sizes = gather_sizes(tile_sizes, self.device, self.group)
+        counts = shard_counts(self.W, self.H, world)
+        if len(tile_sizes) != counts[rank]:
+            raise RuntimeError("rank %d holds %d tile sizes, its shard has %d tiles" % (rank, len(tile_sizes), counts[rank]))
+        sizes = gather_sizes(tile_sizes, self.device, self.group, counts)
         blob_sizes = [int(s.sum(dtype=np.int64)) for s in sizes]
         if blob_sizes[rank] != size:
             raise RuntimeError("tile sizes do not add up to the blob size")
-        m = max(blob_sizes)
-        if blob.numel() < m:
-            raise RuntimeError("blob capacity %d < largest shard %d" % (blob.numel(), m))
-        if rank == 0:
-            if self.slots is None or self.slots[0].numel() < m:
-                self.slots = [torch.empty(m, dtype=torch.uint8, device=self.device) for _ in range(world)]
-            dist.gather(blob[:m], [s[:m] for s in self.slots], dst=0, group=self.group)
-        else:
-            dist.gather(blob[:m], None, dst=0, group=self.group)
+        ranks = dist.get_process_group_ranks(self.group) if self.group is not None else list(range(world))
+        if rank != 0:
+            if size:
+                dist.batch_isend_irecv([dist.P2POp(dist.isend, blob[:size], ranks[0], self.group)])[0].wait()
             return None, 0
-        all_sizes = np.concatenate(sizes)
-        prefix = file_prefix(self.W, self.H, all_sizes)
+        prefix = file_prefix(self.W, self.H, np.concatenate(sizes))
         total = len(prefix) + sum(blob_sizes)
         if self.file is None or self.file.numel() < total:
             self.file = torch.empty(total, dtype=torch.uint8, device=self.device)
         self.file[:len(prefix)] = torch.frombuffer(bytearray(prefix), dtype=torch.uint8).to(self.device)
-        off = len(prefix)
-        for r in range(world):
-            self.file[off:off + blob_sizes[r]] = self.slots[r][:blob_sizes[r]]
-            off += blob_sizes[r]
+        offs = np.cumsum([len(prefix)] + blob_sizes)
+        ops = [dist.P2POp(dist.irecv, self.file[offs[r]:offs[r] + blob_sizes[r]], ranks[r], self.group)
+               for r in range(1, world) if blob_sizes[r]]
+        reqs = dist.batch_isend_irecv(ops) if ops else []
+        self.file[offs[0]:offs[0] + blob_sizes[0]] = blob[:blob_sizes[0]]
+        for q in reqs:
+            q.wait()
         return self.file, total
