@@ -352,7 +352,6 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   if ((e = ensure(c->tab_fast, S * HOH_FAST_RANGE * sizeof(EncFast)))) return e;
   if ((e = ensure(c->tab_gen, S * 512 * sizeof(EncGen)))) return e;
   if ((e = ensure(c->slabs, nslab * 4))) return e;
-  if ((e = ensure(c->ckpt, nck * sizeof(Checkpoint)))) return e;
   if ((e = ensure(c->misc, 64))) return e;
   j.sym = (uint16_t*)c->sym.p;
   j.hist = (uint32_t*)c->hist.p;
@@ -366,7 +365,13 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   j.tab_gen = (EncGen*)c->tab_gen.p;
   j.slabs = (uint32_t*)c->slabs.p;
   j.slab_words = nslab;
-  j.ckpt = speed ? nullptr : (Checkpoint*)c->ckpt.p;      // -s>=1 files get no side index
+  // checkpoints are only kept for a side index, and the encoder writes them straight into it
+  // (its layout is the index's: stream s at s * (npix_cap / HOH_SEG + 2)); -s>=1 files get none
+  j.ckpt = nullptr;
+  if (!speed && idx) {
+    if ((e = index_reserve(idx, S, nck))) return e;
+    j.ckpt = index_ckpt_buf(idx);
+  }
   j.gerr = (uint32_t*)c->misc.p;
   j.total = (uint64_t*)((uint8_t*)c->misc.p + 8);
   j.tile_sizes = d_tile_sizes;
@@ -566,7 +571,6 @@ int encode_streams_impl(hoh_ctx* c, const uint16_t* d_syms, const uint64_t* off,
   if ((e = ensure(c->hdr, (size_t)nstreams * hcap))) return e;
   if ((e = ensure(c->tab_gen, (size_t)nstreams * range * sizeof(EncGen)))) return e;
   if ((e = ensure(c->slabs, (size_t)nstreams * slab * 4))) return e;
-  if ((e = ensure(c->ckpt, (size_t)nstreams * per_ck * sizeof(Checkpoint)))) return e;
   if ((e = ensure(c->misc, 64))) return e;
   std::vector<StreamInfo> st((size_t)nstreams);
   for (int i = 0; i < nstreams; i++) {
@@ -590,7 +594,7 @@ int encode_streams_impl(hoh_ctx* c, const uint16_t* d_syms, const uint64_t* off,
   j.tab_gen = (EncGen*)c->tab_gen.p;
   j.gen_stride = range;
   j.slabs = (uint32_t*)c->slabs.p;
-  j.ckpt = (Checkpoint*)c->ckpt.p;
+  j.ckpt = nullptr;                           // stream-level decodes are serial: no checkpoints
   j.gerr = (uint32_t*)c->misc.p;
   j.total = (uint64_t*)((uint8_t*)c->misc.p + 8);
   j.out = d_out;
@@ -675,15 +679,23 @@ size_t hoh_index_bytes(const hoh_index* idx) {
 }  // extern "C"
 
 // index capture: copy every plane stream's checkpoints + payload location (device to device)
+int index_reserve(hoh_index* idx, size_t nstreams, size_t nck) {
+  int e;
+  if ((e = ensure(idx->streams, nstreams * sizeof(IndexStream)))) return e;
+  return ensure(idx->ck, nck * sizeof(Checkpoint));
+}
+Checkpoint* index_ckpt_buf(hoh_index* idx) { return (Checkpoint*)idx->ck.p; }
+
+// the encoder already wrote the checkpoints into the index (j.ckpt); record where each stream's
+// payload sits in the file
 int index_capture(hoh_index* idx, const EncodeJob& j, hipStream_t s) {
   const int S = j.ntiles * SK_PER_TILE;
   const size_t per = j.npix_cap / HOH_SEG + 2;
   int e;
-  if ((e = ensure(idx->streams, (size_t)S * sizeof(IndexStream)))) return e;
-  if ((e = ensure(idx->ck, (size_t)S * per * sizeof(Checkpoint)))) return e;
+  if ((e = index_reserve(idx, (size_t)S, (size_t)S * per))) return e;
   idx->nstreams = S;
   idx->ck_count = (size_t)S * per;
-  launch_index_capture(j, (IndexStream*)idx->streams.p, (Checkpoint*)idx->ck.p, per, s);
+  launch_index_capture(j, (IndexStream*)idx->streams.p, per, s);
   return hipGetLastError() == hipSuccess ? HOH_OK : HOH_E_HIP;
 }
 

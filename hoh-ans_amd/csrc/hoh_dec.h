@@ -40,7 +40,9 @@ struct DecWork {
 
 void dec_free(DecWork& w);
 int index_capture(hoh_index* idx, const EncodeJob& j, hipStream_t s);
-void launch_index_capture(const EncodeJob& j, IndexStream* is, Checkpoint* ck, size_t per, hipStream_t s);
+int index_reserve(hoh_index* idx, size_t nstreams, size_t nck);
+Checkpoint* index_ckpt_buf(hoh_index* idx);
+void launch_index_capture(const EncodeJob& j, IndexStream* is, size_t per, hipStream_t s);
 const IndexStream* index_streams(const hoh_index* idx);
 const Checkpoint* index_ckpts(const hoh_index* idx);
 int index_nstreams(const hoh_index* idx);

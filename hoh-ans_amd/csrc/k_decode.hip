@@ -38,6 +38,7 @@ struct DecJob {
   uint32_t cum_stride;          // entries per stream in cum (>= range + 1)
   uint32_t* matches;            // [tile][lz_cap+1][4]: pixel index, length, back, nuked before
   int lzband;                   // rows per band of k_dunpred_lz (LDS-bound)
+  uint32_t* lzt;                // tiles with LZ copies (w >= 64), appended by k_dlz; count in gerr[2]
   uint32_t dbg;                 // measurement knobs (HOH_DEC_DBG), 0 in production
   uint64_t* dbgbuf;             // per-workgroup s_memtime stamps when dbg & 16
   uint8_t* rgb;                 // output image
@@ -432,6 +433,15 @@ __device__ bool dec_run(const DecJob& j, const DecStream& d, const uint32_t* cum
 // exact slot -> symbol table (a byte per slot: the symbol's offset from the first symbol of its
 // 32-slot bucket, plus that first symbol per bucket) and the whole payload, so the per-symbol
 // chain is two LDS round trips and no global load; the symbol stores are never awaited.
+__device__ __forceinline__ void dec_stored(const DecJob& j, int sid, const DecStream& d) {
+  uint16_t* out = j.dsym + d.out_off;
+  const uint32_t sw = skew_w(j, sid, d.n);
+  for (uint32_t i = threadIdx.x; i < d.n; i += blockDim.x) {
+    const uint16_t v = (uint16_t)get_bits(j.in, d.payload_off * 8 + (uint64_t)i * d.maxbits, d.maxbits);
+    out[sw ? skew_pos(i % sw, i / sw, sw) : i] = v;
+  }
+}
+
 // Dynamic LDS: cum (514 u32) | bucket symbols (u16) | slot table (u8) | payload words.  Output is
 // the flat plane: each thread stores its segment 8 symbols (16 B) at a time.
 __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams, uint32_t wcap) {
@@ -440,6 +450,7 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams, uint32_t
   const int tid = threadIdx.x;
   const int sid = blockIdx.x;
   const DecStream d = j.streams[sid];
+  if (d.mode == SM_STORED) { dec_stored(j, sid, d); return; }     // no separate launch
   if (d.mode != SM_RANS || d.range > 512) return;
   uint64_t T0 = 0, T1 = 0;
   if (j.dbg & 16) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(T0)::"memory");
@@ -617,18 +628,14 @@ __global__ __launch_bounds__(64) void k_drans_serial(DecJob j, int nstreams) {
     atomicOr(j.gerr, 4u);
 }
 
-// stored streams: MSB-first fixed-width fields
+// stored streams: MSB-first fixed-width fields (the no-index path; with an index k_drans's
+// workgroup of the stream does this itself)
 __global__ void k_dstored(DecJob j, int nstreams) {
   if (dec_abort(j)) return;
   const int sid = blockIdx.x;
   const DecStream d = j.streams[sid];
   if (d.mode != SM_STORED) return;
-  uint16_t* out = j.dsym + d.out_off;
-  const uint32_t sw = skew_w(j, sid, d.n);
-  for (uint32_t i = threadIdx.x; i < d.n; i += blockDim.x) {
-    const uint16_t v = (uint16_t)get_bits(j.in, d.payload_off * 8 + (uint64_t)i * d.maxbits, d.maxbits);
-    out[sw ? skew_pos(i % sw, i / sw, sw) : i] = v;
-  }
+  dec_stored(j, sid, d);
 }
 
 // LZ streams -> matches (un_lz.hpp:150-170); one lane per tile
@@ -663,6 +670,7 @@ __global__ void k_dlz(DecJob j) {
   ti.nmatch = nm;
   if (bad) { ti.err = 1; atomicOr(j.gerr, 1u); }
   j.tiles[t] = ti;
+  if (!bad && nm && ti.w >= 64) j.lzt[atomicAdd(j.gerr + 2, 1u)] = (uint32_t)t;   // k_dunpred_lz's work list
 }
 
 __device__ __forceinline__ uint16_t dmed16(uint16_t a, uint16_t b, uint16_t c) {
@@ -856,16 +864,26 @@ __device__ __forceinline__ uint32_t unpred_px(uint32_t T, uint32_t L, uint32_t T
 // (b) a copy's source pixel is done.  Decoded pixels (packed G/R'/B') live in LDS rows
 // [row above band | band rows]; the band's residuals (a contiguous range, residuals skip
 // copied pixels) are staged in LDS first.  Needs w >= 64 (copies reach at most one row up).
+// A small persistent grid walks the list of LZ tiles k_dlz built (a launch over every tile
+// would dispatch ~1000 idle workgroups that each need the 66 KB band).
+__device__ __forceinline__ void dunpred_lz_tile(const DecJob& j, int t, uint32_t* lz_lds);
+
 __global__ __launch_bounds__(64) void k_dunpred_lz(DecJob j) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lz_lds[];
   if (dec_abort(j)) return;
-  const int t = blockIdx.x;
+  const uint32_t cnt = *(volatile const uint32_t*)(j.gerr + 2);
+  for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+    dunpred_lz_tile(j, (int)j.lzt[i], lz_lds);
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ void dunpred_lz_tile(const DecJob& j, int t, uint32_t* lz_lds) {
   const DecTile ti = j.tiles[t];
   if (ti.err || unpred_fast(j, t, ti) || ti.w < 64) return;
   const int lane = threadIdx.x;
   const int w = ti.w, h = ti.h, BR = j.lzband;
   uint32_t* band = lz_lds;                                   // (BR+1) rows x w
-  uint32_t* rs = lz_lds + (size_t)(BR + 1) * w;              // BR*w packed residuals
   const DecStream* st = j.streams + (size_t)t * SK_PER_TILE + 3;
   const uint32_t* mt = j.matches + (size_t)t * 4 * (j.lz_cap + 1);
   const uint32_t nm = ti.nmatch, npix = (uint32_t)w * h;
@@ -883,8 +901,6 @@ __global__ __launch_bounds__(64) void k_dunpred_lz(DecJob j) {
     const int r1 = min(h, r0 + BR);
     const uint32_t kb0 = (uint32_t)r0 * w - nuked_before(mt, nm, (uint32_t)r0 * w);
     const uint32_t kb1 = (uint32_t)r1 * w - nuked_before(mt, nm, (uint32_t)r1 * w);
-    for (uint32_t e = lane; e < kb1 - kb0; e += 64)
-      rs[e] = resG[kb0 + e] | ((uint32_t)resR[kb0 + e] << 8) | ((uint32_t)resB[kb0 + e] << 17);
     __syncthreads();
     const int y = r0 + lane;
     const bool act = lane < BR && y < h;
@@ -934,7 +950,8 @@ __global__ __launch_bounds__(64) void k_dunpred_lz(DecJob j) {
             const uint32_t L = x == 0 ? PK_HALF : left;
             const uint32_t k = i - nuk;
             uint32_t r = 0;
-            if (k < kb0 || k >= kb1) bad = true; else r = rs[k - kb0];
+            if (k < kb0 || k >= kb1) bad = true;
+            else r = resG[k] | ((uint32_t)resR[k] << 8) | ((uint32_t)resB[k] << 17);
             v = unpred_px(T, L, TL, r);
           }
           myrow[x] = v;
@@ -956,9 +973,15 @@ __global__ __launch_bounds__(64) void k_dunpred_lz(DecJob j) {
 
 // Tiles with LZ copies narrower than 64 pixels (copies may reach two rows up): serial raster
 // walk per plane, one lane per plane, into dplane.
+__device__ __forceinline__ void dunpred_serial_tile(const DecJob& j, int t);
+
+// a small grid strides over the tiles (only LZ tiles narrower than 64 pixels work here)
 __global__ __launch_bounds__(192) void k_dunpred_serial(DecJob j) {
   if (dec_abort(j)) return;
-  const int t = blockIdx.x;
+  for (int t = blockIdx.x; t < j.ntiles; t += gridDim.x) dunpred_serial_tile(j, t);
+}
+
+__device__ __forceinline__ void dunpred_serial_tile(const DecJob& j, int t) {
   const DecTile ti = j.tiles[t];
   if (ti.err || unpred_fast(j, t, ti) || ti.w >= 64) return;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1153,6 +1176,7 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   if ((e = dbuf(w, 5, (size_t)j.ntiles * 4 * (j.lz_cap + 1) * 4, &q))) return e; j.matches = (uint32_t*)q;
   if ((e = dbuf(w, 6, 64, &q))) return e; j.gerr = (uint32_t*)q;
   if ((e = dbuf(w, 7, (size_t)j.ntiles * 3 * j.npix_cap * 2, &q))) return e; j.dplane = (uint16_t*)q;
+  if ((e = dbuf(w, 14, (size_t)j.ntiles * 4, &q))) return e; j.lzt = (uint32_t*)q;
   j.ix = index_streams(idx);
   j.ck = index_ckpts(idx);
   j.nix = index_nstreams(idx);
@@ -1187,14 +1211,16 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
     hipLaunchKernelGGL(k_drans_serial, dim3((S + 63) / 64), dim3(64), 0, s, j, S);
   }
   ctx_mark(c, s, "drans", false);
-  hipLaunchKernelGGL(k_dstored, dim3(S), dim3(256), 0, s, j, S);
+  if (!indexed) hipLaunchKernelGGL(k_dstored, dim3(S), dim3(256), 0, s, j, S);
   hipLaunchKernelGGL(k_dlz, dim3((j.ntiles + 63) / 64), dim3(64), 0, s, j);
   ctx_mark(c, s, "dlz", false);
+  if (j.dbg & 0x100) goto done;                  // measurement: stop before the unpredict stage
   hipLaunchKernelGGL(k_dunpred_fast, dim3(j.ntiles), dim3(64), (size_t)64 * ORING_PITCH + (size_t)3 * j.tw * 2, s, j);
-  j.lzband = (int)std::min<size_t>(64, (160 * 1024 - (size_t)j.tw * 4) / ((size_t)j.tw * 8));
-  hipLaunchKernelGGL(k_dunpred_lz, dim3(j.ntiles), dim3(64), (size_t)(2 * j.lzband + 1) * j.tw * 4, s, j);
-  hipLaunchKernelGGL(k_dunpred_serial, dim3(j.ntiles), dim3(192), 0, s, j);
+  j.lzband = (int)std::min<size_t>(64, (160 * 1024 - (size_t)j.tw * 4) / ((size_t)j.tw * 4) - 1);
+  hipLaunchKernelGGL(k_dunpred_lz, dim3(std::min(j.ntiles, 64)), dim3(64), (size_t)(j.lzband + 1) * j.tw * 4, s, j);
+  hipLaunchKernelGGL(k_dunpred_serial, dim3(std::min(j.ntiles, 64)), dim3(192), 0, s, j);
   ctx_mark(c, s, "dunpred", false);
+done:
   if (hipGetLastError() != hipSuccess) return 3;
   if (as) {
     launch_status_dec(j.gerr, (uint64_t)j.W * j.H * 3, as->status, s);

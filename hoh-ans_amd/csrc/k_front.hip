@@ -327,11 +327,21 @@ __global__ __launch_bounds__(NT) void k_front_wide(EncodeJob j) { front_tile<fal
 // (prediction.hpp:6-44) and its histogram.  One workgroup per tile; pass 1 writes the indices
 // into the tile's indexed-plane slot, pass 2 turns them into residuals in place, walking blocks
 // from the last to the first so every neighbour (q-1, q-w, q-w-1) is still an index when read.
+__device__ __forceinline__ void palette_tile(const EncodeJob& j, int t, uint32_t* hk, uint32_t* hv, uint32_t* phist);
+
+// a small grid strides over the tiles (palette candidates are rare): no idle workgroup per tile
 __global__ __launch_bounds__(NT) void k_palette(EncodeJob j) {
   __shared__ uint32_t hk[1024];
   __shared__ uint32_t hv[1024];
   __shared__ uint32_t phist[256];
-  const int t = blockIdx.x, tid = threadIdx.x;
+  for (int t = blockIdx.x; t < j.ntiles; t += gridDim.x) {
+    palette_tile(j, t, hk, hv, phist);
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ void palette_tile(const EncodeJob& j, int t, uint32_t* hk, uint32_t* hv, uint32_t* phist) {
+  const int tid = threadIdx.x;
   const TileInfo ti = j.tiles[t];
   if (!(ti.flags & TF_PALETTE_CAND) || (ti.flags & TF_GREY)) return;
   const int w = ti.w, h = ti.h, ncol = ti.colours;
@@ -383,7 +393,7 @@ __global__ __launch_bounds__(NT) void k_palette(EncodeJob j) {
 }
 
 void launch_palette(const EncodeJob& j, hipStream_t s) {
-  hipLaunchKernelGGL(k_palette, dim3(j.ntiles), dim3(NT), 0, s, j);
+  hipLaunchKernelGGL(k_palette, dim3(j.ntiles < 128 ? j.ntiles : 128), dim3(NT), 0, s, j);
 }
 
 void launch_front(const EncodeJob& j, hipStream_t s) {

@@ -7,6 +7,8 @@
 // (layer_encode.hpp:93-99).  Also fills the StreamInfo of the tile's streams.
 #include "hoh_internal.h"
 
+#include <algorithm>
+
 __device__ __forceinline__ uint32_t img_px(const EncodeJob& j, int x0, int y0, int w, uint32_t q) {
   const uint8_t* p = j.rgb + ((size_t)(y0 + (int)(q / w)) * j.W + x0 + (int)(q % w)) * 3;
   return p[0] | (p[1] << 8) | (p[2] << 16);
@@ -153,10 +155,18 @@ __global__ __launch_bounds__(64) void k_lz(EncodeJob j) {
 // the three residual planes (four with the indexed plane; order kept) and their histograms.
 // One 256-thread workgroup per tile; the nuke bitmap is built in LDS from the match list, then the plane is walked in
 // 256-pixel blocks with a block-wide rank of the kept pixels.
+__device__ __forceinline__ void nuke_tile(const EncodeJob& j, int t, uint32_t* nk_bits, uint32_t* wsum);
+
+// A small grid strides over the tiles (most have no match): a launch over every tile dispatches
+// ~1000 idle workgroups, which waits for free CUs when other images are in flight.
 __global__ __launch_bounds__(256) void k_nuke(EncodeJob j) {
   extern __shared__ uint32_t nk_bits[];                  // npix_cap / 32 words
   __shared__ uint32_t wsum[4];
-  const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int t = blockIdx.x; t < j.ntiles; t += gridDim.x) nuke_tile(j, t, nk_bits, wsum);
+}
+
+__device__ __forceinline__ void nuke_tile(const EncodeJob& j, int t, uint32_t* nk_bits, uint32_t* wsum) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const TileInfo ti = j.tiles[t];
   const uint32_t nm = ti.nmatch;
   if (nm == 0 || (ti.flags & TF_OVERFLOW) || nm > j.lz_cap) return;
@@ -217,5 +227,5 @@ void launch_lz(const EncodeJob& j, hipStream_t s) {
 }
 
 void launch_nuke(const EncodeJob& j, hipStream_t s) {
-  hipLaunchKernelGGL(k_nuke, dim3(j.ntiles), dim3(256), (size_t)(j.npix_cap / 32 + 1) * 4, s, j);
+  hipLaunchKernelGGL(k_nuke, dim3(std::min(j.ntiles, 128)), dim3(256), (size_t)(j.npix_cap / 32 + 1) * 4, s, j);
 }
