@@ -426,13 +426,9 @@ __device__ bool dec_run(const DecJob& j, const DecStream& d, const uint32_t* cum
 }
 
 #define DR_T 256      // threads per stream workgroup (lane = segment of HOH_SEG symbols)
-#define DR_BSH 5      // slot bucket = 32 slots
+#define DR_NB 1024    // 32-slot buckets (prob_bits <= 15)
+#define DR_FIXED ((2 * DR_NB + 2 * 512) * 4)   // LDS bytes before the payload stage
 
-// Indexed decode (rans64.hpp:107-142): one 256-thread workgroup per stream, thread = segment of
-// HOH_SEG symbols starting from the encoder's checkpoint.  LDS holds the cumulative table, an
-// exact slot -> symbol table (a byte per slot: the symbol's offset from the first symbol of its
-// 32-slot bucket, plus that first symbol per bucket) and the whole payload, so the per-symbol
-// chain is two LDS round trips and no global load; the symbol stores are never awaited.
 __device__ __forceinline__ void dec_stored(const DecJob& j, int sid, const DecStream& d) {
   uint16_t* out = j.dsym + d.out_off;
   const uint32_t sw = skew_w(j, sid, d.n);
@@ -442,27 +438,75 @@ __device__ __forceinline__ void dec_stored(const DecJob& j, int sid, const DecSt
   }
 }
 
-// Dynamic LDS: cum (514 u32) | bucket symbols (u16) | slot table (u8) | payload words.  Output is
-// the flat plane: each thread stores its segment 8 symbols (16 B) at a time.
+// Exact slot -> symbol lookup in two LDS reads.  Symbols present in the table get a compact
+// index k (ascending); per 32-slot bucket b: k0 = index of the symbol covering slot 32b and a
+// mask with bit i set where a symbol starts at slot 32b + i (i > 0); per k: {c | f << 16, sym}.
+// k(slot) = k0 + popcount(bits 1..slot&31 of the mask).  12 KB in all (a byte per slot was 32 KB).
+struct DrTables {
+  uint2* bk;    // [DR_NB] {start mask, k0}
+  uint2* sy;    // [512]   {c | f << 16, symbol}
+  __device__ __forceinline__ void lookup(uint32_t slot, uint32_t& sym, uint32_t& c, uint32_t& f) const {
+    const uint2 e = bk[slot >> 5];
+    const uint32_t k = e.y + __popc(__builtin_amdgcn_ubfe(e.x, 1, slot & 31));
+    const uint2 t = sy[k];
+    c = t.x & 0xffffu;
+    f = t.x >> 16;
+    sym = t.y;
+  }
+};
+
+// Indexed decode (rans64.hpp:107-142): one 256-thread workgroup per stream, thread = segment of
+// HOH_SEG symbols starting from the encoder's checkpoint.  LDS holds the lookup tables (12 KB) and
+// the whole payload (<= wcap words; three workgroups per CU at the default 40 KB stage), so the
+// per-symbol chain is two LDS round trips and no global load; the symbol stores are never awaited.
+// Output is the flat plane: each thread stores its segment 16 symbols (32 B) at a time.
 __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams, uint32_t wcap) {
   extern __shared__ __attribute__((aligned(16))) uint32_t dr_lds[];
   if (dec_abort(j)) return;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int sid = blockIdx.x;
   const DecStream d = j.streams[sid];
   if (d.mode == SM_STORED) { dec_stored(j, sid, d); return; }     // no separate launch
-  if (d.mode != SM_RANS || d.range > 512) return;
+  if (d.mode != SM_RANS || d.range > 512 || d.pb > 15) return;
   uint64_t T0 = 0, T1 = 0;
   if (j.dbg & 16) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(T0)::"memory");
   const uint32_t pb = d.pb, M = 1u << pb, mask = M - 1, range = d.range;
-  const uint32_t bsh = pb < DR_BSH ? pb : DR_BSH;
-  uint32_t* cum_s = dr_lds;                                   // 514
-  uint16_t* sy_s = (uint16_t*)(dr_lds + 514);                 // nbk (<= 1024)
-  uint8_t* tb = (uint8_t*)(dr_lds + 514 + 512);               // M (<= 32768)
-  uint32_t* pw = dr_lds + 514 + 512 + 8192;                   // wcap words
-  __shared__ int wide;
-  if (tid == 0) wide = 0;
+  DrTables tb;
+  tb.bk = (uint2*)dr_lds;                                     // 2 * DR_NB words
+  tb.sy = (uint2*)(dr_lds + 2 * DR_NB);                       // 2 * 512 words
+  uint32_t* pw = dr_lds + DR_FIXED / 4;                       // wcap words (the payload stage)
+  uint32_t* cum_s = pw;                                       // range + 1 words, until staging
+  __shared__ uint32_t wtot[DR_T / 64];
   for (uint32_t i = tid; i <= range; i += DR_T) cum_s[i] = j.cum[(size_t)sid * j.cum_stride + i];
+  const uint32_t nb = (M + 31) >> 5;
+  for (uint32_t b = tid; b < nb; b += DR_T) tb.bk[b] = make_uint2(0, 0);
+  __syncthreads();
+  {
+    // compact index of the symbols present: thread t owns symbols 2t, 2t+1 (range <= 512)
+    const uint32_t s0 = 2 * tid, s1 = s0 + 1;
+    const uint32_t a0 = s0 < range ? cum_s[s0] : 0, a1 = s0 < range ? cum_s[s0 + 1] : 0;
+    const uint32_t a2 = s1 < range ? cum_s[s1 + 1] : 0;
+    const uint32_t p0 = s0 < range && a1 > a0, p1 = s1 < range && a2 > a1;
+    const uint32_t cnt = p0 + p1;
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(incl, o);
+      if (lane >= o) incl += t;
+    }
+    if (lane == 63) wtot[wv] = incl;
+    __syncthreads();
+    uint32_t k = incl - cnt;
+    for (int q = 0; q < wv; q++) k += wtot[q];
+    auto put = [&](uint32_t s, uint32_t c0, uint32_t c1, uint32_t kk) {
+      tb.sy[kk] = make_uint2(c0 | ((c1 - c0) << 16), s);
+      for (uint32_t b = (c0 + 31) >> 5; b <= (c1 - 1) >> 5; b++) tb.bk[b].y = kk;   // buckets it starts
+      if (c0 & 31) atomicOr(&tb.bk[c0 >> 5].x, 1u << (c0 & 31));
+    };
+    if (p0) put(s0, a0, a1, k);
+    if (p1) put(s1, a1, a2, k + p0);
+  }
+  __syncthreads();
   const bool staged = d.words <= wcap;
   if (staged) {
     const uint64_t last = j.size >= 4 ? (j.size & ~3ull) - 4 : 0;
@@ -494,53 +538,41 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams, uint32_t
   __syncthreads();
   uint64_t Ta = 0;
   if (j.dbg & 16) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(Ta)::"memory");
-  // slot table.  A slot's byte is (its symbol) - (first symbol of its 32-slot bucket), so it is
-  // 0 everywhere except in buckets where a symbol starts mid-bucket: (1) first symbol of every
-  // bucket, one thread per symbol; (2) zero fill; (3) each symbol writes its slots inside the
-  // bucket it starts in (at most 31).  All stores independent, no serial walk.
-  for (uint32_t s = tid; s < range; s += DR_T) {
-    const uint32_t c0 = cum_s[s], c1 = cum_s[s + 1];
-    if (c1 <= c0) continue;
-    const uint32_t b1 = (c1 - 1) >> bsh;
-    for (uint32_t b = (c0 + (1u << bsh) - 1) >> bsh; b <= b1; b++) sy_s[b] = (uint16_t)s;
-  }
-  for (uint32_t q = tid; q < (M + 3) / 4; q += DR_T) ((uint32_t*)tb)[q] = 0;
-  __syncthreads();
-  for (uint32_t s = tid; s < range; s += DR_T) {
-    const uint32_t c0 = cum_s[s], c1 = cum_s[s + 1];
-    if (c1 <= c0 || (c0 & ((1u << bsh) - 1)) == 0) continue;  // starts a bucket: bytes stay 0
-    const uint32_t b = c0 >> bsh;
-    const uint32_t off = s - sy_s[b];
-    if (off > 255) wide = 1;
-    const uint32_t e = min(c1, (b + 1) << bsh);
-    for (uint32_t slot = c0; slot < e; slot++) tb[slot] = (uint8_t)off;
-  }
-  __syncthreads();
   uint16_t* out = j.dsym + d.out_off;
   const uint32_t sw = skew_w(j, sid, d.n);
-  if (d.ix < 0 || wide || !staged) {
-    // no index for this stream (or a table/payload that does not fit): serial on thread 0
-    if (tid == 0) {
-      const uint64_t wend = d.payload_off + (uint64_t)d.words * 4;
-      uint64_t x = (uint64_t)ld_u32_unaligned(j.in, d.payload_off) | ((uint64_t)ld_u32_unaligned(j.in, d.payload_off + 4) << 32);
-      uint64_t xe;
-      bool ok;
-      if (d.ix < 0) {
-        ok = staged ? dec_run<true>(j, d, cum_s, sy_s, bsh, pw, x, 2, d.words, 0, d.n, OutCursor(out, sw, 0), &xe)
-                    : dec_run<false>(j, d, cum_s, sy_s, bsh, nullptr, x, d.payload_off + 8, wend, 0, d.n,
-                                     OutCursor(out, sw, 0), &xe);
-        if (!ok || xe != (1ull << 31)) atomicOr(j.gerr, 4u);
-        return;
+  // generic decode of symbols [s0, s1) from state x (payload word wi of the stage, or the file)
+  auto run = [&](uint64_t x, uint32_t wi, uint32_t s0, uint32_t s1, uint64_t* xe) -> bool {
+    OutCursor oc(out, sw, s0);
+    const uint64_t wend = (uint64_t)d.words;
+    for (uint32_t i = s0; i < s1; i++) {
+      const uint32_t slot = (uint32_t)x & mask;
+      uint32_t sym, c, f;
+      tb.lookup(slot, sym, c, f);
+      oc.put(i, (uint16_t)sym);
+      x = (uint64_t)f * (x >> pb) + (slot - c);             // Rans64DecAdvance
+      if (x < (1ull << 31)) {
+        if (wi >= wend) return false;
+        x = (x << 32) | (staged ? pw[wi] : ld_u32_unaligned(j.in, d.payload_off + (uint64_t)wi * 4));
+        wi++;
       }
     }
-    if (d.ix < 0) return;
+    *xe = x;
+    return true;
+  };
+  if (d.ix < 0) {
+    // no index for this stream: serial on thread 0
+    if (tid == 0) {
+      const uint64_t x = (uint64_t)ld_u32_unaligned(j.in, d.payload_off) | ((uint64_t)ld_u32_unaligned(j.in, d.payload_off + 4) << 32);
+      uint64_t xe;
+      if (!run(x, 2, 0, d.n, &xe) || xe != (1ull << 31)) atomicOr(j.gerr, 4u);
+    }
+    return;
   }
   if (j.dbg & 16) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(T1)::"memory");
   if (j.dbg & 4) return;
   const IndexStream xs = j.ix[d.ix];
   const uint32_t nseg = (d.n + DSEG - 1) / DSEG;
   bool bad = false;
-  const bool fast = staged && !wide;
   for (uint32_t sg0 = 0; sg0 < nseg; sg0 += DR_T) {
     const uint32_t sg = sg0 + tid;
     const bool act = sg < nseg;
@@ -554,7 +586,7 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams, uint32_t
       s1 = min(d.n, s0 + DSEG);
       if (sg + 1 < nseg) { const Checkpoint c2 = j.ck[xs.ckpt_off + sg + 1]; want = (uint64_t)c2.xl | ((uint64_t)c2.xh << 32); }
     }
-    if (fast && act && s1 - s0 == DSEG) {
+    if (staged && act && s1 - s0 == DSEG) {
       // a whole segment: 16 symbols per 32-B store of the lane's own (flat) output range; the
       // stores are never awaited, and nothing but the chain touches LDS
       uint4* o4 = (uint4*)(out + s0);
@@ -564,8 +596,8 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams, uint32_t
         for (int u = 0; u < 16; u++) {
           const uint32_t nw = pw[min(wi, wcap - 1)];
           const uint32_t slot = (uint32_t)x & mask;
-          const uint32_t sym = sy_s[slot >> bsh] + tb[slot];
-          const uint32_t cc = cum_s[sym], f = cum_s[sym + 1] - cc;
+          uint32_t sym, cc, f;
+          tb.lookup(slot, sym, cc, f);
           if (u & 1) pk[u >> 1] |= sym << 16; else pk[u >> 1] = sym;
           x = (uint64_t)f * (x >> pb) + (slot - cc);       // Rans64DecAdvance
           if (x < (1ull << 31)) { x = (x << 32) | nw; wi++; }
@@ -579,26 +611,8 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams, uint32_t
       continue;
     }
     if (!act) continue;
-    if (fast) {
-      OutCursor oc(out, sw, s0);
-      for (uint32_t i = s0; i < s1; i++) {
-        const uint32_t nw = pw[min(wi, wcap - 1)];
-        const uint32_t slot = (uint32_t)x & mask;
-        const uint32_t sym = sy_s[slot >> bsh] + tb[slot];
-        const uint32_t cc = cum_s[sym], f = cum_s[sym + 1] - cc;
-        oc.put(i, (uint16_t)sym);
-        x = (uint64_t)f * (x >> pb) + (slot - cc);         // Rans64DecAdvance
-        if (x < (1ull << 31)) { x = (x << 32) | nw; wi++; }
-      }
-      if (x != want || wi > d.words) bad = true;
-    } else {
-      const uint64_t wend = d.payload_off + (uint64_t)d.words * 4;
-      uint64_t xe;
-      const bool ok = staged ? dec_run<true>(j, d, cum_s, sy_s, bsh, pw, x, wi, d.words, s0, s1, OutCursor(out, sw, s0), &xe)
-                             : dec_run<false>(j, d, cum_s, sy_s, bsh, nullptr, x, d.payload_off + (uint64_t)wi * 4, wend,
-                                              s0, s1, OutCursor(out, sw, s0), &xe);
-      if (!ok || xe != want) bad = true;
-    }
+    uint64_t xe;
+    if (!run(x, wi, s0, s1, &xe) || xe != want) bad = true;
   }
   if (bad) atomicOr(j.gerr, 4u);
   if ((j.dbg & 16) && tid == 0) {
@@ -1203,8 +1217,9 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   }
   if (indexed) {
     // payload stage sized to the largest stream when it fits next to the tables (<= 128 KB)
-    const size_t fixed = (514 + 512 + 8192) * 4;                      // cum + bucket symbols + slot table
-    const uint32_t wcap = (uint32_t)std::min<size_t>(std::max<uint32_t>(maxw, 1), (150 * 1024 - fixed) / 4);
+    const size_t fixed = DR_FIXED;                                     // lookup tables
+    const uint32_t wcap = (uint32_t)std::min<size_t>(std::max<uint32_t>(std::max<uint32_t>(maxw, 1), 514),
+                                                     (150 * 1024 - fixed) / 4);   // >= 514: cum_s lives there first
     hipLaunchKernelGGL(k_dmatch, dim3((S + 255) / 256), dim3(256), 0, s, j, S);
     hipLaunchKernelGGL(k_drans, dim3(S), dim3(DR_T), fixed + (size_t)wcap * 4, s, j, S, wcap);
   } else {
