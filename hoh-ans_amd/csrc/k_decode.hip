@@ -930,9 +930,16 @@ __device__ __forceinline__ void dunpred_lz_tile(const DecJob& j, int t, uint32_t
     if (m < nm) { midx = mt[4 * m]; mlen = mt[4 * m + 1]; mback = mt[4 * m + 2]; }
     uint32_t left = PK_HALF;
     const uint32_t rowbase = (uint32_t)y * w;
+    // the lane's next residual (index rowbase - nuked-before-row), loaded one use ahead so the
+    // dependent loop never waits on memory for it
+    auto ldres = [&](uint32_t k) -> uint32_t {
+      const uint32_t kk = k < kb1 ? k : (kb1 ? kb1 - 1 : 0);
+      return resG[kk] | ((uint32_t)resR[kk] << 8) | ((uint32_t)resB[kk] << 17);
+    };
+    uint32_t kcur = rowbase - nuk;
+    uint32_t rcur = act ? ldres(kcur) : 0u;
     uint32_t* myrow = band + (size_t)(lane + 1) * w;
     const uint32_t* uprow = band + (size_t)lane * w;
-    uint8_t* orow = obase + (size_t)y * j.W * 3;
     while (__any(prog < (uint32_t)w)) {
       const uint32_t above = wave_shr1(prog, (uint32_t)w);
       if (prog < (uint32_t)w) {
@@ -964,20 +971,29 @@ __device__ __forceinline__ void dunpred_lz_tile(const DecJob& j, int t, uint32_t
             const uint32_t L = x == 0 ? PK_HALF : left;
             const uint32_t k = i - nuk;
             uint32_t r = 0;
-            if (k < kb0 || k >= kb1) bad = true;
-            else r = resG[k] | ((uint32_t)resR[k] << 8) | ((uint32_t)resB[k] << 17);
+            if (k < kb0 || k >= kb1 || k != kcur) bad = true;
+            else r = rcur;
+            kcur = k + 1;
+            rcur = ldres(kcur);
             v = unpred_px(T, L, TL, r);
           }
           myrow[x] = v;
           left = v;
-          const uint32_t G = v & 255;
-          uint8_t* o = orow + (size_t)x * 3;
-          o[0] = (uint8_t)(((v >> 8) & 511) + G); o[1] = (uint8_t)G; o[2] = (uint8_t)((v >> 17) + G);
           prog++;
         }
       }
     }
     __syncthreads();
+    // the band's RGB rows leave from LDS as coalesced row segments (lanes = consecutive pixels)
+    for (int rr = 0; rr < r1 - r0; rr++) {
+      const uint32_t* brow = band + (size_t)(rr + 1) * w;
+      uint8_t* orow = obase + (size_t)(r0 + rr) * j.W * 3;
+      for (int x = lane; x < w; x += 64) {
+        const uint32_t v = brow[x], G = v & 255;
+        uint8_t* o = orow + (size_t)x * 3;
+        o[0] = (uint8_t)(((v >> 8) & 511) + G); o[1] = (uint8_t)G; o[2] = (uint8_t)((v >> 17) + G);
+      }
+    }
     const int lastrow = r1 - r0;                            // LDS row of the band's last image row
     for (int x = lane; x < w; x += 64) band[x] = band[(size_t)lastrow * w + x];
     __syncthreads();
@@ -1232,7 +1248,7 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   if (j.dbg & 0x100) goto done;                  // measurement: stop before the unpredict stage
   hipLaunchKernelGGL(k_dunpred_fast, dim3(j.ntiles), dim3(64), (size_t)64 * ORING_PITCH + (size_t)3 * j.tw * 2, s, j);
   j.lzband = (int)std::min<size_t>(64, (160 * 1024 - (size_t)j.tw * 4) / ((size_t)j.tw * 4) - 1);
-  hipLaunchKernelGGL(k_dunpred_lz, dim3(std::min(j.ntiles, 64)), dim3(64), (size_t)(j.lzband + 1) * j.tw * 4, s, j);
+  hipLaunchKernelGGL(k_dunpred_lz, dim3(std::min(j.ntiles, 256)), dim3(64), (size_t)(j.lzband + 1) * j.tw * 4, s, j);
   hipLaunchKernelGGL(k_dunpred_serial, dim3(std::min(j.ntiles, 64)), dim3(192), 0, s, j);
   ctx_mark(c, s, "dunpred", false);
 done:

@@ -181,45 +181,55 @@ __device__ __forceinline__ void nuke_tile(const EncodeJob& j, int t, uint32_t* n
   __syncthreads();
   const bool grey = ti.flags & TF_GREY, pal = !grey && (ti.flags & TF_PALETTE_CAND);
   const int nslots = j.speed ? 2 * HOH_NPLANE_S : 4;
+  // plane slots: -s0 the MED planes G R' B' (+ indexed); -s>=1 the six MED planes, then the six
+  // searched planes, each with its stream's histogram.  The kept pixels' ranks are the same in
+  // every plane, so each 256-pixel block ranks once and moves all present planes.
+  uint16_t* r[2 * HOH_NPLANE_S];
+  uint32_t* hk[2 * HOH_NPLANE_S];
+  int np = 0;
   for (int k = 0; k < nslots; k++) {
-    // plane slots: -s0 the MED planes G R' B' (+ indexed); -s>=1 the six MED planes, then the six
-    // searched planes, each with its stream's histogram
     const int p = k % HOH_NPLANE_S;
     const bool present = !grey && (p < 3 || (p == 3 && pal) || (p >= 4 && j.speed >= 3));
     if (!present) continue;
-    uint16_t* r;
-    uint32_t* hk;
     if (k < HOH_NPLANE_S || !j.speed) {
-      r = j.sym + med_plane_off(j, t, p);
-      hk = j.hist + (size_t)(t * j.spt + med_kind(j, p)) * 512;
+      r[np] = j.sym + med_plane_off(j, t, p);
+      hk[np] = j.hist + (size_t)(t * j.spt + med_kind(j, p)) * 512;
     } else {
-      r = j.sym + fin_plane_off(j, t, p);
-      hk = j.hist + (size_t)(t * j.spt + KS_FIN + p) * 512;
+      r[np] = j.sym + fin_plane_off(j, t, p);
+      hk[np] = j.hist + (size_t)(t * j.spt + KS_FIN + p) * 512;
     }
-    uint32_t outc = 0;
-    uint16_t vnext = tid < npix ? r[tid] : 0;
-    for (uint32_t base = 0; base < npix; base += 256) {
-      const uint32_t p = base + tid;
-      const bool valid = p < npix;
-      const uint16_t v = vnext;
-      if (base + 256 + tid < npix) vnext = r[base + 256 + tid];
-      const bool nuked = valid && ((nk_bits[p >> 5] >> (p & 31)) & 1);
-      if (nuked) atomicSub(&hk[v], 1u);
-      const bool keep = valid && !nuked;
-      const uint64_t bal = __ballot(keep);
-      if (lane == 0) wsum[wv] = (uint32_t)__popcll(bal);
-      __syncthreads();
-      uint32_t before = 0, tot = 0;
-      for (int q = 0; q < 4; q++) { const uint32_t c = wsum[q]; if (q < wv) before += c; tot += c; }
-      const uint32_t dest = outc + before + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
-      __syncthreads();
-      // in place: dest <= p, and every block reads its values before any write of this pass
-      // reaches them (writes of block i land below block i's end)
-      if (keep) r[dest] = v;
-      outc += tot;
-    }
-    __syncthreads();
+    np++;
   }
+  if (np == 0) return;
+  uint32_t outc = 0;
+  for (uint32_t base = 0; base < npix; base += 256) {
+    const uint32_t p = base + tid;
+    const bool valid = p < npix;
+    uint16_t v[2 * HOH_NPLANE_S];
+#pragma unroll
+    for (int k = 0; k < 2 * HOH_NPLANE_S; k++) v[k] = (k < np && valid) ? r[k][p] : 0;
+    const bool nuked = valid && ((nk_bits[p >> 5] >> (p & 31)) & 1);
+    if (nuked) {
+#pragma unroll
+      for (int k = 0; k < 2 * HOH_NPLANE_S; k++) if (k < np) atomicSub(&hk[k][v[k]], 1u);
+    }
+    const bool keep = valid && !nuked;
+    const uint64_t bal = __ballot(keep);
+    if (lane == 0) wsum[wv] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+    for (int q = 0; q < 4; q++) { const uint32_t c = wsum[q]; if (q < wv) before += c; tot += c; }
+    const uint32_t dest = outc + before + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+    __syncthreads();
+    // in place: dest <= p, and every block reads its values before any write of this pass
+    // reaches them (writes of block i land below block i's end)
+    if (keep) {
+#pragma unroll
+      for (int k = 0; k < 2 * HOH_NPLANE_S; k++) if (k < np) r[k][dest] = v[k];
+    }
+    outc += tot;
+  }
+  __syncthreads();
 }
 
 void launch_lz(const EncodeJob& j, hipStream_t s) {
