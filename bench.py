@@ -17,9 +17,14 @@ One step = one pass of the hot path over the workload, inputs resident in HBM:
 value = raw RGB bytes of all ranks x K / max-over-ranks(time of the K steps) / 1e6.
 Images in flight (--inflight, default 12): each GPU keeps D images in flight, one library context,
 HIP stream and hardware queue per slot (GPU_MAX_HW_QUEUES raised to D), steps dealt round-robin
-to the slots.  The serial rANS chain of one image (65,536 dependent steps per tile-plane) leaves
+to the slots.  At N = 1 one host thread enqueues every step through the enqueue-only calls
+(hoh_encode_image_async / hoh_decode_image_async): no host round trip inside the timed region,
+the per-step status words are checked afterwards (--threads: one host thread per slot with the
+synchronous calls instead, which is what N > 1 does because the gather needs the tile sizes on
+the host).  The serial rANS chain of one image (65,536 dependent steps per tile-plane) leaves
 most CUs idle; the other images' kernels fill them.  detail.latency_ms_* is the per-image latency
-under that load; --inflight 1 measures one image at a time.
+under that load (HIP events on each slot's stream at N = 1); --inflight 1 measures one image at a
+time.
 
 Outside the timed region: the decoded image is compared with the input (lossless), and at
 N = 1 the encoded file's sha256 with the golden of the compiled reference (tests/golden).
