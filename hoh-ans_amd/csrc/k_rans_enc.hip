@@ -112,11 +112,11 @@ __device__ __forceinline__ void ckpt(const Coder& c, Checkpoint* ck, uint32_t k)
   ck[k] = p;
 }
 
-template <int LANES>
-__global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane, SidMap ma, int na, SidMap mb, int nblk,
-                                                  int rot) {
+template <int LANES, int WAVES = 1>
+__global__ __launch_bounds__(64 * WAVES) void k_rans_fast(EncodeJob j, int nplane, SidMap ma, int na, SidMap mb,
+                                                          int nblk, int rot) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // the grid covers every CU; the working blocks are a window rotated per launch so that the
   // chains of images in flight land on different CUs instead of sharing the first ones
   const int blk = (int)((blockIdx.x + gridDim.x - rot) % gridDim.x);
@@ -125,7 +125,7 @@ __global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane, SidMa
   if (!(j.dbg & 0x400000)) __builtin_amdgcn_s_setprio(3);
   uint64_t t_beg = 0;
   if (j.dbgbuf && lane == 0) t_beg = __builtin_amdgcn_s_memrealtime();
-  const int pi = blk * LANES + lane;
+  const int pi = (blk * WAVES + wave) * LANES + lane;
   if (lane >= LANES || pi >= nplane) return;
   const uint32_t sid = plane_sid(pi, j.spt, ma, na, mb);
   StreamInfo st = j.streams[sid];
@@ -137,7 +137,7 @@ __global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane, SidMa
   c.xh = 0; c.xl = 1u << 31; c.mask = 0; c.slot = 0;
   c.slab = j.slabs + st.slab_off;
   c.widx = st.slab_cap;
-  c.win = (uint32_t*)(lds + lane * WIN * 4);
+  c.win = (uint32_t*)(lds + threadIdx.x * WIN * 4);
   Checkpoint* ck = j.ckpt ? j.ckpt + st.ckpt_off : nullptr;
   const uint16_t* sp = j.sym + st.sym_off;
   // prologue: the top n % 32 symbols one at a time (descending); the rest is whole windows
@@ -227,24 +227,36 @@ __global__ __launch_bounds__(64) void k_rans_gen(EncodeJob j, int nstreams, SidM
 static std::atomic<unsigned> g_rot{0};
 
 void launch_rans_fast(const EncodeJob& j, int nplane, hipStream_t s, SidMap a, int na, SidMap b) {
-  const int lanes = (j.dbg >> 8) & 127 ? (j.dbg >> 8) & 127 : 64;     // measurement knob
   if (nplane <= 0) return;
-  const int nblk = (nplane + lanes - 1) / lanes;
-  const int grid = nblk >= 1024 || (j.dbg & 0x100000) ? nblk : 1024;
+  // The chain is issue-bound, so two chains on one SIMD run at half speed, and a launch ends with
+  // its slowest chain; more than two chains per CU also slow each other.  One chain wave per
+  // workgroup with a 56 KB LDS request (8 KB are used) caps the chains at two per CU and, alone,
+  // spreads an image's 48 chains over 48 CUs.  The grid covers the chip with a per-launch rotation
+  // so that the chains of images in flight land on different CUs.  Measurement knobs: dbg bit 23 =
+  // two chain waves per workgroup with an 81 KB request (one workgroup, i.e. two chains, per CU:
+  // 40 KB of LDS per chain; +2 % bench throughput at 12 in flight but 25 % slower chains for one
+  // image alone, so not the default), bits 8..14 = lanes per wave, bits 24..31 = the request in KB.
+  const bool one = !(j.dbg & 0x800000) || ((j.dbg >> 8) & 127);
+  const int lanes = (j.dbg >> 8) & 127 ? (j.dbg >> 8) & 127 : 64;
+  const int waves = one ? 1 : 2;
+  const int per = lanes * waves;
+  const int nblk = (nplane + per - 1) / per;
+  const int span = one ? 1024 : 512;
+  const int grid = nblk >= span || (j.dbg & 0x100000) ? nblk : span;
   const int rot = grid == nblk ? 0 : (int)((g_rot.fetch_add(1) * 8u * (unsigned)((nblk + 7) / 8)) % (unsigned)grid);
-  // The chain is issue-bound, so two chains on one SIMD run at half speed, and a launch ends
-  // with its slowest chain.  Asking for 56 KB of LDS (8 KB are used) caps the chains at
-  // two per CU (one per SIMD in practice) when several images are in flight.  dbg bits 24..31
-  // override the size in KB (measurement).
-  const size_t pad = (j.dbg >> 24) ? (size_t)((j.dbg >> 24) & 255) * 1024 : (size_t)56 * 1024;
-  if (lanes == 16) {
+  const size_t pad = (j.dbg >> 24) ? (size_t)((j.dbg >> 24) & 255) * 1024 : (size_t)(one ? 56 : 81) * 1024;
+  if (!one) {
+    hipLaunchKernelGGL((k_rans_fast<64, 2>), dim3(grid), dim3(128), std::max<size_t>(128 * WIN * 4, pad), s, j, nplane,
+                       a, na, b, nblk, rot);
+  } else if (lanes == 16) {
     hipLaunchKernelGGL(k_rans_fast<16>, dim3(grid), dim3(64), 16 * WIN * 4, s, j, nplane, a, na, b, nblk, rot);
   } else if (lanes == 32) {
     hipLaunchKernelGGL(k_rans_fast<32>, dim3(grid), dim3(64), 32 * WIN * 4, s, j, nplane, a, na, b, nblk, rot);
   } else if (lanes == 8) {
     hipLaunchKernelGGL(k_rans_fast<8>, dim3(grid), dim3(64), 8 * WIN * 4, s, j, nplane, a, na, b, nblk, rot);
   } else {
-    hipLaunchKernelGGL(k_rans_fast<64>, dim3(grid), dim3(64), std::max<size_t>(64 * WIN * 4, pad), s, j, nplane, a, na, b, nblk, rot);
+    hipLaunchKernelGGL(k_rans_fast<64>, dim3(grid), dim3(64), std::max<size_t>(64 * WIN * 4, pad), s, j, nplane, a, na,
+                       b, nblk, rot);
   }
 }
 
