@@ -103,3 +103,45 @@ def test_async_errors_in_status(hoh):
     with pytest.raises(hoh.HohError):
         hoh.encode_image_async(small, 64, 64, out, st[3, 0:2], ctx=ctx)
     ctx.close()
+
+
+@pytest.mark.parametrize("speed", [1, 3])
+def test_async_speed_matches_sync(hoh, speed):
+    """-s1 / -s3 encodes enqueued without host waits give the synchronous call's bytes"""
+    import torch
+    from hoh_ans.synth import synth_rgb
+    W, H = 768, 520
+    img = synth_rgb(W, H, 21, 3)
+    d = torch.from_numpy(img.reshape(-1).copy()).cuda()
+    want, n, _ = hoh.encode_image(d, W, H, speed=speed)
+    want = want[:n].cpu().numpy().tobytes()
+    ctx = hoh.Context(0)
+    out = torch.empty(hoh.lib().hoh_encode_bound(W, H), dtype=torch.uint8, device="cuda")
+    st = _status(torch)
+    hoh.encode_image_async(d, W, H, out, st[0:2], ctx=ctx, speed=speed)
+    torch.cuda.synchronize()
+    m = hoh.check_status(st.cpu().numpy()[0:2], "encode")
+    assert out[:m].cpu().numpy().tobytes() == want
+    ctx.close()
+
+
+def test_async_unsupported_in_status(hoh):
+    """a file with an indexed (palette, mode 127) tile decodes to HOH_E_UNSUPPORTED through the
+    status word, like the synchronous call's return code"""
+    import torch
+    rs = np.random.RandomState(11)
+    pal = np.stack([rs.randint(0, 256, 64), np.full(64, 100), rs.randint(0, 256, 64)], 1).astype(np.uint8)
+    img = pal[rs.randint(0, 64, (512, 512))]
+    H, W, _ = img.shape
+    d = torch.from_numpy(img.reshape(-1).copy()).cuda()
+    ctx = hoh.Context(0)
+    out = torch.empty(hoh.lib().hoh_encode_bound(W, H), dtype=torch.uint8, device="cuda")
+    dec = torch.empty(W * H * 3, dtype=torch.uint8, device="cuda")
+    st = _status(torch)
+    hoh.encode_image_async(d, W, H, out, st[0:2], ctx=ctx)
+    hoh.decode_image_async(out, out.numel(), W, H, dec, st[2:4], ctx=ctx)
+    torch.cuda.synchronize()
+    s = st.cpu().numpy()
+    hoh.check_status(s[0:2], "encode")
+    assert s[2] == 6
+    ctx.close()
