@@ -428,6 +428,7 @@ __device__ bool dec_run(const DecJob& j, const DecStream& d, const uint32_t* cum
 #define DR_T 256      // threads per stream workgroup (lane = segment of HOH_SEG symbols)
 #define DR_NB 1024    // 32-slot buckets (prob_bits <= 15)
 #define DR_FIXED ((2 * DR_NB + 2 * 512) * 4)   // LDS bytes before the payload stage
+#define DR_RW 16      // payload ring words per thread (ringed k_drans)
 
 __device__ __forceinline__ void dec_stored(const DecJob& j, int sid, const DecStream& d) {
   uint16_t* out = j.dsym + d.out_off;
@@ -457,8 +458,9 @@ struct DrTables {
 
 // Indexed decode (rans64.hpp:107-142): one 256-thread workgroup per stream, thread = segment of
 // HOH_SEG symbols starting from the encoder's checkpoint.  LDS holds the lookup tables (12 KB) and
-// the whole payload (<= wcap words; three workgroups per CU at the default 40 KB stage), so the
-// per-symbol chain is two LDS round trips and no global load; the symbol stores are never awaited.
+// a 16-word payload ring per thread (16 KB), refilled from the file 4 words a group ahead, so the
+// per-symbol chain is LDS round trips only and five workgroups fit a CU (staging the whole payload,
+// HOH_DEC_DBG 0x200, needs a 40 KB stage and allows three); the symbol stores are never awaited.
 // Output is the flat plane: each thread stores its segment 16 symbols (32 B) at a time.
 __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams, uint32_t wcap) {
   extern __shared__ __attribute__((aligned(16))) uint32_t dr_lds[];
@@ -507,7 +509,10 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams, uint32_t
     if (p1) put(s1, a1, a2, k + p0);
   }
   __syncthreads();
-  const bool staged = d.words <= wcap;
+  // ringed (default): each thread streams its segment's payload words from the file through a
+  // 16-word ring of its own in LDS; staged (dbg 0x200): the whole payload is copied to LDS first
+  const bool ringed = !(j.dbg & 0x200);
+  const bool staged = !ringed && d.words <= wcap;
   if (staged) {
     const uint64_t last = j.size >= 4 ? (j.size & ~3ull) - 4 : 0;
     uint32_t tail = 0;
@@ -585,6 +590,77 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams, uint32_t
       s0 = sg * DSEG;
       s1 = min(d.n, s0 + DSEG);
       if (sg + 1 < nseg) { const Checkpoint c2 = j.ck[xs.ckpt_off + sg + 1]; want = (uint64_t)c2.xl | ((uint64_t)c2.xh << 32); }
+    }
+    if (ringed && act && s1 - s0 == DSEG) {
+      // Payload word k of the stream = bytes P+4k .. P+4k+3 of the file.  The lane's ring holds
+      // words [fill-DR_RW, fill) in slots k % DR_RW (slot-major: lanes read consecutive banks).
+      // A 16-symbol group reads at most 8 words (each symbol takes <= 15 bits, a renorm adds 32,
+      // and the state stays in [2^31, 2^63)), so 8 words ready at a group's start suffice; the
+      // next 4 are fetched one group ahead.
+      uint32_t* rg = pw + tid;
+      const uint64_t P = d.payload_off;
+      const uint32_t al = (uint32_t)(P & 3);
+      const uint64_t szal = j.size & ~3ull;
+      uint32_t tailw = 0;
+      for (uint64_t q = szal; q < j.size; q++) tailw |= (uint32_t)j.in[q] << (8 * (q & 3));
+      auto fetch4 = [&](uint32_t k, uint32_t* o) {           // words k .. k+3
+        const uint64_t a = (P & ~3ull) + (uint64_t)k * 4;
+        uint32_t A[5];
+        if (a + 20 <= szal) {
+          typedef uint32_t u4a __attribute__((ext_vector_type(4), aligned(4)));
+          const u4a v = *(const u4a*)(j.in + a);
+          A[0] = v.x; A[1] = v.y; A[2] = v.z; A[3] = v.w;
+          A[4] = *(const uint32_t*)(j.in + a + 16);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 5; e++) {
+            const uint64_t b = a + 4 * e;
+            A[e] = b + 4 <= szal ? *(const uint32_t*)(j.in + b) : (b == szal ? tailw : 0u);
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; e++) o[e] = __builtin_amdgcn_alignbyte(A[e + 1], A[e], al);
+      };
+      auto put4 = [&](uint32_t k, const uint32_t* o) {
+#pragma unroll
+        for (int e = 0; e < 4; e++) rg[((k + e) & (DR_RW - 1)) * DR_T] = o[e];
+      };
+      uint32_t fill = wi, pend[4];
+      bool hp = true;                                        // pend holds words fill .. fill+3
+      {
+        uint32_t t0[4], t1[4];
+        fetch4(fill, t0); fetch4(fill + 4, t1);
+        put4(fill, t0); put4(fill + 4, t1);
+        fill += 8;
+        fetch4(fill, pend);                                  // lands at the first group
+      }
+      uint4* o4 = (uint4*)(out + s0);
+      for (uint32_t g = 0; g < DSEG / 16; g++) {
+        // land the words fetched a group ago (fill + 4 - wi <= DR_RW held when they were issued,
+        // so no unread word is overwritten)
+        if (hp) { put4(fill, pend); fill += 4; }
+        while (fill - wi < 8) {                              // a lane that read fast: fetch now
+          uint32_t t[4];
+          fetch4(fill, t); put4(fill, t); fill += 4;
+        }
+        hp = fill + 4 - wi <= DR_RW;
+        if (hp) fetch4(fill, pend);
+        uint32_t pk[8];
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+          const uint32_t nw = rg[(wi & (DR_RW - 1)) * DR_T];
+          const uint32_t slot = (uint32_t)x & mask;
+          uint32_t sym, cc, f;
+          tb.lookup(slot, sym, cc, f);
+          if (u & 1) pk[u >> 1] |= sym << 16; else pk[u >> 1] = sym;
+          x = (uint64_t)f * (x >> pb) + (slot - cc);       // Rans64DecAdvance
+          if (x < (1ull << 31)) { x = (x << 32) | nw; wi++; }
+        }
+        o4[2 * g] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+        o4[2 * g + 1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
+      }
+      if (x != want || wi > d.words) bad = true;
+      continue;
     }
     if (staged && act && s1 - s0 == DSEG) {
       // a whole segment: 16 symbols per 32-B store of the lane's own (flat) output range; the
@@ -1237,7 +1313,8 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
     const uint32_t wcap = (uint32_t)std::min<size_t>(std::max<uint32_t>(std::max<uint32_t>(maxw, 1), 514),
                                                      (150 * 1024 - fixed) / 4);   // >= 514: cum_s lives there first
     hipLaunchKernelGGL(k_dmatch, dim3((S + 255) / 256), dim3(256), 0, s, j, S);
-    hipLaunchKernelGGL(k_drans, dim3(S), dim3(DR_T), fixed + (size_t)wcap * 4, s, j, S, wcap);
+    const size_t stage = (j.dbg & 0x200) ? (size_t)wcap * 4 : (size_t)DR_RW * DR_T * 4;
+    hipLaunchKernelGGL(k_drans, dim3(S), dim3(DR_T), fixed + stage, s, j, S, wcap);
   } else {
     hipLaunchKernelGGL(k_drans_serial, dim3((S + 63) / 64), dim3(64), 0, s, j, S);
   }
