@@ -17,7 +17,13 @@
 // ring allows (only untiled images) read their neighbours from memory instead.
 #include "hoh_internal.h"
 
-#define RING 2048               // positions; the span in use is [q - w - 1 - 256, q + 512)
+// Ring of RING positions (stored twice): a block's writes land while the slowest wave may still
+// read the previous block's neighbourhood, so the span in use is [q - 256 - max(w + 1, 67), q + 512)
+// and RING >= 768 + max(w + 1, 67).  Tiles up to 511 wide (every tiled image) use 1280 positions
+// (10 KB: five workgroups per CU), up to 1279 wide 2048.
+#define RING_SMALL 1280
+#define RING_SMALL_MAX_W 511
+#define RING 2048
 #define RING_MAX_W 1200
 #define WTAB 512                // slots of a wave's fingerprint table (128 keys)
 #define CSET 512                // colour set slots (<= 257 colours are counted)
@@ -76,7 +82,7 @@ __device__ __forceinline__ uint32_t px_mem(const uint8_t* img, size_t pitch, int
   return p[0] | (p[1] << 8) | (p[2] << 16);
 }
 
-template <bool RINGED>
+template <bool RINGED, uint32_t RG>
 __device__ __forceinline__ void front_tile(const EncodeJob& j, uint32_t* ring) {
   __shared__ uint32_t wkey[4][WTAB + 1];
   __shared__ uint32_t wdup[4][WTAB / 32];
@@ -144,8 +150,8 @@ __device__ __forceinline__ void front_tile(const EncodeJob& j, uint32_t* ring) {
   uint32_t own = 0, nv[PF];
   if (RINGED) {
     own = load_px(tid);
-    ring[tid & (RING - 1)] = own;
-    ring[(tid & (RING - 1)) + RING] = own;
+    ring[tid] = own;                                 // tid < 256 < RG
+    ring[tid + RG] = own;
     advance();
 #pragma unroll
     for (int k = 1; k <= PF; k++) {
@@ -158,6 +164,7 @@ __device__ __forceinline__ void front_tile(const EncodeJob& j, uint32_t* ring) {
   while (cx >= (uint32_t)w) { cx -= w; cy++; }
   __syncthreads();
 
+  uint32_t ri = tid;                                 // (blk * NT + tid) % RG, kept incrementally
   uint32_t notgrey = 0;
   int ncand = 0;
   const uint32_t nblk = (npix + NT - 1) / NT;
@@ -166,9 +173,9 @@ __device__ __forceinline__ void front_tile(const EncodeJob& j, uint32_t* ring) {
     const uint32_t q = base + tid;
     uint32_t v;
     if (RINGED) {   // land block blk+1, issue block blk+1+PF into its slot
-      const uint32_t qn = base + NT + tid;
-      ring[qn & (RING - 1)] = slot;
-      ring[(qn & (RING - 1)) + RING] = slot;
+      const uint32_t rn = ri + NT >= RG ? ri + NT - RG : ri + NT;   // position base + NT + tid
+      ring[rn] = slot;
+      ring[rn + RG] = slot;
       v = own;
       own = slot;
       slot = load_px(base + (1 + PF) * NT + tid);
@@ -176,11 +183,12 @@ __device__ __forceinline__ void front_tile(const EncodeJob& j, uint32_t* ring) {
     } else {
       v = px_mem(img, pitch, w, npix, q);
     }
-    // forward / backward neighbours by raster distance: ring copies [ri] and [ri + RING] hold
+    // forward / backward neighbours by raster distance: ring copies [ri] and [ri + RG] hold
     // the same pixels, so q + k and q - d never wrap
-    const uint32_t ri = q & (RING - 1);
-    auto F = [&](uint32_t k) -> uint32_t { return RINGED ? ring[ri + k] : px_mem(img, pitch, w, npix, q + k); };
-    auto B = [&](uint32_t d) -> uint32_t { return RINGED ? ring[ri + RING - d] : px_mem(img, pitch, w, npix, q - d); };
+    const uint32_t rq = ri;
+    ri = ri + NT >= RG ? ri + NT - RG : ri + NT;
+    auto F = [&](uint32_t k) -> uint32_t { return RINGED ? ring[rq + k] : px_mem(img, pitch, w, npix, q + k); };
+    auto B = [&](uint32_t d) -> uint32_t { return RINGED ? ring[rq + RG - d] : px_mem(img, pitch, w, npix, q - d); };
     __syncthreads();
     const bool act = q < npix;
     if (act) {
@@ -315,12 +323,13 @@ __device__ __forceinline__ void front_tile(const EncodeJob& j, uint32_t* ring) {
   }
 }
 
+template <uint32_t RG>
 __global__ __launch_bounds__(NT) void k_front(EncodeJob j) {
-  __shared__ uint32_t ring[2 * RING];
-  front_tile<true>(j, ring);
+  __shared__ uint32_t ring[2 * RG];
+  front_tile<true, RG>(j, ring);
 }
 
-__global__ __launch_bounds__(NT) void k_front_wide(EncodeJob j) { front_tile<false>(j, nullptr); }
+__global__ __launch_bounds__(NT) void k_front_wide(EncodeJob j) { front_tile<false, 1>(j, nullptr); }
 
 // Indexed plane of a palette-candidate tile (choh.cpp:48-102 palette_encode + layer_encode -s0):
 // index = first-occurrence rank of the pixel's colour, then the MED fast-path residual at depth 8
@@ -397,6 +406,7 @@ void launch_palette(const EncodeJob& j, hipStream_t s) {
 }
 
 void launch_front(const EncodeJob& j, hipStream_t s) {
-  if (j.tw <= RING_MAX_W) hipLaunchKernelGGL(k_front, dim3(j.ntiles), dim3(NT), 0, s, j);
+  if (j.tw <= RING_SMALL_MAX_W) hipLaunchKernelGGL(k_front<RING_SMALL>, dim3(j.ntiles), dim3(NT), 0, s, j);
+  else if (j.tw <= RING_MAX_W) hipLaunchKernelGGL(k_front<RING>, dim3(j.ntiles), dim3(NT), 0, s, j);
   else hipLaunchKernelGGL(k_front_wide, dim3(j.ntiles), dim3(NT), 0, s, j);
 }
