@@ -152,6 +152,7 @@ __device__ __forceinline__ void front_tile(const EncodeJob& j, uint32_t* ring) {
     own = load_px(tid);
     ring[tid] = own;                                 // tid < 256 < RG
     ring[tid + RG] = own;
+    if (tid < 4) ring[tid + 2 * RG] = own;
     advance();
 #pragma unroll
     for (int k = 1; k <= PF; k++) {
@@ -176,6 +177,7 @@ __device__ __forceinline__ void front_tile(const EncodeJob& j, uint32_t* ring) {
       const uint32_t rn = ri + NT >= RG ? ri + NT - RG : ri + NT;   // position base + NT + tid
       ring[rn] = slot;
       ring[rn + RG] = slot;
+      if (rn < 4) ring[rn + 2 * RG] = slot;
       v = own;
       own = slot;
       slot = load_px(base + (1 + PF) * NT + tid);
@@ -184,7 +186,8 @@ __device__ __forceinline__ void front_tile(const EncodeJob& j, uint32_t* ring) {
       v = px_mem(img, pitch, w, npix, q);
     }
     // forward / backward neighbours by raster distance: ring copies [ri] and [ri + RG] hold
-    // the same pixels, so q + k and q - d never wrap
+    // the same pixels, so q + k and q - d never wrap; the LZ check's window q - b + 3 (b >= 1)
+    // reaches index ri + RG + 2, so slots 0..3 have a third copy at 2 RG
     const uint32_t rq = ri;
     ri = ri + NT >= RG ? ri + NT - RG : ri + NT;
     auto F = [&](uint32_t k) -> uint32_t { return RINGED ? ring[rq + k] : px_mem(img, pitch, w, npix, q + k); };
@@ -325,7 +328,7 @@ __device__ __forceinline__ void front_tile(const EncodeJob& j, uint32_t* ring) {
 
 template <uint32_t RG>
 __global__ __launch_bounds__(NT) void k_front(EncodeJob j) {
-  __shared__ uint32_t ring[2 * RG];
+  __shared__ uint32_t ring[2 * RG + 4];
   front_tile<true, RG>(j, ring);
 }
 

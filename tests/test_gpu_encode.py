@@ -40,6 +40,10 @@ def cases():
         y, x, L, b = rs.randint(0, 120), rs.randint(70, 1400), rs.randint(4, 60), rs.randint(1, 65)
         img[y, x:x + L] = img[y, x - b:x - b + L]
     out.append(("untiled1500x120-repeats", img))
+    # flat gradients (dense LZ candidates) at the widest tile each k_front pixel ring takes
+    out.append(("untiled511x200-lz", synth_rgb(511, 200, 16, 0)))
+    out.append(("untiled1200x120-lz", synth_rgb(1200, 120, 17, 0)))
+    out.append(("untiled512x100-lz", synth_rgb(512, 100, 18, 0)))
     out += palette_cases()
     return out
 
