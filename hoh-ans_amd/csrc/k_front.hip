@@ -19,10 +19,10 @@
 
 // Ring of RING positions (stored twice): a block's writes land while the slowest wave may still
 // read the previous block's neighbourhood, so the span in use is [q - 256 - max(w + 1, 67), q + 512)
-// and RING >= 768 + max(w + 1, 67).  Tiles up to 511 wide (every tiled image) use 1280 positions
-// (10 KB: five workgroups per CU), up to 1279 wide 2048.
-#define RING_SMALL 1280
-#define RING_SMALL_MAX_W 511
+// and RING >= 768 + max(w + 1, 67).  Tiles up to 271 wide (every tiled image) use 1040 positions
+// (8 KB; with the 256-bin G histogram a workgroup needs 26.4 KB: six per CU), up to 1279 wide 2048.
+#define RING_SMALL 1040
+#define RING_SMALL_MAX_W 271
 #define RING 2048
 #define RING_MAX_W 1200
 #define WTAB 512                // slots of a wave's fingerprint table (128 keys)
@@ -86,7 +86,7 @@ template <bool RINGED, uint32_t RG>
 __device__ __forceinline__ void front_tile(const EncodeJob& j, uint32_t* ring) {
   __shared__ uint32_t wkey[4][WTAB + 1];
   __shared__ uint32_t wdup[4][WTAB / 32];
-  __shared__ uint32_t hist[3][512];
+  __shared__ uint32_t hist[3 * 512 - 256];         // G: 256 bins at 0, R': 512 at 256, B': 512 at 768
   __shared__ uint32_t hset[CSET];
   __shared__ uint32_t hpos[CSET];                   // first raster position of each colour
   __shared__ int s_ncol, s_notgrey, s_ncand, s_np;
@@ -96,7 +96,7 @@ __device__ __forceinline__ void front_tile(const EncodeJob& j, uint32_t* ring) {
   const int x0 = (gt % j.xt) * j.tw, y0 = (gt / j.xt) * j.th;
   const int w = min(j.tw, j.W - x0), h = min(j.th, j.H - y0);
   const uint32_t npix = (uint32_t)w * h;
-  for (int i = tid; i < 3 * 512; i += NT) (&hist[0][0])[i] = 0;
+  for (int i = tid; i < 3 * 512 - 256; i += NT) hist[i] = 0;
   for (int i = tid; i < CSET; i += NT) { hset[i] = 0xffffffffu; hpos[i] = 0xffffffffu; }
   for (int i = lane; i <= WTAB; i += 64) wkey[wv][i] = 0;
   if (lane < WTAB / 32) wdup[wv][lane] = 0;
@@ -229,9 +229,9 @@ __device__ __forceinline__ void front_tile(const EncodeJob& j, uint32_t* ring) {
       res1[q] = (uint16_t)rr;
       res2[q] = (uint16_t)rb;
       if (!(j.dbg & 2)) {
-        atomicAdd(&hist[0][rg], 1u);
-        atomicAdd(&hist[1][rr], 1u);
-        atomicAdd(&hist[2][rb], 1u);
+        atomicAdd(&hist[rg], 1u);
+        atomicAdd(&hist[256 + rr], 1u);
+        atomicAdd(&hist[768 + rb], 1u);
       }
     }
     cx += NT;
@@ -285,7 +285,7 @@ __device__ __forceinline__ void front_tile(const EncodeJob& j, uint32_t* ring) {
   __syncthreads();
   for (int i = tid; i < 3 * 512; i += NT) {
     const int k = i / 512, s = i % 512;
-    j.hist[(size_t)(t * j.spt + med_kind(j, k)) * 512 + s] = hist[k][s];
+    j.hist[(size_t)(t * j.spt + med_kind(j, k)) * 512 + s] = k == 0 ? (s < 256 ? hist[s] : 0u) : hist[k * 512 - 256 + s];
   }
   if (s_ncol <= 256 && s_notgrey) {
     // palette in first-occurrence order (choh.cpp:64-88): rank of a colour = number of colours

@@ -41,6 +41,7 @@ def cases():
         img[y, x:x + L] = img[y, x - b:x - b + L]
     out.append(("untiled1500x120-repeats", img))
     # flat gradients (dense LZ candidates) at the widest tile each k_front pixel ring takes
+    out.append(("untiled271x200-lz", synth_rgb(271, 200, 19, 0)))
     out.append(("untiled511x200-lz", synth_rgb(511, 200, 16, 0)))
     out.append(("untiled1200x120-lz", synth_rgb(1200, 120, 17, 0)))
     out.append(("untiled512x100-lz", synth_rgb(512, 100, 18, 0)))
