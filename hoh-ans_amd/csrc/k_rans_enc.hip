@@ -112,7 +112,7 @@ __device__ __forceinline__ void ckpt(const Coder& c, Checkpoint* ck, uint32_t k)
   ck[k] = p;
 }
 
-template <int LANES, int WAVES = 1>
+template <int LANES, int WAVES = 1, bool DEEP = false>
 __global__ __launch_bounds__(64 * WAVES) void k_rans_fast(EncodeJob j, int nplane, SidMap ma, int na, SidMap mb,
                                                           int nblk, int rot) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -145,7 +145,40 @@ __global__ __launch_bounds__(64 * WAVES) void k_rans_fast(EncodeJob j, int nplan
   for (uint32_t i = n; i > n - r; i--) step15(c, ent(tb, tbase + (uint32_t)sp[i - 1] * 16u));
   flush_win(c);
   if (((nb * 8) % HOH_SEG) == 0 && nb * 8 < n) ckpt(c, ck, nb * 8 / HOH_SEG);
-  if (nb) {
+  if (DEEP && nb) {
+    // table entries gathered 16 steps ahead (two 8-symbol blocks per buffer): with several images
+    // in flight the 8 KB-per-stream tables live in MALL/HBM rather than L2, and an 8-step lead
+    // left the chain waiting on the gather (15 % of its time even alone; four 8-entry buffers
+    // 24 steps ahead, or unconditional gathers past the stream's start, measured slower)
+    const uint4* sp4 = (const uint4*)sp;
+    const int np = (int)nb / 2;                    // pairs of blocks, even
+    EncFast eA[16], eB[16];
+    auto syms = [&](int p, uint4& hi, uint4& lo) { hi = sp4[2 * p + 1]; lo = sp4[2 * p]; };
+    auto look = [&](EncFast* e, const uint4& hi, const uint4& lo) {
+      lookup8(e, hi, tb, tbase);
+      lookup8(e + 8, lo, tb, tbase);
+    };
+    auto run = [&](const EncFast* e, int p) {
+#pragma unroll
+      for (int k = 7; k >= 0; --k) step15(c, e[k]);
+      if (((2 * p + 1) & (HOH_SEG / 8 - 1)) == 0) ckpt(c, ck, (uint32_t)(2 * p + 1) * 8 / HOH_SEG);
+#pragma unroll
+      for (int k = 7; k >= 0; --k) step15(c, e[8 + k]);
+      if (((2 * p) & (HOH_SEG / 8 - 1)) == 0) ckpt(c, ck, (uint32_t)(2 * p) * 8 / HOH_SEG);
+    };
+    uint4 h, l;
+    syms(np - 1, h, l); look(eA, h, l);
+    syms(np - 2, h, l); look(eB, h, l);
+    if (np >= 3) syms(np - 3, h, l);
+    for (int p = np - 1; p >= 1; p -= 2) {
+      // entering: eA = pair p, eB = pair p-1 (in flight), {h, l} = symbols of pair p-2
+      run(eA, p);
+      if (p >= 2) { look(eA, h, l); if (p >= 3) syms(p - 3, h, l); }
+      run(eB, p - 1);
+      if (p >= 3) { look(eB, h, l); if (p >= 4) syms(p - 4, h, l); }
+      flush_win(c);
+    }
+  } else if (nb) {
     const uint4* sp4 = (const uint4*)sp;
     EncFast eA[8], eB[8];
     uint4 s1 = sp4[nb - 2];
@@ -254,9 +287,12 @@ void launch_rans_fast(const EncodeJob& j, int nplane, hipStream_t s, SidMap a, i
     hipLaunchKernelGGL(k_rans_fast<32>, dim3(grid), dim3(64), 32 * WIN * 4, s, j, nplane, a, na, b, nblk, rot);
   } else if (lanes == 8) {
     hipLaunchKernelGGL(k_rans_fast<8>, dim3(grid), dim3(64), 8 * WIN * 4, s, j, nplane, a, na, b, nblk, rot);
-  } else {
+  } else if (j.dbg & 0x8000) {   // measurement: table gathers 8 steps ahead
     hipLaunchKernelGGL(k_rans_fast<64>, dim3(grid), dim3(64), std::max<size_t>(64 * WIN * 4, pad), s, j, nplane, a, na,
                        b, nblk, rot);
+  } else {
+    hipLaunchKernelGGL((k_rans_fast<64, 1, true>), dim3(grid), dim3(64), std::max<size_t>(64 * WIN * 4, pad), s, j,
+                       nplane, a, na, b, nblk, rot);
   }
 }
 
