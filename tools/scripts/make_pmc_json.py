@@ -3,8 +3,16 @@
 # 128-B request for wide (16 B/lane) streaming reads, so it is doubled ("fetch_corrected").
 import csv, collections, json, sys
 
-KMAP = {"k_rans_fast<64>": "rans_enc_fast", "k_front": "front", "k_drans": "drans",
+KMAP = {"k_rans_fast<64": "rans_enc_fast", "k_front<": "front", "k_drans": "drans",
         "k_dunpred_fast": "dunpred_fast", "k_tables": "tables", "k_streambytes": "streambytes"}
+
+
+def kname(k):
+    """stage name of a kernel (template arguments vary: match by prefix)"""
+    for pre, name in KMAP.items():
+        if k == pre or k.startswith(pre):
+            return name
+    return k
 
 
 def per_kernel(path, counter):
@@ -26,7 +34,7 @@ out = {"W": 8192, "H": 8192, "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE
 for k in sorted(set(fetch) | set(write)):
     f = fetch.get(k, 0.0) * 1024
     w = write.get(k, 0.0) * 1024
-    name = KMAP.get(k, k)
+    name = kname(k)
     out["kernels"][name] = {"kernel": k, "fetch_raw": round(f), "fetch_corrected": round(2 * f),
                             "write": round(w), "hbm_bytes_per_launch": round(2 * f + w)}
 json.dump(out, open(sys.argv[3], "w"), indent=1)
