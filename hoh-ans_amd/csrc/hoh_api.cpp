@@ -379,7 +379,9 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   j.cap = cap;
   j.prefix = prefix;
   j.write_table = write_table;
-  if (hipMemsetAsync(j.candbits, 0, (size_t)ntiles * (j.npix_cap / 64) * 8, s) != hipSuccess) return HOH_E_HIP;
+  // at -s0 k_front writes every candidate word of every tile (k_lz reads no others)
+  if ((speed || (j.dbg & 4)) &&
+      hipMemsetAsync(j.candbits, 0, (size_t)ntiles * (j.npix_cap / 64) * 8, s) != hipSuccess) return HOH_E_HIP;
   if (hipMemsetAsync(c->misc.p, 0, 64, s) != hipSuccess) return HOH_E_HIP;
   prof.mark("memset");
   launch_front(j, s);            prof.mark("front");
