@@ -345,7 +345,7 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   if ((e = ensure(c->hist, S * 512 * 4))) return e;
   if ((e = ensure(c->candbits, (size_t)ntiles * (j.npix_cap / 64) * 8))) return e;
   if ((e = ensure(c->matches, (size_t)ntiles * 3 * (j.lz_cap + 1) * 4))) return e;
-  if ((e = ensure(c->pal, (size_t)ntiles * 256 * 4))) return e;
+  if ((e = ensure(c->pal, (size_t)ntiles * 257 * 4))) return e;   // palettes, then colour counts
   if ((e = ensure(c->streams, S * sizeof(StreamInfo)))) return e;
   if ((e = ensure(c->tiles, (size_t)ntiles * sizeof(TileInfo)))) return e;
   if ((e = ensure(c->hdr, S * HOH_HDR_CAP))) return e;
@@ -358,6 +358,7 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   j.candbits = (uint64_t*)c->candbits.p;
   j.matches = (uint32_t*)c->matches.p;
   j.palette = (uint32_t*)c->pal.p;
+  j.ncol = (int32_t*)c->pal.p + (size_t)ntiles * 256;
   j.streams = (StreamInfo*)c->streams.p;
   j.tiles = (TileInfo*)c->tiles.p;
   j.hdr = (uint8_t*)c->hdr.p;

@@ -159,6 +159,7 @@ struct EncodeJob {
   uint64_t* candbits;     // [tile][npix_cap/64] LZ candidate bitmap
   uint32_t* matches;      // [tile][lz_cap] packed (pos, len, back) triples (3 words each)
   uint32_t* palette;      // [tile][256] colours in first-occurrence order (palette tiles)
+  int32_t* ncol;          // [tile] distinct colours (<= 256) or -1 (k_colours)
   uint8_t* idx8;          // -s>=1: [tile][npix_cap] palette indices (the indexed plane's data)
   uint32_t* fpb;          // -s>=1: [tile][npix_cap] 4-pixel window fingerprints (LZ)
   PlaneInfo* pinfo;       // -s>=1: [tile][6]

@@ -87,9 +87,7 @@ __device__ __forceinline__ void front_tile(const EncodeJob& j, uint32_t* ring) {
   __shared__ uint32_t wkey[4][WTAB + 1];
   __shared__ uint32_t wdup[4][WTAB / 32];
   __shared__ uint32_t hist[3 * 512 - 256];         // G: 256 bins at 0, R': 512 at 256, B': 512 at 768
-  __shared__ uint32_t hset[CSET];
-  __shared__ uint32_t hpos[CSET];                   // first raster position of each colour
-  __shared__ int s_ncol, s_notgrey, s_ncand, s_np;
+  __shared__ int s_notgrey, s_ncand;
 
   const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int gt = j.t0 + t;
@@ -97,10 +95,9 @@ __device__ __forceinline__ void front_tile(const EncodeJob& j, uint32_t* ring) {
   const int w = min(j.tw, j.W - x0), h = min(j.th, j.H - y0);
   const uint32_t npix = (uint32_t)w * h;
   for (int i = tid; i < 3 * 512 - 256; i += NT) hist[i] = 0;
-  for (int i = tid; i < CSET; i += NT) { hset[i] = 0xffffffffu; hpos[i] = 0xffffffffu; }
   for (int i = lane; i <= WTAB; i += 64) wkey[wv][i] = 0;
   if (lane < WTAB / 32) wdup[wv][lane] = 0;
-  if (tid == 0) { s_ncol = 0; s_notgrey = 0; s_ncand = 0; s_np = 0; }
+  if (tid == 0) { s_notgrey = 0; s_ncand = 0; }
 
   uint16_t* res0 = j.sym + med_plane_off(j, t, 0);
   uint16_t* res1 = j.sym + med_plane_off(j, t, 1);
@@ -197,15 +194,6 @@ __device__ __forceinline__ void front_tile(const EncodeJob& j, uint32_t* ring) {
     if (act) {
       const uint32_t g = (v >> 8) & 255u;
       notgrey |= (v ^ (g * 0x010101u)) & 0xffffffu;
-      if (__builtin_amdgcn_readfirstlane(s_ncol) <= 256 && !(j.dbg & 1)) {   // distinct colours, stop past 256
-        uint32_t hsh = (v * 2654435761u) >> 23;
-        for (int probe = 0; probe < CSET; probe++) {
-          uint32_t old = atomicCAS(&hset[hsh], 0xffffffffu, v);
-          if (old == 0xffffffffu) { atomicAdd(&s_ncol, 1); atomicMin(&hpos[hsh], q); break; }
-          if (old == v) { atomicMin(&hpos[hsh], q); break; }
-          hsh = (hsh + 1) & (CSET - 1);
-        }
-      }
       // neighbours; outside the tile the reference uses c/2 in every plane (prediction.hpp:21-28),
       // i.e. the grey pixel 128,128,128 (G = 128, R' = B' = 256)
       const bool hasL = cx > 0, hasT = cy > 0;
@@ -287,30 +275,10 @@ __device__ __forceinline__ void front_tile(const EncodeJob& j, uint32_t* ring) {
     const int k = i / 512, s = i % 512;
     j.hist[(size_t)(t * j.spt + med_kind(j, k)) * 512 + s] = k == 0 ? (s < 256 ? hist[s] : 0u) : hist[k * 512 - 256 + s];
   }
-  if (s_ncol <= 256 && s_notgrey) {
-    // palette in first-occurrence order (choh.cpp:64-88): rank of a colour = number of colours
-    // whose first position is smaller
-    uint32_t* pc = &wkey[0][0];
-    uint32_t* pp = &wkey[0][0] + 256;
-    for (int i = tid; i < CSET; i += NT) {
-      if (hset[i] != 0xffffffffu) {
-        const int k = atomicAdd(&s_np, 1);
-        pc[k] = hset[i];
-        pp[k] = hpos[i];
-      }
-    }
-    __syncthreads();
-    if (tid < s_np) {
-      const uint32_t me = pp[tid];
-      uint32_t rank = 0;
-      for (int m = 0; m < s_np; m++) rank += pp[m] < me;
-      j.palette[(size_t)t * 256 + rank] = pc[tid];
-    }
-  }
   if (tid == 0) {
     TileInfo ti;
     ti.x0 = x0; ti.y0 = y0; ti.w = w; ti.h = h;
-    ti.colours = s_ncol > 256 ? -1 : s_ncol;
+    ti.colours = j.ncol[t];                          // k_colours ran before this kernel
     uint32_t fl = 0;
     if (!s_notgrey) fl |= TF_GREY;
     if (!s_notgrey && ti.colours != -1 && ti.colours <= 2) fl |= TF_BINARY;
@@ -324,6 +292,66 @@ __device__ __forceinline__ void front_tile(const EncodeJob& j, uint32_t* ring) {
     ti.pad = 0;
     j.tiles[t] = ti;
   }
+}
+
+// Distinct colours of each tile, capped at 257 (choh.cpp:17-46), and for tiles with <= 256 the
+// palette in first-occurrence order (choh.cpp:64-88).  One workgroup per tile walks raster blocks
+// and stops as soon as a tile has shown 257 colours, which natural tiles do within a block or
+// two, so k_front carries no colour set (and fits seven workgroups per CU).
+__global__ __launch_bounds__(NT) void k_colours(EncodeJob j) {
+  __shared__ uint32_t hset[CSET];
+  __shared__ uint32_t hpos[CSET];                   // first raster position of each colour
+  __shared__ uint32_t pc[256], pp[256];
+  __shared__ int s_ncol, s_np;
+  const int t = blockIdx.x, tid = threadIdx.x;
+  const int gt = j.t0 + t;
+  const int x0 = (gt % j.xt) * j.tw, y0 = (gt / j.xt) * j.th;
+  const int w = min(j.tw, j.W - x0), h = min(j.th, j.H - y0);
+  const uint32_t npix = (uint32_t)w * h;
+  const uint8_t* img = j.rgb + ((size_t)y0 * j.W + x0) * 3;
+  const size_t pitch = (size_t)j.W * 3;
+  for (int i = tid; i < CSET; i += NT) { hset[i] = 0xffffffffu; hpos[i] = 0xffffffffu; }
+  if (tid == 0) { s_ncol = 0; s_np = 0; }
+  uint32_t x = tid, y = 0;
+  while (x >= (uint32_t)w) { x -= w; y++; }
+  __syncthreads();
+  for (uint32_t q = tid; q - tid < npix; q += NT) {
+    if (q < npix) {
+      const uint8_t* p = img + (size_t)y * pitch + (size_t)x * 3;
+      const uint32_t v = p[0] | (p[1] << 8) | (p[2] << 16);
+      uint32_t hsh = (v * 2654435761u) >> 23;
+      for (int probe = 0; probe < CSET; probe++) {
+        const uint32_t old = atomicCAS(&hset[hsh], 0xffffffffu, v);
+        if (old == 0xffffffffu) { atomicAdd(&s_ncol, 1); atomicMin(&hpos[hsh], q); break; }
+        if (old == v) { atomicMin(&hpos[hsh], q); break; }
+        hsh = (hsh + 1) & (CSET - 1);
+      }
+    }
+    x += NT;
+    while (x >= (uint32_t)w) { x -= w; y++; }
+    __syncthreads();
+    if (s_ncol > 256) break;                         // block-uniform after the barrier
+  }
+  if (s_ncol > 256) {
+    if (tid == 0) j.ncol[t] = -1;
+    return;
+  }
+  // rank of a colour = number of colours whose first position is smaller
+  for (int i = tid; i < CSET; i += NT) {
+    if (hset[i] != 0xffffffffu) {
+      const int k = atomicAdd(&s_np, 1);
+      pc[k] = hset[i];
+      pp[k] = hpos[i];
+    }
+  }
+  __syncthreads();
+  if (tid < s_np) {
+    const uint32_t me = pp[tid];
+    uint32_t rank = 0;
+    for (int m = 0; m < s_np; m++) rank += pp[m] < me;
+    j.palette[(size_t)t * 256 + rank] = pc[tid];
+  }
+  if (tid == 0) j.ncol[t] = s_ncol;
 }
 
 template <uint32_t RG>
@@ -409,6 +437,7 @@ void launch_palette(const EncodeJob& j, hipStream_t s) {
 }
 
 void launch_front(const EncodeJob& j, hipStream_t s) {
+  hipLaunchKernelGGL(k_colours, dim3(j.ntiles), dim3(NT), 0, s, j);
   if (j.tw <= RING_SMALL_MAX_W) hipLaunchKernelGGL(k_front<RING_SMALL>, dim3(j.ntiles), dim3(NT), 0, s, j);
   else if (j.tw <= RING_MAX_W) hipLaunchKernelGGL(k_front<RING>, dim3(j.ntiles), dim3(NT), 0, s, j);
   else hipLaunchKernelGGL(k_front_wide, dim3(j.ntiles), dim3(NT), 0, s, j);
