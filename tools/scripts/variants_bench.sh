@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 cp hoh-ans_amd/lib/libhohgpu.so /tmp/orig.so
 first=$(ls variants/*.so | head -1)
 cp $first hoh-ans_amd/lib/libhohgpu.so
-timeout -k 10 400 python -u -m pytest tests/test_gpu_encode.py -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/t.log 2>&1 || { tail -20 gpurun_out/t.log; cp /tmp/orig.so hoh-ans_amd/lib/libhohgpu.so; exit 1; }
+timeout -k 10 400 python -u -m pytest ${VT:-tests/test_gpu_encode.py} -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/t.log 2>&1 || { tail -20 gpurun_out/t.log; cp /tmp/orig.so hoh-ans_amd/lib/libhohgpu.so; exit 1; }
 echo "$first: $(tail -1 gpurun_out/t.log)"
 for r in 1 2; do
   for v in variants/*.so; do
