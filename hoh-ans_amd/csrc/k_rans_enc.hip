@@ -267,8 +267,8 @@ void launch_rans_fast(const EncodeJob& j, int nplane, hipStream_t s, SidMap a, i
   // spreads an image's 48 chains over 48 CUs.  The grid covers the chip with a per-launch rotation
   // so that the chains of images in flight land on different CUs.  Measurement knobs: dbg bit 23 =
   // two chain waves per workgroup with an 81 KB request (one workgroup, i.e. two chains, per CU:
-  // 40 KB of LDS per chain; +2 % bench throughput at 12 in flight but 25 % slower chains for one
-  // image alone, so not the default), bits 8..14 = lanes per wave, bits 24..31 = the request in KB.
+  // 40 KB of LDS per chain; 25 % slower chains for one image alone, and with the 16-step gathers
+  // 2-4 % lower bench throughput), bits 8..14 = lanes per wave, bits 24..31 = the request in KB.
   const bool one = !(j.dbg & 0x800000) || ((j.dbg >> 8) & 127);
   const int lanes = (j.dbg >> 8) & 127 ? (j.dbg >> 8) & 127 : 64;
   const int waves = one ? 1 : 2;
@@ -279,7 +279,7 @@ void launch_rans_fast(const EncodeJob& j, int nplane, hipStream_t s, SidMap a, i
   const int rot = grid == nblk ? 0 : (int)((g_rot.fetch_add(1) * 8u * (unsigned)((nblk + 7) / 8)) % (unsigned)grid);
   const size_t pad = (j.dbg >> 24) ? (size_t)((j.dbg >> 24) & 255) * 1024 : (size_t)(one ? 56 : 81) * 1024;
   if (!one) {
-    hipLaunchKernelGGL((k_rans_fast<64, 2>), dim3(grid), dim3(128), std::max<size_t>(128 * WIN * 4, pad), s, j, nplane,
+    hipLaunchKernelGGL((k_rans_fast<64, 2, true>), dim3(grid), dim3(128), std::max<size_t>(128 * WIN * 4, pad), s, j, nplane,
                        a, na, b, nblk, rot);
   } else if (lanes == 16) {
     hipLaunchKernelGGL(k_rans_fast<16>, dim3(grid), dim3(64), 16 * WIN * 4, s, j, nplane, a, na, b, nblk, rot);
