@@ -15,7 +15,7 @@ One step = one pass of the hot path over the workload, inputs resident in HBM:
          .hoh is assembled (prefix + concatenation; byte-identical to a 1-GPU encode), and
          decode the shard (hoh_decode_tiles).
 value = raw RGB bytes of all ranks x K / max-over-ranks(time of the K steps) / 1e6.
-Images in flight (--inflight; default 16 at N = 1, 12 at N > 1): each GPU keeps D images in
+Images in flight (--inflight; default 20 at N = 1, 12 at N > 1): each GPU keeps D images in
 flight, one library context,
 HIP stream and hardware queue per slot (GPU_MAX_HW_QUEUES raised to D), steps dealt round-robin
 to the slots.  At N = 1 one host thread enqueues every step through the enqueue-only calls
@@ -144,10 +144,10 @@ def main():
                          "enqueue-only calls from one thread")
     ap.add_argument("--inflight", type=int, default=0,
                     help="images in flight per GPU (each with its own context/stream); 1 = one at a time; "
-                         "default 16 at N = 1 (enqueue-only lanes), 12 at N > 1 (a process group per lane)")
+                         "default 20 at N = 1 (enqueue-only lanes), 12 at N > 1 (a process group per lane)")
     args = ap.parse_args()
     if args.inflight <= 0:
-        args.inflight = 16 if int(os.environ.get("WORLD_SIZE", "1")) == 1 else 12
+        args.inflight = 20 if int(os.environ.get("WORLD_SIZE", "1")) == 1 else 12
     # one hardware queue per in-flight image (HIP reads this at runtime init; <= 32 allowed here)
     try:
         q = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
