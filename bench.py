@@ -131,7 +131,7 @@ def pmc_traffic(kernel, W, H):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=96)
+    ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=12)
     ap.add_argument("--size", type=int, default=8192, help="image width; height per GPU")
     ap.add_argument("--seed", type=int, default=1)
