@@ -4,7 +4,8 @@
 //    (prediction.hpp:6-44), written to the residual arena, histograms in LDS.  A pixel is kept
 //    as {R' | B' << 16, rgb}: the two 9-bit planes go through packed 16-bit arithmetic (the
 //    uint16 gradient wrap of Q8 is exactly the packed u16 wrap), G through SDWA byte selects;
-//  * grey test (channel.hpp:21-31) and distinct-colour count capped at 257 (choh.cpp:17-46);
+//  * grey test (channel.hpp:21-31); the distinct-colour count capped at 257 (choh.cpp:17-46)
+//    and the palette order come from k_colours, launched just before (early exit per tile);
 //  * LZ candidate detection for find_lz_rgb at -s0 (lz.hpp:32-53): a position q is a candidate
 //    iff some back distance b in [1, min(64, q)] gives 4 equal RGB pixels q..q+3 vs q-b..q-b+3.
 //    Each wave fingerprints the 4-pixel windows of its 64 positions and of the 64 before them,
@@ -12,7 +13,8 @@
 //    (b = 1..64, first hit wins) only positions whose fingerprint occurs twice; equal windows
 //    have equal fingerprints, so the candidate set is exact.  The greedy selection runs in
 //    k_lz.hip over the (sparse) candidate bitmap.
-// Pixels live in an LDS ring (stored twice, so reads at q+k and q-d never wrap); every pixel is
+// Pixels live in an LDS ring (stored twice, plus a third copy of slots 0..3 for the LZ check's
+// window, so reads at q+k and q-d never wrap); every pixel is
 // read from HBM once (one unaligned dword), one block ahead of its use.  Tiles wider than the
 // ring allows (only untiled images) read their neighbours from memory instead.
 #include "hoh_internal.h"
