@@ -15,6 +15,7 @@
 #include <string>
 
 void launch_synth(uint8_t* rgb, int W, int H, int y0, uint64_t seed, int noise, hipStream_t s);
+void launch_natural(uint8_t* rgb, int W, int rows, int y0, uint64_t seed, hipStream_t s);
 void launch_put_bytes(uint8_t* dst, const uint8_t* b, int n, hipStream_t s);
 void launch_status_enc(const uint32_t* gerr, const uint64_t* total, uint64_t cap, uint64_t* out, hipStream_t s);
 
@@ -51,7 +52,6 @@ struct hoh_ctx {
   int device = 0;
   hipStream_t own = nullptr;
   Buf idx8, fpb, pinfo, lg;     // -s>=1 workspaces
-  Buf dbgb;                     // measurement stamps
   uint32_t lg_key[4] = {0, 0, 0, 0};
   uint64_t lg_off[4] = {0, 0, 0, 0};
   Buf sym, hist, candbits, matches, pal, streams, tiles, hdr, tab_fast, tab_gen, slabs, ckpt, misc, tsizes;
@@ -151,7 +151,7 @@ static void freebuf(Buf& b) { if (b.p) (void)hipFree(b.p); b.p = nullptr; b.n = 
 void hoh_ctx_destroy(hoh_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  Buf* all[] = {&c->dbgb, &c->idx8, &c->fpb, &c->pinfo, &c->lg, &c->sym, &c->hist, &c->candbits, &c->matches, &c->pal, &c->streams, &c->tiles, &c->hdr,
+  Buf* all[] = {&c->idx8, &c->fpb, &c->pinfo, &c->lg, &c->sym, &c->hist, &c->candbits, &c->matches, &c->pal, &c->streams, &c->tiles, &c->hdr,
                 &c->tab_fast, &c->tab_gen, &c->slabs, &c->ckpt, &c->misc, &c->tsizes};
   for (Buf* b : all) freebuf(*b);
   dec_free(c->dec);
@@ -308,10 +308,6 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   Prof prof(c, s, async);
   EncodeJob j;
   memset(&j, 0, sizeof(j));
-  {
-    const char* e = getenv("HOH_ENC_DBG");
-    j.dbg = e ? (uint32_t)atoi(e) : 0;
-  }
   j.speed = speed;
   j.spt = speed ? SPT_S : SK_PER_TILE;
   j.rgb = d_rgb; j.W = W; j.H = H;
@@ -381,7 +377,7 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   j.prefix = prefix;
   j.write_table = write_table;
   // at -s0 k_front writes every candidate word of every tile (k_lz reads no others)
-  if ((speed || (j.dbg & 4)) &&
+  if (speed &&
       hipMemsetAsync(j.candbits, 0, (size_t)ntiles * (j.npix_cap / 64) * 8, s) != hipSuccess) return HOH_E_HIP;
   if (hipMemsetAsync(c->misc.p, 0, 64, s) != hipSuccess) return HOH_E_HIP;
   prof.mark("memset");
@@ -392,43 +388,14 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
     if (hipGetLastError() != hipSuccess) return HOH_E_HIP;
     idx = nullptr;
   } else {
-  // (HOH_ENC_DBG bits 16..19 stop after a stage: pipelined cost per stage, output invalid)
-  do {
-    if (j.dbg & 0x10000) break;
     launch_lz(j, s);
     launch_nuke(j, s);             prof.mark("lz");
-    if (j.dbg & 0x20000) break;
     launch_tables(j, (int)S, s);   prof.mark("tables");
-    if (j.dbg & 0x40000) break;
-    if ((j.dbg & 0x200000) && !async) {
-      if ((e = ensure(c->dbgb, (size_t)ntiles * 4 * 16))) return e;
-      j.dbgbuf = (uint64_t*)c->dbgb.p;
-      (void)hipMemsetAsync(j.dbgbuf, 0, (size_t)ntiles * 4 * 16, s);
-    }
     launch_rans_fast(j, ntiles * 4, s, SidMap{3, SK_G}, ntiles * 3, SidMap{1, SK_I}); prof.mark("rans_enc_fast");
-    if ((j.dbg & 0x200000) && !async) {
-      // per workgroup: start / end (100 MHz); print the spread of one launch
-      const int nb = (ntiles * 4 + 63) / 64;
-      std::vector<uint64_t> h((size_t)nb * 2);
-      (void)hipMemcpyAsync(h.data(), j.dbgbuf, h.size() * 8, hipMemcpyDeviceToHost, s);
-      (void)hipStreamSynchronize(s);
-      uint64_t b0 = ~0ull, e1 = 0, dsum = 0, dmax = 0;
-      int n = 0;
-      for (int i = 0; i < nb; i++) {
-        if (!h[2 * i]) continue;
-        b0 = std::min(b0, h[2 * i]); e1 = std::max(e1, h[2 * i + 1]);
-        const uint64_t d = h[2 * i + 1] - h[2 * i];
-        dsum += d; dmax = std::max(dmax, d); n++;
-      }
-      if (n) fprintf(stderr, "rans_fast: %d WGs, span %.0f us, mean %.0f us, max %.0f us, last start +%.0f us\n", n,
-                     (e1 - b0) / 100.0, dsum / 100.0 / n, dmax / 100.0, 0.0);
-    }
     launch_rans_gen(j, (int)S, s); prof.mark("rans_enc_gen");
-    if (j.dbg & 0x80000) break;
     launch_finalize(j, (int)S, s); prof.mark("finalize");
     launch_layout(j, s);           prof.mark("layout");
     launch_assemble(j, (int)S, s); prof.mark("assemble");
-  } while (0);
   }
   if (hipGetLastError() != hipSuccess) return HOH_E_HIP;
   if (idx) {
@@ -549,6 +516,15 @@ int hoh_synth_rgb_rows(hoh_ctx* c, uint8_t* d_rgb, int W, int y0, int rows, uint
   (void)hipSetDevice(c->device);
   hipStream_t s = pick(c, stream);
   launch_synth(d_rgb, W, rows, y0, seed, noise, s);
+  if (hipGetLastError() != hipSuccess) return HOH_E_HIP;
+  return hipStreamSynchronize(s) == hipSuccess ? HOH_OK : HOH_E_HIP;
+}
+
+int hoh_natural_rgb_rows(hoh_ctx* c, uint8_t* d_rgb, int W, int y0, int rows, uint64_t seed, void* stream) {
+  if (!c || !d_rgb || W <= 0 || rows <= 0 || y0 < 0 || W >= (1 << 24) || y0 + rows >= (1 << 24)) return HOH_E_ARG;
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick(c, stream);
+  launch_natural(d_rgb, W, rows, y0, seed, s);
   if (hipGetLastError() != hipSuccess) return HOH_E_HIP;
   return hipStreamSynchronize(s) == hipSuccess ? HOH_OK : HOH_E_HIP;
 }

@@ -149,8 +149,6 @@ struct EncodeJob {
   int t0, ntiles;         // tiles [t0, t0 + ntiles) of the image are coded
   uint32_t npix_cap;      // max pixels of one tile (per-plane stride of the residual arena)
   uint32_t lz_cap;        // symbols per LZ stream slot
-  uint32_t dbg;           // measurement knobs (HOH_ENC_DBG), 0 in production
-  uint64_t* dbgbuf;       // measurement: per-workgroup s_memrealtime stamps (dbg bit 21)
   int speed;              // cruncher_mode (-sN)
   int spt;                // streams per tile: SK_PER_TILE (-s0) or SPT_S
   // arenas

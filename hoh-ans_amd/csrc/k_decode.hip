@@ -39,8 +39,6 @@ struct DecJob {
   uint32_t* matches;            // [tile][lz_cap+1][4]: pixel index, length, back, nuked before
   int lzband;                   // rows per band of k_dunpred_lz (LDS-bound)
   uint32_t* lzt;                // tiles with LZ copies (w >= 64), appended by k_dlz; count in gerr[2]
-  uint32_t dbg;                 // measurement knobs (HOH_DEC_DBG), 0 in production
-  uint64_t* dbgbuf;             // per-workgroup s_memtime stamps when dbg & 16
   uint8_t* rgb;                 // output image
   uint32_t* gerr;
   const IndexStream* ix;        // optional side index
@@ -459,10 +457,10 @@ struct DrTables {
 // Indexed decode (rans64.hpp:107-142): one 256-thread workgroup per stream, thread = segment of
 // HOH_SEG symbols starting from the encoder's checkpoint.  LDS holds the lookup tables (12 KB) and
 // a 16-word payload ring per thread (16 KB), refilled from the file 4 words a group ahead, so the
-// per-symbol chain is LDS round trips only and five workgroups fit a CU (staging the whole payload,
-// HOH_DEC_DBG 0x200, needs a 40 KB stage and allows three); the symbol stores are never awaited.
+// per-symbol chain is LDS round trips only and five workgroups fit a CU (staging the whole payload
+// needed a 40 KB stage and allowed three); the symbol stores are never awaited.
 // Output is the flat plane: each thread stores its segment 16 symbols (32 B) at a time.
-__global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams, uint32_t wcap) {
+__global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams) {
   extern __shared__ __attribute__((aligned(16))) uint32_t dr_lds[];
   if (dec_abort(j)) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -470,14 +468,12 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams, uint32_t
   const DecStream d = j.streams[sid];
   if (d.mode == SM_STORED) { dec_stored(j, sid, d); return; }     // no separate launch
   if (d.mode != SM_RANS || d.range > 512 || d.pb > 15) return;
-  uint64_t T0 = 0, T1 = 0;
-  if (j.dbg & 16) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(T0)::"memory");
   const uint32_t pb = d.pb, M = 1u << pb, mask = M - 1, range = d.range;
   DrTables tb;
   tb.bk = (uint2*)dr_lds;                                     // 2 * DR_NB words
   tb.sy = (uint2*)(dr_lds + 2 * DR_NB);                       // 2 * 512 words
-  uint32_t* pw = dr_lds + DR_FIXED / 4;                       // wcap words (the payload stage)
-  uint32_t* cum_s = pw;                                       // range + 1 words, until staging
+  uint32_t* pw = dr_lds + DR_FIXED / 4;                       // payload rings (DR_RW words per thread)
+  uint32_t* cum_s = pw;                                       // range + 1 words, before the rings
   __shared__ uint32_t wtot[DR_T / 64];
   for (uint32_t i = tid; i <= range; i += DR_T) cum_s[i] = j.cum[(size_t)sid * j.cum_stride + i];
   const uint32_t nb = (M + 31) >> 5;
@@ -509,40 +505,6 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams, uint32_t
     if (p1) put(s1, a1, a2, k + p0);
   }
   __syncthreads();
-  // ringed (default): each thread streams its segment's payload words from the file through a
-  // 16-word ring of its own in LDS; staged (dbg 0x200): the whole payload is copied to LDS first
-  const bool ringed = !(j.dbg & 0x200);
-  const bool staged = !ringed && d.words <= wcap;
-  if (staged) {
-    const uint64_t last = j.size >= 4 ? (j.size & ~3ull) - 4 : 0;
-    uint32_t tail = 0;
-    for (uint64_t q = j.size & ~3ull; q < j.size; q++) tail |= (uint32_t)j.in[q] << (8 * (q & 3));
-    const uint32_t al = (uint32_t)(d.payload_off & 3);
-    const uint64_t base = d.payload_off & ~3ull;
-    // 8 words per thread in flight per round (the loads of a round are issued back to back)
-    for (uint32_t i0 = 0; i0 < d.words; i0 += DR_T * 8) {
-      uint32_t v0[8], v1[8];
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const uint64_t a0 = min(base + (uint64_t)(i0 + k * DR_T + tid) * 4, last), a1 = min(a0 + 4, last);
-        v0[k] = *(const uint32_t*)(j.in + a0);
-        v1[k] = *(const uint32_t*)(j.in + a1);
-      }
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const uint32_t i = i0 + k * DR_T + tid;
-        if (i < d.words) {
-          const uint64_t a0 = base + (uint64_t)i * 4, a1 = a0 + 4;
-          const uint32_t w0 = a0 <= last ? v0[k] : (a0 == last + 4 ? tail : 0u);
-          const uint32_t w1 = a1 <= last ? v1[k] : (a1 == last + 4 ? tail : 0u);
-          pw[i] = __builtin_amdgcn_alignbyte(w1, w0, al);
-        }
-      }
-    }
-  }
-  __syncthreads();
-  uint64_t Ta = 0;
-  if (j.dbg & 16) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(Ta)::"memory");
   uint16_t* out = j.dsym + d.out_off;
   const uint32_t sw = skew_w(j, sid, d.n);
   // generic decode of symbols [s0, s1) from state x (payload word wi of the stage, or the file)
@@ -557,7 +519,7 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams, uint32_t
       x = (uint64_t)f * (x >> pb) + (slot - c);             // Rans64DecAdvance
       if (x < (1ull << 31)) {
         if (wi >= wend) return false;
-        x = (x << 32) | (staged ? pw[wi] : ld_u32_unaligned(j.in, d.payload_off + (uint64_t)wi * 4));
+        x = (x << 32) | ld_u32_unaligned(j.in, d.payload_off + (uint64_t)wi * 4);
         wi++;
       }
     }
@@ -573,8 +535,6 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams, uint32_t
     }
     return;
   }
-  if (j.dbg & 16) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(T1)::"memory");
-  if (j.dbg & 4) return;
   const IndexStream xs = j.ix[d.ix];
   const uint32_t nseg = (d.n + DSEG - 1) / DSEG;
   bool bad = false;
@@ -591,7 +551,7 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams, uint32_t
       s1 = min(d.n, s0 + DSEG);
       if (sg + 1 < nseg) { const Checkpoint c2 = j.ck[xs.ckpt_off + sg + 1]; want = (uint64_t)c2.xl | ((uint64_t)c2.xh << 32); }
     }
-    if (ringed && act && s1 - s0 == DSEG) {
+    if (act && s1 - s0 == DSEG) {
       // Payload word k of the stream = bytes P+4k .. P+4k+3 of the file.  The lane's ring holds
       // words [fill-DR_RW, fill) in slots k % DR_RW (slot-major: lanes read consecutive banks).
       // A 16-symbol group reads at most 8 words (each symbol takes <= 15 bits, a renorm adds 32,
@@ -662,43 +622,11 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams, uint32_t
       if (x != want || wi > d.words) bad = true;
       continue;
     }
-    if (staged && act && s1 - s0 == DSEG) {
-      // a whole segment: 16 symbols per 32-B store of the lane's own (flat) output range; the
-      // stores are never awaited, and nothing but the chain touches LDS
-      uint4* o4 = (uint4*)(out + s0);
-      for (uint32_t g = 0; g < DSEG / 16; g++) {
-        uint32_t pk[8];
-#pragma unroll
-        for (int u = 0; u < 16; u++) {
-          const uint32_t nw = pw[min(wi, wcap - 1)];
-          const uint32_t slot = (uint32_t)x & mask;
-          uint32_t sym, cc, f;
-          tb.lookup(slot, sym, cc, f);
-          if (u & 1) pk[u >> 1] |= sym << 16; else pk[u >> 1] = sym;
-          x = (uint64_t)f * (x >> pb) + (slot - cc);       // Rans64DecAdvance
-          if (x < (1ull << 31)) { x = (x << 32) | nw; wi++; }
-        }
-        if (!(j.dbg & 32)) {                                 // 32 contiguous bytes per thread
-          o4[2 * g] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-          o4[2 * g + 1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
-        } else if (pk[0] == 0xffffffffu) bad = true;         // keep the chain live (measurement)
-      }
-      if (x != want || wi > d.words) bad = true;
-      continue;
-    }
     if (!act) continue;
     uint64_t xe;
     if (!run(x, wi, s0, s1, &xe) || xe != want) bad = true;
   }
   if (bad) atomicOr(j.gerr, 4u);
-  if ((j.dbg & 16) && tid == 0) {
-    uint64_t T2;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(T2)::"memory");
-    j.dbgbuf[sid * 4] = T1 - T0;
-    j.dbgbuf[sid * 4 + 1] = T2 - T1;
-    j.dbgbuf[sid * 4 + 2] = 1;
-    j.dbgbuf[sid * 4 + 3] = Ta - T0;
-  }
 }
 
 // Without an index: one lane per stream, tables from the parse kernel (512 buckets).
@@ -1252,17 +1180,6 @@ int decode_tiles_impl(hoh_ctx* c, const uint8_t* d_blob, size_t size, int W, int
 }
 
 static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s, const AsyncDec* as) {
-  {
-    const char* e = getenv("HOH_DEC_DBG");
-    j.dbg = e ? (uint32_t)atoi(e) : 0;
-  }
-  DecWork& w0 = ctx_dec(c);
-  if (j.dbg & 16) {
-    void* q;
-    if (dbuf(w0, 13, (size_t)j.ntiles * SK_PER_TILE * 32, &q)) return 3;
-    j.dbgbuf = (uint64_t*)q;
-    (void)hipMemsetAsync(q, 0, (size_t)j.ntiles * SK_PER_TILE * 32, s);
-  }
   j.npix_cap = (uint32_t)(((size_t)j.tw * j.th + 63) / 64 * 64);
   j.lz_cap = (uint32_t)((j.npix_cap / 4 + j.npix_cap / 255 + 16 + 7) / 8 * 8);
   {
@@ -1295,26 +1212,9 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   ctx_mark(c, s, "dtable", false);
   hipLaunchKernelGGL(k_dparse, dim3(j.ntiles), dim3(64), 0, s, j);
   ctx_mark(c, s, "dparse", false);
-  uint64_t* pin = ctx_pinned(c);
-  // the largest payload sizes k_drans's LDS stage; an enqueue-only call cannot wait for it and
-  // stages streams of up to 40 KB (two workgroups per CU; larger streams decode unstaged)
-  uint32_t maxw = 10240;
-  if (!as) {
-    if (hipMemcpyAsync(pin, j.gerr, 8, hipMemcpyDeviceToHost, s) != hipSuccess) return 3;
-    if (hipStreamSynchronize(s) != hipSuccess) return 3;
-    const uint32_t ge = (uint32_t)pin[0];
-    if (ge & 2) return 6;
-    if (ge) return 7;
-    maxw = (uint32_t)(pin[0] >> 32);
-  }
   if (indexed) {
-    // payload stage sized to the largest stream when it fits next to the tables (<= 128 KB)
-    const size_t fixed = DR_FIXED;                                     // lookup tables
-    const uint32_t wcap = (uint32_t)std::min<size_t>(std::max<uint32_t>(std::max<uint32_t>(maxw, 1), 514),
-                                                     (150 * 1024 - fixed) / 4);   // >= 514: cum_s lives there first
     hipLaunchKernelGGL(k_dmatch, dim3((S + 255) / 256), dim3(256), 0, s, j, S);
-    const size_t stage = (j.dbg & 0x200) ? (size_t)wcap * 4 : (size_t)DR_RW * DR_T * 4;
-    hipLaunchKernelGGL(k_drans, dim3(S), dim3(DR_T), fixed + stage, s, j, S, wcap);
+    hipLaunchKernelGGL(k_drans, dim3(S), dim3(DR_T), DR_FIXED + (size_t)DR_RW * DR_T * 4, s, j, S);
   } else {
     hipLaunchKernelGGL(k_drans_serial, dim3((S + 63) / 64), dim3(64), 0, s, j, S);
   }
@@ -1322,27 +1222,17 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   if (!indexed) hipLaunchKernelGGL(k_dstored, dim3(S), dim3(256), 0, s, j, S);
   hipLaunchKernelGGL(k_dlz, dim3((j.ntiles + 63) / 64), dim3(64), 0, s, j);
   ctx_mark(c, s, "dlz", false);
-  if (j.dbg & 0x100) goto done;                  // measurement: stop before the unpredict stage
   hipLaunchKernelGGL(k_dunpred_fast, dim3(j.ntiles), dim3(64), (size_t)64 * ORING_PITCH + (size_t)3 * j.tw * 2, s, j);
   j.lzband = (int)std::min<size_t>(64, (160 * 1024 - (size_t)j.tw * 4) / ((size_t)j.tw * 4) - 1);
   hipLaunchKernelGGL(k_dunpred_lz, dim3(std::min(j.ntiles, 256)), dim3(64), (size_t)(j.lzband + 1) * j.tw * 4, s, j);
   hipLaunchKernelGGL(k_dunpred_serial, dim3(std::min(j.ntiles, 64)), dim3(192), 0, s, j);
   ctx_mark(c, s, "dunpred", false);
-done:
   if (hipGetLastError() != hipSuccess) return 3;
   if (as) {
     launch_status_dec(j.gerr, (uint64_t)j.W * j.H * 3, as->status, s);
     return hipGetLastError() == hipSuccess ? 0 : 3;
   }
-  if (j.dbg & 16) {
-    std::vector<uint64_t> h((size_t)S * 4);
-    (void)hipMemcpyAsync(h.data(), j.dbgbuf, h.size() * 8, hipMemcpyDeviceToHost, s);
-    (void)hipStreamSynchronize(s);
-    double a = 0, b = 0, n = 0, st = 0;
-    for (int i = 0; i < S; i++) if (h[i * 4 + 2]) { a += h[i * 4]; b += h[i * 4 + 1]; st += h[i * 4 + 3]; n++; }
-    fprintf(stderr, "k_drans: %d rANS workgroups, avg setup %.0f (staging %.0f), decode %.0f s_memtime ticks\n", (int)n,
-            a / n, st / n, b / n);
-  }
+  uint64_t* pin = ctx_pinned(c);
   if (hipMemcpyAsync(pin, j.gerr, 8, hipMemcpyDeviceToHost, s) != hipSuccess) return 3;
   if (hipStreamSynchronize(s) != hipSuccess) return 3;
   const uint32_t ge = (uint32_t)pin[0];

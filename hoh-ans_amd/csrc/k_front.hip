@@ -107,7 +107,7 @@ __device__ __forceinline__ void front_tile(const EncodeJob& j, uint32_t* ring) {
   uint64_t* cand = j.candbits + (size_t)t * (j.npix_cap / 64);
   const uint8_t* img = j.rgb + ((size_t)y0 * j.W + x0) * 3;
   const size_t pitch = (size_t)j.W * 3;
-  const bool lz = !(j.dbg & 4) && j.speed == 0;     // -s>=1: k_lzcand screens a longer window
+  const bool lz = j.speed == 0;     // -s>=1: k_lzcand screens a longer window
 
   // loader cursor: this thread's pixel of the block being loaded (raster blk*256 + tid) as a
   // byte offset from the tile origin
@@ -218,11 +218,9 @@ __device__ __forceinline__ void front_tile(const EncodeJob& j, uint32_t* ring) {
       res0[q] = (uint16_t)rg;
       res1[q] = (uint16_t)rr;
       res2[q] = (uint16_t)rb;
-      if (!(j.dbg & 2)) {
-        atomicAdd(&hist[rg], 1u);
-        atomicAdd(&hist[256 + rr], 1u);
-        atomicAdd(&hist[768 + rb], 1u);
-      }
+      atomicAdd(&hist[rg], 1u);
+      atomicAdd(&hist[256 + rr], 1u);
+      atomicAdd(&hist[768 + rb], 1u);
     }
     cx += NT;
     if (wide_rows) {

@@ -4,7 +4,7 @@
 // the encoder is a chain of 65,536 dependent steps per 256x256 tile plane, and one wave issues
 // one instruction every ~6 cycles: the chain's length is its instruction count.  The fast
 // kernel therefore spends all its effort on instructions per step:
-//  * one stream per lane, RF_LANES streams per wave; the symbol tables (16-B entries: 1/f as
+//  * one stream per lane, 64 streams per wave; the symbol tables (16-B entries: 1/f as
 //    f64, f, c) are gathered from global memory (L2-resident, ~8 KB per stream) one 8-symbol
 //    block ahead through 32-bit offsets from one scalar base (two symbol offsets per packed
 //    16-bit shift);
@@ -112,21 +112,19 @@ __device__ __forceinline__ void ckpt(const Coder& c, Checkpoint* ck, uint32_t k)
   ck[k] = p;
 }
 
-template <int LANES, int WAVES = 1, bool DEEP = false>
-__global__ __launch_bounds__(64 * WAVES) void k_rans_fast(EncodeJob j, int nplane, SidMap ma, int na, SidMap mb,
-                                                          int nblk, int rot) {
+// One lane per stream, 64 streams per wave, one wave per workgroup.
+__global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane, SidMap ma, int na, SidMap mb, int nblk,
+                                                  int rot) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x;
   // the grid covers every CU; the working blocks are a window rotated per launch so that the
   // chains of images in flight land on different CUs instead of sharing the first ones
   const int blk = (int)((blockIdx.x + gridDim.x - rot) % gridDim.x);
   if (blk >= nblk) return;
   // the chain is the critical path of an image: win issue arbitration against co-resident waves
-  if (!(j.dbg & 0x400000)) __builtin_amdgcn_s_setprio(3);
-  uint64_t t_beg = 0;
-  if (j.dbgbuf && lane == 0) t_beg = __builtin_amdgcn_s_memrealtime();
-  const int pi = (blk * WAVES + wave) * LANES + lane;
-  if (lane >= LANES || pi >= nplane) return;
+  __builtin_amdgcn_s_setprio(3);
+  const int pi = blk * 64 + lane;
+  if (pi >= nplane) return;
   const uint32_t sid = plane_sid(pi, j.spt, ma, na, mb);
   StreamInfo st = j.streams[sid];
   if (!st.fast || st.mode != SM_RANS || st.err || st.n == 0) return;
@@ -145,7 +143,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_rans_fast(EncodeJob j, int nplan
   for (uint32_t i = n; i > n - r; i--) step15(c, ent(tb, tbase + (uint32_t)sp[i - 1] * 16u));
   flush_win(c);
   if (((nb * 8) % HOH_SEG) == 0 && nb * 8 < n) ckpt(c, ck, nb * 8 / HOH_SEG);
-  if (DEEP && nb) {
+  if (nb) {
     // table entries gathered 16 steps ahead (two 8-symbol blocks per buffer): with several images
     // in flight the 8 KB-per-stream tables live in MALL/HBM rather than L2, and an 8-step lead
     // left the chain waiting on the gather (15 % of its time even alone; four 8-entry buffers
@@ -178,45 +176,12 @@ __global__ __launch_bounds__(64 * WAVES) void k_rans_fast(EncodeJob j, int nplan
       if (p >= 3) { look(eB, h, l); if (p >= 4) syms(p - 4, h, l); }
       flush_win(c);
     }
-  } else if (nb) {
-    const uint4* sp4 = (const uint4*)sp;
-    EncFast eA[8], eB[8];
-    uint4 s1 = sp4[nb - 2];
-    uint4 s0 = sp4[nb - 3];
-    lookup8(eA, sp4[nb - 1], tb, tbase);
-    for (int b = (int)nb - 1; b >= 3; b -= 4) {
-      // entering: eA = entries of block b, s1 = symbols of b-1, s0 = symbols of b-2
-      lookup8(eB, s1, tb, tbase);
-      if (b - 3 >= 0) s1 = sp4[b - 3];
-#pragma unroll
-      for (int k = 7; k >= 0; --k) step15(c, eA[k]);
-      if ((b & (HOH_SEG / 8 - 1)) == 0) ckpt(c, ck, (uint32_t)b * 8 / HOH_SEG);
-      lookup8(eA, s0, tb, tbase);
-      if (b - 4 >= 0) s0 = sp4[b - 4];
-#pragma unroll
-      for (int k = 7; k >= 0; --k) step15(c, eB[k]);
-      if (((b - 1) & (HOH_SEG / 8 - 1)) == 0) ckpt(c, ck, (uint32_t)(b - 1) * 8 / HOH_SEG);
-      lookup8(eB, s1, tb, tbase);
-      if (b - 5 >= 0) s1 = sp4[b - 5];
-#pragma unroll
-      for (int k = 7; k >= 0; --k) step15(c, eA[k]);
-      if (((b - 2) & (HOH_SEG / 8 - 1)) == 0) ckpt(c, ck, (uint32_t)(b - 2) * 8 / HOH_SEG);
-      if (b - 4 >= 0) lookup8(eA, s0, tb, tbase);
-      if (b - 6 >= 0) s0 = sp4[b - 6];
-#pragma unroll
-      for (int k = 7; k >= 0; --k) step15(c, eB[k]);
-      if (((b - 3) & (HOH_SEG / 8 - 1)) == 0) ckpt(c, ck, (uint32_t)(b - 3) * 8 / HOH_SEG);
-      flush_win(c);
-    }
   }
   flush_win(c);
   c.slab[--c.widx] = c.xh;                 // Rans64EncFlush: lo at the lower address
   c.slab[--c.widx] = c.xl;
-  if (lane < LANES) {
-    j.streams[sid].words = st.slab_cap - c.widx;
-    j.streams[sid].widx_end = c.widx;
-  }
-  if (j.dbgbuf && lane == 0) { j.dbgbuf[2 * blk] = t_beg; j.dbgbuf[2 * blk + 1] = __builtin_amdgcn_s_memrealtime(); }
+  j.streams[sid].words = st.slab_cap - c.widx;
+  j.streams[sid].widx_end = c.widx;
 }
 
 // Generic: one lane per stream, rans64.hpp:262-278 verbatim (64x64 high product).
@@ -265,35 +230,12 @@ void launch_rans_fast(const EncodeJob& j, int nplane, hipStream_t s, SidMap a, i
   // its slowest chain; more than two chains per CU also slow each other.  One chain wave per
   // workgroup with a 56 KB LDS request (8 KB are used) caps the chains at two per CU and, alone,
   // spreads an image's 48 chains over 48 CUs.  The grid covers the chip with a per-launch rotation
-  // so that the chains of images in flight land on different CUs.  Measurement knobs: dbg bit 23 =
-  // two chain waves per workgroup with an 81 KB request (one workgroup, i.e. two chains, per CU:
-  // 40 KB of LDS per chain; 25 % slower chains for one image alone, and with the 16-step gathers
-  // 2-4 % lower bench throughput), bits 8..14 = lanes per wave, bits 24..31 = the request in KB.
-  const bool one = !(j.dbg & 0x800000) || ((j.dbg >> 8) & 127);
-  const int lanes = (j.dbg >> 8) & 127 ? (j.dbg >> 8) & 127 : 64;
-  const int waves = one ? 1 : 2;
-  const int per = lanes * waves;
-  const int nblk = (nplane + per - 1) / per;
-  const int span = one ? 1024 : 512;
-  const int grid = nblk >= span || (j.dbg & 0x100000) ? nblk : span;
+  // so that the chains of images in flight land on different CUs.  (Measured alternatives:
+  // DESIGN.md §4.)
+  const int nblk = (nplane + 63) / 64;
+  const int grid = nblk >= 1024 ? nblk : 1024;
   const int rot = grid == nblk ? 0 : (int)((g_rot.fetch_add(1) * 8u * (unsigned)((nblk + 7) / 8)) % (unsigned)grid);
-  const size_t pad = (j.dbg >> 24) ? (size_t)((j.dbg >> 24) & 255) * 1024 : (size_t)(one ? 56 : 81) * 1024;
-  if (!one) {
-    hipLaunchKernelGGL((k_rans_fast<64, 2, true>), dim3(grid), dim3(128), std::max<size_t>(128 * WIN * 4, pad), s, j, nplane,
-                       a, na, b, nblk, rot);
-  } else if (lanes == 16) {
-    hipLaunchKernelGGL(k_rans_fast<16>, dim3(grid), dim3(64), 16 * WIN * 4, s, j, nplane, a, na, b, nblk, rot);
-  } else if (lanes == 32) {
-    hipLaunchKernelGGL(k_rans_fast<32>, dim3(grid), dim3(64), 32 * WIN * 4, s, j, nplane, a, na, b, nblk, rot);
-  } else if (lanes == 8) {
-    hipLaunchKernelGGL(k_rans_fast<8>, dim3(grid), dim3(64), 8 * WIN * 4, s, j, nplane, a, na, b, nblk, rot);
-  } else if (j.dbg & 0x8000) {   // measurement: table gathers 8 steps ahead
-    hipLaunchKernelGGL(k_rans_fast<64>, dim3(grid), dim3(64), std::max<size_t>(64 * WIN * 4, pad), s, j, nplane, a, na,
-                       b, nblk, rot);
-  } else {
-    hipLaunchKernelGGL((k_rans_fast<64, 1, true>), dim3(grid), dim3(64), std::max<size_t>(64 * WIN * 4, pad), s, j,
-                       nplane, a, na, b, nblk, rot);
-  }
+  hipLaunchKernelGGL(k_rans_fast, dim3(grid), dim3(64), 56 * 1024, s, j, nplane, a, na, b, nblk, rot);
 }
 
 void launch_rans_gen(const EncodeJob& j, int nstreams, hipStream_t s, SidMap m) {

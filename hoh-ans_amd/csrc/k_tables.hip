@@ -105,7 +105,7 @@ __global__ __launch_bounds__(64) void k_tables(EncodeJob j, SidMap sm) {
   const uint32_t target = 1u << pb;
   for (uint32_t i = 1 + lane; i <= range; i += 64) cum[i] = (uint32_t)(((uint64_t)target * cum[i]) / total);
   __syncthreads();
-  for (uint32_t base = 0; base < ((j.dbg & 64) ? 0u : range); base += 64) {
+  for (uint32_t base = 0; base < range; base += 64) {
     const uint32_t i0 = base + lane;
     uint64_t zm = __ballot(i0 < range && fr[i0] && cum[i0 + 1] == cum[i0]);
     while (zm) {
@@ -240,7 +240,7 @@ __global__ __launch_bounds__(64) void k_tables(EncodeJob j, SidMap sm) {
       mybits += sb;
     }
   uint32_t loc;
-  if (__ballot(!fits) == 0 && !(j.dbg & 128)) {
+  if (__ballot(!fits) == 0) {
     // parallel writer: fields MSB-first into an LDS bit buffer (cum is free now), then copied
     uint32_t* bb = cum;
     const uint32_t head = 2 * cn * maxbits;

@@ -78,3 +78,63 @@ void launch_status_enc(const uint32_t* gerr, const uint64_t* total, uint64_t cap
 void launch_status_dec(const uint32_t* gerr, uint64_t bytes, uint64_t* out, hipStream_t s) {
   hipLaunchKernelGGL(k_status_dec, dim3(1), dim3(64), 0, s, gerr, bytes, out);
 }
+
+// ---- natural-statistic synthetic RGB (hoh_ans/natural.py, the same integer formula) ----------
+
+__device__ __forceinline__ uint64_t nat_h(uint64_t salt, uint64_t k, uint64_t a, uint64_t b) {
+  return splitmix64(salt + (k << 48) + (a << 24) + b);
+}
+
+// bilinear value noise on a 2^lg grid, node values h(k, gx, gy) & m
+__device__ __forceinline__ long long nat_vnoise(uint64_t salt, int k, int lg, uint64_t m, long long x, long long y) {
+  const long long S = 1ll << lg;
+  const uint64_t gx = (uint64_t)(x >> lg), gy = (uint64_t)(y >> lg);
+  const long long fx = x & (S - 1), fy = y & (S - 1);
+  const long long v00 = (long long)(nat_h(salt, k, gx, gy) & m), v10 = (long long)(nat_h(salt, k, gx + 1, gy) & m);
+  const long long v01 = (long long)(nat_h(salt, k, gx, gy + 1) & m), v11 = (long long)(nat_h(salt, k, gx + 1, gy + 1) & m);
+  const long long top = v00 * (S - fx) + v10 * fx, bot = v01 * (S - fx) + v11 * fx;
+  return (top * (S - fy) + bot * fy) >> (2 * lg);
+}
+
+__global__ void k_natural(uint8_t* rgb, int W, int rows, int y0, uint64_t salt) {
+  const size_t total = (size_t)W * rows;
+  for (size_t px = (size_t)blockIdx.x * blockDim.x + threadIdx.x; px < total; px += (size_t)gridDim.x * blockDim.x) {
+    const long long x = (long long)(px % W), y = (long long)(px / W) + y0;
+    const long long R = nat_vnoise(salt, 1, 7, 1023, x, y) + nat_vnoise(salt, 2, 4, 127, x, y);
+    const uint64_t rk = nat_h(salt, 3, (uint64_t)(R >> 6), (uint64_t)(((x >> 9) << 12) | (y >> 9)));
+    const long long Lf = 2 * nat_vnoise(salt, 4, 8, 255, x, y) + nat_vnoise(salt, 5, 6, 255, x, y) +
+                         nat_vnoise(salt, 6, 3, 63, x, y);
+    const long long L = (Lf * 79) >> 8;
+    const long long T = nat_vnoise(salt, 8, 2, 63, x, y) - 32;
+    const uint64_t hp = nat_h(salt, 7, (uint64_t)x, (uint64_t)y);
+    auto u = [](uint64_t v, int s, uint64_t m) { return (long long)((v >> s) & m); };
+    const long long t = u(rk, 0, 7), base = u(rk, 8, 255);
+    long long chR = u(rk, 16, 63) - 32;
+    if (chR == 0) chR = 9;
+    const long long ch[3] = {chR, 0, u(rk, 22, 63) - 32};
+    const long long gain = u(rk, 28, 7), sx = u(rk, 32, 63) - 32, sy = u(rk, 38, 63) - 32;
+    const long long nl = u(hp, 0, 7) + u(hp, 3, 7) - 7, nb = u(hp, 16, 63) - 32;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      const long long nc = u(hp, 6 + 2 * c, 3) == 0 ? u(hp, 12 + c, 1) * 2 - 1 : 0;
+      long long v = base + ch[c];
+      if (t == 0) {
+      } else if (t <= 3) {
+        v += (((L - 128) * gain) >> 2) + nl + nc;
+      } else if (t <= 5) {
+        v += T + (nb >> 1) + nc;
+      } else if (t == 6) {
+        v += (((x & 511) * sx + (y & 511) * sy) >> 7) + (nl >> 1);
+      } else {
+        v += 48 * (((x >> 2) + (y >> 2)) & 1);
+      }
+      v = v < 0 ? 0 : v > 255 ? 255 : v;
+      rgb[px * 3 + c] = (uint8_t)v;
+    }
+  }
+}
+
+void launch_natural(uint8_t* rgb, int W, int rows, int y0, uint64_t seed, hipStream_t s) {
+  const uint64_t salt = seed * 0xD6E8FEB86659FD93ull;
+  hipLaunchKernelGGL(k_natural, dim3(4096), dim3(256), 0, s, rgb, W, rows, y0, salt);
+}

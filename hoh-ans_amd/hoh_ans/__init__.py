@@ -75,6 +75,7 @@ def lib():
         L.hoh_peek_header.argtypes = [vp, sz, ip, ip, ip, ip]
         L.hoh_synth_rgb.argtypes = [vp, vp, C.c_int, C.c_int, C.c_uint64, C.c_int, vp]
         L.hoh_synth_rgb_rows.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int, vp]
+        L.hoh_natural_rgb_rows.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_uint64, vp]
         L.hoh_encode_tiles_ix.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, sz, vp, szp, vp, vp]
         L.hoh_encode_tiles_speed.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, sz, vp, szp,
                                              vp, vp]
@@ -308,6 +309,17 @@ def synth_rgb_dev(W, H, seed=1, noise=4, ctx=None, device="cuda", row0=0):
     t = torch.empty(W * H * 3, dtype=torch.uint8, device=device)
     check(lib().hoh_synth_rgb_rows(ctx.h, vp(t.data_ptr()), W, row0, H, seed, noise, _stream_ptr(torch)),
           "hoh_synth_rgb_rows")
+    return t
+
+
+def natural_rgb_dev(W, H, seed=1, ctx=None, device="cuda", row0=0):
+    """Natural-statistic image generated in HBM (same bytes as hoh_ans.natural.natural_rgb);
+    with row0, rows [row0, row0+H) of the width-W global image."""
+    import torch
+    ctx = ctx or default_ctx()
+    t = torch.empty(W * H * 3, dtype=torch.uint8, device=device)
+    check(lib().hoh_natural_rgb_rows(ctx.h, vp(t.data_ptr()), W, row0, H, seed, _stream_ptr(torch)),
+          "hoh_natural_rgb_rows")
     return t
 
 

@@ -207,6 +207,9 @@ int hoh_add_green(hoh_ctx* ctx, const uint16_t* G, const uint16_t* R, const uint
 int hoh_synth_rgb(hoh_ctx* ctx, uint8_t* d_rgb, int W, int H, uint64_t seed, int noise, void* stream);
 int hoh_synth_rgb_rows(hoh_ctx* ctx, uint8_t* d_rgb, int W, int y0, int rows, uint64_t seed, int noise,
                        void* stream);
+/* Natural-statistic synthetic RGB (hoh_ans/natural.py formula: piecewise-smooth regions, hard
+ * edges, textures, flat runs, short repeats), rows [y0, y0+rows) of a width-W image. */
+int hoh_natural_rgb_rows(hoh_ctx* ctx, uint8_t* d_rgb, int W, int y0, int rows, uint64_t seed, void* stream);
 
 #ifdef __cplusplus
 }

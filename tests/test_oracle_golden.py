@@ -2,6 +2,7 @@
 itself (tests/golden/make_golden.py).  These pin the oracle on machines without /root/reference."""
 import ctypes as C
 import hashlib
+import os
 
 import numpy as np
 import pytest
@@ -71,6 +72,22 @@ def test_decode_entropy_roundtrip(golden, orc):
         assert bp == len(enc), sp
 
 
+@pytest.mark.skipif(not os.path.exists("/root/reference/simple_entropy_encoder.cpp"),
+                    reason="the input of entropy_roundtrip_test.sh is reference source text (not stored)")
+def test_entropy_roundtrip_test_digest(golden, orc):
+    """entropy_roundtrip_test.sh (the reference's own test): simple_entropy_encoder on its own
+    source, i.e. encode_entropy(u8 bytes, range 256, prob_bits 12) (simple_entropy_encoder.cpp:26-33).
+    The oracle's stream must carry the digest the compiled reference produced, and decode back."""
+    g = golden["entropy_roundtrip_test"]
+    src = open("/root/reference/simple_entropy_encoder.cpp", "rb").read()
+    assert len(src) == g["input_len"] and sha(src) == g["input_sha256"]
+    sym = np.frombuffer(src, np.uint8).astype(np.uint16)
+    enc = orc.encode_entropy(sym, 256, 12)
+    assert len(enc) == g["enc"]["len"] and sha(enc) == g["enc"]["sha256"]
+    dec, bp = orc.decode_entropy(enc + b"\x00" * 8)
+    assert np.array_equal(dec, sym) and bp == len(enc)
+
+
 def test_predict_fastpath(golden, orc):
     for p in golden["predict_fastpath"]:
         plane = make_plane(p["spec"])
@@ -130,3 +147,17 @@ def test_oracle_roundtrip_files(orc):
         img = synth_rgb(W, H, seed, noise)
         data, _ = orc.choh(img)
         assert np.array_equal(orc.dhoh(data), img)
+
+
+@pytest.mark.parametrize("speed", [0, 1, 2, 3, 4])
+def test_natural_image_vs_reference(orc, speed):
+    """config 5 input: the natural-statistic generator (hoh_ans/natural.py) through the oracle's
+    choh at -s0..-s4 reproduces the file the compiled reference choh wrote for the same image
+    (tests/golden/golden_natural.json) -- pins the generator and the oracle's -s>=1 search together."""
+    import json
+    from hoh_ans.natural import natural_rgb
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden_natural.json")))
+    rec = [f for f in g["files"] if (f["spec"]["W"], f["spec"]["H"], f["spec"]["speed"]) == (768, 512, speed)][0]
+    data, printed = orc.choh(natural_rgb(768, 512, rec["spec"]["seed"]), speed)
+    assert printed == rec["printed"]
+    check(rec["out"], data)
