@@ -447,6 +447,20 @@ int hoh_encode_tiles_speed(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int s
   return r;
 }
 
+int hoh_encode_tiles_async(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int speed, int t0, int ntiles,
+                           uint8_t* d_out, size_t cap, uint32_t* d_tile_sizes, hoh_index* idx, uint64_t* d_status,
+                           void* stream) {
+  if (!c || !d_rgb || !d_out || !d_tile_sizes || !d_status || W <= 0 || H <= 0 || speed < 0 || speed > 4)
+    return HOH_E_ARG;
+  if (speed && idx) idx->nstreams = 0;
+  (void)hipSetDevice(c->device);
+  int xt, yt, tw, th;
+  if (!hoh_tiling(W, H, &xt, &yt, &tw, &th)) return HOH_E_ARG;
+  uint64_t total = 0;
+  return encode_tiles_impl(c, d_rgb, W, H, t0, ntiles, d_out, cap, 0, 0, d_tile_sizes, &total, speed ? nullptr : idx,
+                           pick(c, stream), speed, d_status);
+}
+
 int hoh_encode_image_ix(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int speed, uint8_t* d_out,
                         size_t cap, size_t* out_size, size_t* printed, hoh_index* idx, void* stream) {
   if (!c || !d_rgb || !d_out || !out_size || W <= 0 || H <= 0) return HOH_E_ARG;

@@ -12,6 +12,9 @@ int decode_image_async_impl(hoh_ctx* c, const uint8_t* d_in, size_t size, int W,
                             const hoh_index* idx, uint64_t* d_status, hipStream_t s);
 int decode_tiles_impl(hoh_ctx* c, const uint8_t* d_blob, size_t size, int W, int H, int t0, int ntiles,
                       const uint32_t* h_sizes, uint8_t* d_rgb, const hoh_index* idx, hipStream_t s);
+int decode_tiles_async_impl(hoh_ctx* c, const uint8_t* d_blob, size_t size, int W, int H, int t0, int ntiles,
+                            const uint32_t* d_sizes, uint8_t* d_rgb, const hoh_index* idx, uint64_t* d_status,
+                            hipStream_t s);
 int decode_stream_impl(hoh_ctx* c, const uint8_t* d_in, size_t size, size_t* bp, uint16_t* d_out, size_t cap,
                        size_t* n, hipStream_t s);
 int encode_streams_impl(hoh_ctx* c, const uint16_t* d_syms, const uint64_t* off, const uint32_t* cnt, int nstreams,
@@ -71,6 +74,15 @@ int hoh_decode_tiles(hoh_ctx* c, const uint8_t* d_blob, size_t size, int W, int 
   if (!c || !d_blob || !d_rgb || !h_tile_sizes || W <= 0 || H <= 0) return HOH_E_ARG;
   (void)hipSetDevice(ctx_device(c));
   return decode_tiles_impl(c, d_blob, size, W, H, t0, ntiles, h_tile_sizes, d_rgb, idx, ctx_stream(c, stream));
+}
+
+int hoh_decode_tiles_async(hoh_ctx* c, const uint8_t* d_blob, size_t size, int W, int H, int t0, int ntiles,
+                           const uint32_t* d_tile_sizes, uint8_t* d_rgb, const hoh_index* idx, uint64_t* d_status,
+                           void* stream) {
+  if (!c || !d_blob || !d_rgb || !d_tile_sizes || !d_status || W <= 0 || H <= 0) return HOH_E_ARG;
+  (void)hipSetDevice(ctx_device(c));
+  return decode_tiles_async_impl(c, d_blob, size, W, H, t0, ntiles, d_tile_sizes, d_rgb, idx, d_status,
+                                 ctx_stream(c, stream));
 }
 
 int hoh_decode_image(hoh_ctx* c, const uint8_t* d_hoh, size_t size, uint8_t* d_rgb, size_t cap, int* W, int* H,

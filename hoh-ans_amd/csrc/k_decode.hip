@@ -1079,6 +1079,7 @@ struct AsyncDec {              // enqueue-only decode: expected header bytes and
   uint64_t hdr[2];
   int hl;
   uint64_t* status;
+  uint64_t bytes;               // the status size word on success
 };
 static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s, const AsyncDec* as = nullptr);
 void launch_status_dec(const uint32_t* gerr, uint64_t bytes, uint64_t* out, hipStream_t s);
@@ -1143,6 +1144,7 @@ int decode_image_async_impl(hoh_ctx* c, const uint8_t* d_in, size_t size, int W,
   for (int i = 0; i < p; i++) as.hdr[i / 8] |= (uint64_t)hb[i] << (8 * (i % 8));
   as.hl = p;
   as.status = d_status;
+  as.bytes = (uint64_t)W * H * 3;
   j.prefix = (uint64_t)p;
   j.ntiles = j.xt * j.yt;
   j.in = d_in;
@@ -1179,6 +1181,37 @@ int decode_tiles_impl(hoh_ctx* c, const uint8_t* d_blob, size_t size, int W, int
   return decode_run(c, j, idx, s);
 }
 
+// enqueue-only shard decode: the tile sizes stay on the device (as the encoder wrote them), so
+// nothing waits on the host; {status, tile pixels * 3} land in d_status
+int decode_tiles_async_impl(hoh_ctx* c, const uint8_t* d_blob, size_t size, int W, int H, int t0, int ntiles,
+                            const uint32_t* d_sizes, uint8_t* d_rgb, const hoh_index* idx, uint64_t* d_status,
+                            hipStream_t s) {
+  DecJob j;
+  memset(&j, 0, sizeof(j));
+  j.W = W; j.H = H;
+  if (!((W >= 512 || H >= 512) && W >= 256 && H >= 256)) return 6;
+  j.xt = W / 256; j.yt = H / 256;
+  j.tw = (W + j.xt - 1) / j.xt; j.th = (H + j.yt - 1) / j.yt;
+  if (t0 < 0 || ntiles <= 0 || t0 + ntiles > j.xt * j.yt) return 1;
+  j.t0 = t0;
+  j.ntiles = ntiles;
+  j.prefix = 0;
+  j.in = d_blob;
+  j.size = size;
+  j.rgb = d_rgb;
+  j.tsizes = d_sizes;
+  AsyncDec as;
+  as.hdr[0] = as.hdr[1] = 0;
+  as.hl = 0;                                      // a blob has no header to check
+  as.status = d_status;
+  as.bytes = 0;
+  for (int i = 0; i < ntiles; i++) {
+    const int g = t0 + i, xo = (g % j.xt) * j.tw, yo = (g / j.xt) * j.th;
+    as.bytes += (uint64_t)std::min(j.tw, W - xo) * std::min(j.th, H - yo) * 3;
+  }
+  return decode_run(c, j, idx, s, &as);
+}
+
 static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s, const AsyncDec* as) {
   j.npix_cap = (uint32_t)(((size_t)j.tw * j.th + 63) / 64 * 64);
   j.lz_cap = (uint32_t)((j.npix_cap / 4 + j.npix_cap / 255 + 16 + 7) / 8 * 8);
@@ -1207,7 +1240,7 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   if (hipMemsetAsync(j.gerr, 0, 64, s) != hipSuccess) return 3;
   if (hipMemsetAsync(j.streams, 0, (size_t)S * sizeof(DecStream), s) != hipSuccess) return 3;
   ctx_mark(c, s, "start", as == nullptr);
-  if (as) hipLaunchKernelGGL(k_dhdr, dim3(1), dim3(64), 0, s, j, as->hdr[0], as->hdr[1], as->hl);
+  if (as && as->hl) hipLaunchKernelGGL(k_dhdr, dim3(1), dim3(64), 0, s, j, as->hdr[0], as->hdr[1], as->hl);
   hipLaunchKernelGGL(k_dtable, dim3(1), dim3(1024), 0, s, j);
   ctx_mark(c, s, "dtable", false);
   hipLaunchKernelGGL(k_dparse, dim3(j.ntiles), dim3(64), 0, s, j);
@@ -1229,7 +1262,7 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   ctx_mark(c, s, "dunpred", false);
   if (hipGetLastError() != hipSuccess) return 3;
   if (as) {
-    launch_status_dec(j.gerr, (uint64_t)j.W * j.H * 3, as->status, s);
+    launch_status_dec(j.gerr, as->bytes, as->status, s);
     return hipGetLastError() == hipSuccess ? 0 : 3;
   }
   uint64_t* pin = ctx_pinned(c);

@@ -85,6 +85,9 @@ def lib():
             ("hoh_decode_image_ix", [vp, vp, sz, vp, sz, ip, ip, vp, vp]),
             ("hoh_encode_image_async", [vp, vp, C.c_int, C.c_int, C.c_int, vp, sz, vp, vp, vp]),
             ("hoh_decode_image_async", [vp, vp, sz, C.c_int, C.c_int, vp, sz, vp, vp, vp]),
+            ("hoh_encode_tiles_async", [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, sz, vp, vp, vp,
+                                        vp]),
+            ("hoh_decode_tiles_async", [vp, vp, sz, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, vp]),
             ("hoh_encode_entropy", [vp, vp, sz, sz, C.c_uint32, vp, sz, szp]),
             ("hoh_decode_entropy", [vp, vp, sz, szp, vp, sz, szp]),
             ("hoh_entropy_count", [vp, sz, sz, szp]),
@@ -283,6 +286,31 @@ def decode_tiles(blob_dev, size, W, H, t0, tile_sizes, out_dev, ctx=None, index=
     r = lib().hoh_decode_tiles(ctx.h, vp(blob_dev.data_ptr()), size, W, H, t0, ts.size, _p(ts), vp(base),
                                index.h if index is not None else None, _stream_ptr(torch))
     check(r, "hoh_decode_tiles")
+
+
+def encode_tiles_async(rgb_dev, W, H, t0, ntiles, out_dev, sizes_dev, status_dev, ctx=None, index=None, row0=0,
+                       speed=0):
+    """Enqueue-only encode_tiles on the current stream: the tile sizes land in sizes_dev (device)
+    and {status, blob size} in status_dev (2 x int64, device); nothing waits on the host."""
+    import torch
+    ctx = ctx or default_ctx()
+    base = rgb_dev.data_ptr() - row0 * W * 3
+    r = lib().hoh_encode_tiles_async(ctx.h, vp(base), W, H, speed, t0, ntiles, vp(out_dev.data_ptr()),
+                                     out_dev.numel(), vp(sizes_dev.data_ptr()), index.h if index is not None else None,
+                                     vp(status_dev.data_ptr()), _stream_ptr(torch))
+    check(r, "hoh_encode_tiles_async")
+
+
+def decode_tiles_async(blob_dev, size, W, H, t0, ntiles, sizes_dev, out_dev, status_dev, ctx=None, index=None, row0=0):
+    """Enqueue-only decode_tiles with the tile sizes in DEVICE memory (sizes_dev, as encode_tiles
+    wrote them); {status, shard RGB bytes} land in status_dev."""
+    import torch
+    ctx = ctx or default_ctx()
+    base = out_dev.data_ptr() - row0 * W * 3
+    r = lib().hoh_decode_tiles_async(ctx.h, vp(blob_dev.data_ptr()), size, W, H, t0, ntiles, vp(sizes_dev.data_ptr()),
+                                     vp(base), index.h if index is not None else None, vp(status_dev.data_ptr()),
+                                     _stream_ptr(torch))
+    check(r, "hoh_decode_tiles_async")
 
 
 def file_prefix(W, H, tile_sizes):

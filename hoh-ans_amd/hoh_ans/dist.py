@@ -8,6 +8,10 @@ single-GPU file.  Decode runs per rank on its own blob (decode_tiles); no other 
 
 Works with any torch.distributed backend ("nccl" = RCCL on ROCm for device tensors, "gloo" for
 the CPU tests); the collectives see only uint8/int64 tensors.
+
+Several images in flight per GPU share ONE process group: a single host thread per rank deals the
+steps round-robin to the in-flight slots (run_pipeline), and every rank issues the gathers in
+step order, so the collectives of different slots never interleave differently across ranks.
 """
 import numpy as np
 
@@ -66,7 +70,10 @@ class FileGather:
         self.W, self.H, self.device, self.group = W, H, device, group
         self.file = None
 
-    def __call__(self, blob, size, tile_sizes):
+    def __call__(self, blob, size, tile_sizes, wait=True):
+        """wait=False: return the pending point-to-point requests instead of waiting on them (the
+        caller waits -- for RCCL that makes its current stream wait, not the host -- before it
+        reuses `blob` or the file buffer)."""
         import torch
         import torch.distributed as dist
         rank = dist.get_rank(self.group)
@@ -80,9 +87,12 @@ class FileGather:
             raise RuntimeError("tile sizes do not add up to the blob size")
         ranks = dist.get_process_group_ranks(self.group) if self.group is not None else list(range(world))
         if rank != 0:
-            if size:
-                dist.batch_isend_irecv([dist.P2POp(dist.isend, blob[:size], ranks[0], self.group)])[0].wait()
-            return None, 0
+            reqs = dist.batch_isend_irecv([dist.P2POp(dist.isend, blob[:size], ranks[0], self.group)]) if size else []
+            if wait:
+                for q in reqs:
+                    q.wait()
+                return None, 0
+            return None, 0, reqs
         prefix = file_prefix(self.W, self.H, np.concatenate(sizes))
         total = len(prefix) + sum(blob_sizes)
         if self.file is None or self.file.numel() < total:
@@ -93,6 +103,30 @@ class FileGather:
                for r in range(1, world) if blob_sizes[r]]
         reqs = dist.batch_isend_irecv(ops) if ops else []
         self.file[offs[0]:offs[0] + blob_sizes[0]] = blob[:blob_sizes[0]]
+        if not wait:
+            return self.file, total, reqs
         for q in reqs:
             q.wait()
         return self.file, total
+
+
+def run_pipeline(nslots, total, enqueue, finish):
+    """Single-thread pipeline over `nslots` in-flight slots: step i goes to slot i % nslots.
+    enqueue(slot, i) enqueues step i's device work without waiting on the host; finish(slot, i)
+    completes its host-side part (e.g. the gather, which needs the tile sizes on the host).  Step
+    i's finish runs just before its slot takes step i + nslots, and the last nslots steps finish
+    at the end, so finish is called for steps 0, 1, 2, ... in order on every rank: collectives
+    issued from it match across ranks with one process group."""
+    pending = [None] * nslots
+    order = []
+    for i in range(total):
+        k = i % nslots
+        if pending[k] is not None:
+            finish(k, pending[k])
+            order.append(pending[k])
+        enqueue(k, i)
+        pending[k] = i
+    for i in range(max(0, total - nslots), total):
+        finish(i % nslots, i)
+        order.append(i)
+    return order

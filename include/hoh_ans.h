@@ -130,6 +130,16 @@ int hoh_encode_tiles_speed(hoh_ctx* ctx, const uint8_t* d_rgb, int W, int H, int
  * the base of the whole image).  idx may be the index hoh_encode_tiles_ix recorded. */
 int hoh_decode_tiles(hoh_ctx* ctx, const uint8_t* d_blob, size_t size, int W, int H, int t0, int ntiles,
                      const uint32_t* h_tile_sizes, uint8_t* d_rgb, const hoh_index* idx, void* stream);
+/* Enqueue-only forms of the two calls above (no host round trip; see the image-level async
+ * calls for the d_status convention).  Encode: d_status[1] = the blob size.  Decode: the tile
+ * sizes are read from DEVICE memory (d_tile_sizes, e.g. as the encoder wrote them), so a shard can
+ * be decoded before its sizes ever reach the host; d_status[1] = the shard's RGB bytes. */
+int hoh_encode_tiles_async(hoh_ctx* ctx, const uint8_t* d_rgb, int W, int H, int speed, int t0, int ntiles,
+                           uint8_t* d_out, size_t cap, uint32_t* d_tile_sizes, hoh_index* idx, uint64_t* d_status,
+                           void* stream);
+int hoh_decode_tiles_async(hoh_ctx* ctx, const uint8_t* d_blob, size_t size, int W, int H, int t0, int ntiles,
+                           const uint32_t* d_tile_sizes, uint8_t* d_rgb, const hoh_index* idx, uint64_t* d_status,
+                           void* stream);
 /* Host: the .hoh prefix for a tiled image given every tile's size (choh.cpp:437-498):
  * magic, format, depth, varint W-1, H-1, x_tiles-1, y_tiles-1, n-1 varint sizes.  Returns the
  * prefix length, or 0 if cap is too small. */

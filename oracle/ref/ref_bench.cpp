@@ -3,7 +3,9 @@
 // RGB file).  Encode = encode_tile(-s0) per tile (the whole of choh's per-tile work,
 // choh.cpp:104-383); decode = decode_entropy + unpredict_all per plane + inverse subtract-green
 // (entropy_decoding.hpp:134, unprediction.hpp:6) -- dhoh itself cannot be timed: it crashes on
-// every tiled file.  Prints one JSON line.  Single thread, like the reference.
+// every tiled file.  Prints one JSON line.  Single thread, like the reference; the
+// optional 5th argument (first tile) lets bench.py run one process per core on disjoint tile
+// ranges for the all-cores leg.
 #include <stdio.h>
 #include <stdlib.h>
 #include <stdint.h>
@@ -20,8 +22,9 @@
 static double now() { timespec t; clock_gettime(CLOCK_MONOTONIC, &t); return t.tv_sec + t.tv_nsec * 1e-9; }
 
 int main(int argc, char** argv) {
-  if (argc < 5) { fprintf(stderr, "usage: ref_bench in.rgb W H max_tiles\n"); return 1; }
+  if (argc < 5) { fprintf(stderr, "usage: ref_bench in.rgb W H max_tiles [first_tile]\n"); return 1; }
   int W = atoi(argv[2]), H = atoi(argv[3]), maxt = atoi(argv[4]);
+  const int first = argc > 5 ? atoi(argv[5]) : 0;
   FILE* f = fopen(argv[1], "rb");
   if (!f) return 2;
   size_t sz = (size_t)W * H * 3;
@@ -29,12 +32,13 @@ int main(int argc, char** argv) {
   if (fread(img, 1, sz, f) != sz) return 2;
   fclose(f);
   int xt = W / 256, yt = H / 256, tw = (W + xt - 1) / xt, th = (H + yt - 1) / yt;
-  int nt = xt * yt < maxt ? xt * yt : maxt;
+  int nt = xt * yt - first < maxt ? xt * yt - first : maxt;
+  if (nt < 0) nt = 0;
   int saved = dup(1); int dn = open("/dev/null", O_WRONLY);
   double tenc = 0, tdec = 0;
   size_t raw = 0, comp = 0;
   long bad = 0;
-  for (int i = 0; i < nt; i++) {
+  for (int i = first; i < first + nt; i++) {
     int xo = (i % xt) * tw, yo = (i / xt) * th, nw = tw, nh = th;
     if (W - xo < nw) nw = W - xo;
     if (H - yo < nh) nh = H - yo;

@@ -80,3 +80,58 @@ def test_gloo_gather_matches_single_file(tmp_path):
     img = synth.synth_rgb(W, H, seed=5, noise=4)
     want, printed = oracle.choh(img)
     assert got == want
+
+
+NSTEP, NSLOT = 5, 3
+
+
+def _pipeline_worker(rank, world, port, outdir):
+    """bench.py's N > 1 schedule on gloo: several images in flight per rank, one process group,
+    one host thread; every step's gather must still assemble that step's file exactly."""
+    import torch
+    import torch.distributed as dist
+    import hoh_ans
+    from hoh_ans import dist as hd
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        t0, nt, y0, y1 = hd.shard(W, H, rank, world)
+        _, xt, yt, tw, th = hoh_ans.tiling(W, H)
+        slots = [{"blob": torch.zeros(4 << 20, dtype=torch.uint8), "g": hd.FileGather(W, H, "cpu")}
+                 for _ in range(NSLOT)]
+
+        def enqueue(k, i):
+            img = synth.synth_rgb(W, H, seed=10 + i, noise=4)
+            tiles = []
+            for t in range(t0, t0 + nt):
+                x, y = (t % xt) * tw, (t // xt) * th
+                tiles.append(oracle.encode_tile(img[y:y + th, x:x + tw]))
+            cat = b"".join(tiles)
+            slots[k]["blob"][:len(cat)] = torch.frombuffer(bytearray(cat), dtype=torch.uint8)
+            slots[k]["n"] = len(cat)
+            slots[k]["sizes"] = np.array([len(b) for b in tiles], np.uint32)
+
+        def finish(k, i):
+            sl = slots[k]
+            res = sl["g"](sl["blob"], sl["n"], sl["sizes"], wait=False)
+            for q in res[2]:
+                q.wait()
+            if rank == 0:
+                with open(os.path.join(outdir, "step%d.hoh" % i), "wb") as fh:
+                    fh.write(res[0][:res[1]].numpy().tobytes())
+
+        order = hd.run_pipeline(NSLOT, NSTEP, enqueue, finish)
+        assert order == list(range(NSTEP))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_pipeline_in_step_order(tmp_path):
+    world = 2
+    mp.spawn(_pipeline_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for i in range(NSTEP):
+        img = synth.synth_rgb(W, H, seed=10 + i, noise=4)
+        want, _ = oracle.choh(img)
+        assert (tmp_path / ("step%d.hoh" % i)).read_bytes() == want, "step %d" % i
