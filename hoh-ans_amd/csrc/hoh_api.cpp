@@ -13,11 +13,14 @@
 #include <algorithm>
 #include <stdio.h>
 #include <string>
+#include <atomic>
 
 void launch_synth(uint8_t* rgb, int W, int H, int y0, uint64_t seed, int noise, hipStream_t s);
 void launch_natural(uint8_t* rgb, int W, int rows, int y0, uint64_t seed, hipStream_t s);
 void launch_put_bytes(uint8_t* dst, const uint8_t* b, int n, hipStream_t s);
 void launch_status_enc(const uint32_t* gerr, const uint64_t* total, uint64_t cap, uint64_t* out, hipStream_t s);
+
+std::atomic<uint64_t> g_device_allocs{0};     // every hipMalloc this library makes
 
 namespace {
 
@@ -33,6 +36,7 @@ int ensure(Buf& b, size_t bytes) {
   b.p = nullptr;
   b.n = 0;
   if (hipMalloc(&b.p, bytes) != hipSuccess) return HOH_E_HIP;
+  g_device_allocs.fetch_add(1, std::memory_order_relaxed);
   b.n = bytes;
   return HOH_OK;
 }
@@ -48,8 +52,14 @@ struct hoh_index {
   size_t ck_count = 0;
 };
 
+struct Scratch {                // see ScratchFrame (hoh_dec.h)
+  std::vector<Buf> chunks;
+  size_t cur = 0, used = 0;
+};
+
 struct hoh_ctx {
   int device = 0;
+  Scratch scr;
   hipStream_t own = nullptr;
   Buf idx8, fpb, pinfo, lg;     // -s>=1 workspaces
   uint32_t lg_key[4] = {0, 0, 0, 0};
@@ -115,7 +125,9 @@ struct Prof {
 
 extern "C" {
 
-const char* hoh_version(void) { return "hoh-ans_amd 0.1 (gfx950)"; }
+const char* hoh_version(void) { return "hoh-ans_amd 0.2 (gfx950)"; }
+
+uint64_t hoh_device_alloc_count(void) { return g_device_allocs.load(std::memory_order_relaxed); }
 
 const char* hoh_strerror(int code) {
   switch (code) {
@@ -154,6 +166,7 @@ void hoh_ctx_destroy(hoh_ctx* c) {
   Buf* all[] = {&c->idx8, &c->fpb, &c->pinfo, &c->lg, &c->sym, &c->hist, &c->candbits, &c->matches, &c->pal, &c->streams, &c->tiles, &c->hdr,
                 &c->tab_fast, &c->tab_gen, &c->slabs, &c->ckpt, &c->misc, &c->tsizes};
   for (Buf* b : all) freebuf(*b);
+  for (Buf& b : c->scr.chunks) freebuf(b);
   dec_free(c->dec);
   for (auto e : c->kev) (void)hipEventDestroy(e);
   if (c->pinned) (void)hipHostFree(c->pinned);
@@ -483,11 +496,11 @@ int hoh_encode_image_ix(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int spee
     if (printed) *printed = (size_t)total;
   } else {
     // choh.cpp:508-520: the single tile is coded and discarded; only the header is written (Q13)
-    Buf scratch;
+    ScratchFrame f(c);
     const size_t b = hoh_encode_bound(W, H);
-    if ((r = ensure(scratch, b))) return r;
-    r = encode_tiles_impl(c, d_rgb, W, H, 0, 1, (uint8_t*)scratch.p, b, 0, 0, nullptr, &total, nullptr, s, speed);
-    freebuf(scratch);
+    uint8_t* scratch = f.get<uint8_t>(b);
+    if (!scratch) return HOH_E_HIP;
+    r = encode_tiles_impl(c, d_rgb, W, H, 0, 1, scratch, b, 0, 0, nullptr, &total, nullptr, s, speed);
     if (r == HOH_OK && hipMemcpyAsync(d_out, hb, hl, hipMemcpyHostToDevice, s) != hipSuccess) r = HOH_E_HIP;
     if (r == HOH_OK && hipStreamSynchronize(s) != hipSuccess) r = HOH_E_HIP;
     *out_size = hl;
@@ -565,6 +578,10 @@ int encode_streams_impl(hoh_ctx* c, const uint16_t* d_syms, const uint64_t* off,
   if ((e = ensure(c->tab_gen, (size_t)nstreams * range * sizeof(EncGen)))) return e;
   if ((e = ensure(c->slabs, (size_t)nstreams * slab * 4))) return e;
   if ((e = ensure(c->misc, 64))) return e;
+  // prob_bits 15 with range <= 512 (every -s0 plane, config 2's single stream) takes the tuned
+  // chain k_rans_fast, the rest the reference reciprocal step (k_rans_gen)
+  const bool fast = pb == 15 && range <= HOH_FAST_RANGE;
+  if (fast && (e = ensure(c->tab_fast, (size_t)nstreams * HOH_FAST_RANGE * sizeof(EncFast)))) return e;
   std::vector<StreamInfo> st((size_t)nstreams);
   for (int i = 0; i < nstreams; i++) {
     memset(&st[i], 0, sizeof(StreamInfo));
@@ -577,6 +594,7 @@ int encode_streams_impl(hoh_ctx* c, const uint16_t* d_syms, const uint64_t* off,
     st[i].pb = pb;
     st[i].ckpt_off = (uint32_t)((size_t)i * per_ck);
     st[i].mode = SM_EMPTY;
+    st[i].fast = fast ? 1 : 0;
   }
   EncodeJob j;
   memset(&j, 0, sizeof(j));
@@ -585,6 +603,7 @@ int encode_streams_impl(hoh_ctx* c, const uint16_t* d_syms, const uint64_t* off,
   j.hdr = (uint8_t*)c->hdr.p;
   j.hdr_cap = hcap;
   j.tab_gen = (EncGen*)c->tab_gen.p;
+  j.tab_fast = fast ? (EncFast*)c->tab_fast.p : nullptr;
   j.gen_stride = range;
   j.slabs = (uint32_t*)c->slabs.p;
   j.ckpt = nullptr;                           // stream-level decodes are serial: no checkpoints
@@ -596,7 +615,8 @@ int encode_streams_impl(hoh_ctx* c, const uint16_t* d_syms, const uint64_t* off,
   if (hipMemcpyAsync(c->streams.p, st.data(), st.size() * sizeof(StreamInfo), hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;
   if (hipMemsetAsync(c->misc.p, 0, 64, s) != hipSuccess) return HOH_E_HIP;
   launch_tables(j, nstreams, s);
-  launch_rans_gen(j, nstreams, s);
+  if (fast) launch_rans_fast(j, nstreams, s, SidMap{0, 0}, nstreams, SidMap{0, 0});
+  launch_rans_gen(j, nstreams, s);            // skips the streams k_rans_fast coded
   launch_finalize(j, nstreams, s);
   launch_streambytes(j, nstreams, s);
   if (hipGetLastError() != hipSuccess) return HOH_E_HIP;
@@ -633,21 +653,48 @@ int hoh_encode_entropy(hoh_ctx* c, const uint16_t* symbols, size_t n, size_t ran
   (void)hipSetDevice(c->device);
   hipStream_t s = c->own;
   const size_t bound = hoh_entropy_bound(n, range, pb);
-  Buf ds, dout;
-  int r;
-  if ((r = ensure(ds, n * 2 + 16)) || (r = ensure(dout, bound))) { freebuf(ds); freebuf(dout); return r; }
-  if (n && hipMemcpyAsync(ds.p, symbols, n * 2, hipMemcpyHostToDevice, s) != hipSuccess) r = HOH_E_HIP;
+  ScratchFrame f(c);
+  uint16_t* ds = f.get<uint16_t>(n * 2 + 16);
+  uint8_t* dout = f.get<uint8_t>(bound);
+  if (!ds || !dout) return HOH_E_HIP;
+  int r = HOH_OK;
+  if (n && hipMemcpyAsync(ds, symbols, n * 2, hipMemcpyHostToDevice, s) != hipSuccess) r = HOH_E_HIP;
   uint64_t off = 0, oo = 0;
   uint32_t cnt = (uint32_t)n, size = 0;
-  if (!r) r = encode_streams_impl(c, (const uint16_t*)ds.p, &off, &cnt, 1, (uint32_t)range, pb, (uint8_t*)dout.p, &oo, &size, s);
+  if (!r) r = encode_streams_impl(c, ds, &off, &cnt, 1, (uint32_t)range, pb, dout, &oo, &size, s);
   if (!r) {
     *written = size;
     if (size > cap) r = HOH_E_CAP;
-    else if (hipMemcpy(out, dout.p, size, hipMemcpyDeviceToHost) != hipSuccess) r = HOH_E_HIP;
+    else if (hipMemcpy(out, dout, size, hipMemcpyDeviceToHost) != hipSuccess) r = HOH_E_HIP;
   }
-  freebuf(ds);
-  freebuf(dout);
   return r;
+}
+
+// ---------------------------------------------------------------- host-entry scratch
+
+ScratchFrame::ScratchFrame(hoh_ctx* ctx) : c(ctx), cur(ctx->scr.cur), used(ctx->scr.used) {}
+ScratchFrame::~ScratchFrame() { c->scr.cur = cur; c->scr.used = used; }
+
+void* ScratchFrame::alloc(size_t n) {
+  Scratch& s = c->scr;
+  n = rup(n ? n : 16, 256);
+  for (;;) {
+    if (s.cur == s.chunks.size()) s.chunks.push_back(Buf{});
+    Buf& b = s.chunks[s.cur];
+    if (s.used + n <= b.n) {
+      void* p = (uint8_t*)b.p + s.used;
+      s.used += n;
+      return p;
+    }
+    if (s.used == 0) {
+      // nothing of this chunk (nor of any later one) is live: grow it in place
+      const size_t want = std::max(n, std::max(b.n * 2, (size_t)1 << 20));
+      if (ensure(b, want) != HOH_OK) return nullptr;
+      continue;
+    }
+    s.cur++;
+    s.used = 0;
+  }
 }
 
 // ---------------------------------------------------------------- decode side index

@@ -51,3 +51,16 @@ hipStream_t ctx_stream(hoh_ctx* c, void* s);
 uint64_t* ctx_pinned(hoh_ctx* c);
 int ctx_device(hoh_ctx* c);
 void ctx_mark(hoh_ctx* c, hipStream_t s, const char* name, bool reset);
+
+// Per-context device scratch for the host-buffer entry points (encode_entropy, decode_entropy,
+// layer_*, the predictor/unpredictor drop-ins): a grow-only chunk list used as a stack.  A frame
+// releases everything allocated after it was opened; after the first call of a given shape no
+// call allocates device memory.  alloc() returns nullptr on failure.
+struct ScratchFrame {
+  hoh_ctx* c;
+  size_t cur, used;
+  explicit ScratchFrame(hoh_ctx* ctx);
+  ~ScratchFrame();
+  void* alloc(size_t n);
+  template <class T> T* get(size_t n) { return (T*)alloc(n); }
+};

@@ -31,11 +31,11 @@ int layer_encode_search(hoh_ctx* c, const uint16_t* data, size_t n, int w, int h
 
 namespace {
 
-// scoped device allocation for the host-buffer entry points
+// device buffer of a host-buffer entry point, carved from the context's grow-only scratch
+// (ScratchFrame, hoh_dec.h): no device allocation once the context has seen the call's shape
 struct DevMem {
   void* p = nullptr;
-  explicit DevMem(size_t n) { if (hipMalloc(&p, n ? n : 16) != hipSuccess) p = nullptr; }
-  ~DevMem() { if (p) (void)hipFree(p); }
+  DevMem(ScratchFrame& f, size_t n) : p(f.alloc(n)) {}
   template <class T> T* as() { return (T*)p; }
 };
 
@@ -107,7 +107,8 @@ int hoh_decode_entropy(hoh_ctx* c, const uint8_t* in, size_t in_size, size_t* bp
   int r = hoh_entropy_count(in, in_size, *bp, &cnt);
   if (r) return r;
   if (cnt > cap) return HOH_E_CAP;
-  DevMem din(in_size + 8), dout(cnt * 2 + 16);
+  ScratchFrame sf(c);
+  DevMem din(sf, in_size + 8), dout(sf, cnt * 2 + 16);
   if (!din.p || !dout.p) return HOH_E_HIP;
   if (hipMemcpy(din.p, in, in_size, hipMemcpyHostToDevice) != hipSuccess) return HOH_E_HIP;
   if (hipMemset((uint8_t*)din.p + in_size, 0, 8) != hipSuccess) return HOH_E_HIP;
@@ -125,7 +126,8 @@ int hoh_predict_fastpath(hoh_ctx* c, const uint16_t* data, int w, int h, int dep
   (void)hipSetDevice(ctx_device(c));
   hipStream_t s = ctx_stream(c, nullptr);
   const size_t n = (size_t)w * h;
-  DevMem a(n * 2), b(n * 2);
+  ScratchFrame sf(c);
+  DevMem a(sf, n * 2), b(sf, n * 2);
   if (!a.p || !b.p) return HOH_E_HIP;
   if (hipMemcpyAsync(a.p, data, n * 2, hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;
   launch_predict(a.as<uint16_t>(), w, h, depth, b.as<uint16_t>(), s);
@@ -139,7 +141,8 @@ int hoh_unpredict_fastpath(hoh_ctx* c, const uint16_t* res, size_t nres, const u
   (void)hipSetDevice(ctx_device(c));
   hipStream_t s = ctx_stream(c, nullptr);
   const size_t n = (size_t)w * h;
-  DevMem dr(nres * 2), db(backref ? n * 2 : 16), dout(n * 2), de(16);
+  ScratchFrame sf(c);
+  DevMem dr(sf, nres * 2), db(sf, backref ? n * 2 : 16), dout(sf, n * 2), de(sf, 16);
   if (!dr.p || !db.p || !dout.p || !de.p) return HOH_E_HIP;
   if (nres && hipMemcpyAsync(dr.p, res, nres * 2, hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;
   if (backref && hipMemcpyAsync(db.p, backref, n * 2, hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;
@@ -156,7 +159,8 @@ int hoh_subtract_green(hoh_ctx* c, const uint8_t* rgb, size_t npix, uint16_t* G,
   if (!c || !rgb || !G || !R || !B) return HOH_E_ARG;
   (void)hipSetDevice(ctx_device(c));
   hipStream_t s = ctx_stream(c, nullptr);
-  DevMem a(npix * 3), g(npix * 2), r(npix * 2), b(npix * 2);
+  ScratchFrame sf(c);
+  DevMem a(sf, npix * 3), g(sf, npix * 2), r(sf, npix * 2), b(sf, npix * 2);
   if (!a.p || !g.p || !r.p || !b.p) return HOH_E_HIP;
   if (hipMemcpyAsync(a.p, rgb, npix * 3, hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;
   launch_green(a.as<uint8_t>(), npix, g.as<uint16_t>(), r.as<uint16_t>(), b.as<uint16_t>(), s);
@@ -170,7 +174,8 @@ int hoh_add_green(hoh_ctx* c, const uint16_t* G, const uint16_t* R, const uint16
   if (!c || !rgb || !G || !R || !B) return HOH_E_ARG;
   (void)hipSetDevice(ctx_device(c));
   hipStream_t s = ctx_stream(c, nullptr);
-  DevMem a(npix * 3), g(npix * 2), r(npix * 2), b(npix * 2);
+  ScratchFrame sf(c);
+  DevMem a(sf, npix * 3), g(sf, npix * 2), r(sf, npix * 2), b(sf, npix * 2);
   if (!a.p || !g.p || !r.p || !b.p) return HOH_E_HIP;
   if (hipMemcpyAsync(g.p, G, npix * 2, hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;
   if (hipMemcpyAsync(r.p, R, npix * 2, hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;
@@ -190,7 +195,8 @@ int hoh_layer_encode(hoh_ctx* c, const uint16_t* data, size_t size, int w, int h
   if (cruncher != 0) return layer_encode_search(c, data, size, w, h, depth, (int)cruncher, nuke, out, cap, written);
   hipStream_t s = ctx_stream(c, nullptr);
   const size_t bound = hoh_entropy_bound(size, (size_t)1 << depth, 15);
-  DevMem a(size * 2), res(size * 2 + 16), cl(size * 2 + 16), nk(nuke ? size : 16), cnt(16), eout(bound);
+  ScratchFrame sf(c);
+  DevMem a(sf, size * 2), res(sf, size * 2 + 16), cl(sf, size * 2 + 16), nk(sf, nuke ? size : 16), cnt(sf, 16), eout(sf, bound);
   if (!a.p || !res.p || !cl.p || !nk.p || !cnt.p || !eout.p) return HOH_E_HIP;
   if (hipMemcpyAsync(a.p, data, size * 2, hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;
   if (nuke && hipMemcpyAsync(nk.p, nuke, size, hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;

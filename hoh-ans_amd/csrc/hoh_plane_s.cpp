@@ -30,10 +30,10 @@ void launch_hist16(const uint16_t* in, uint64_t n, uint32_t* hist, hipStream_t s
 
 namespace {
 
+// device buffer carved from the context's grow-only scratch (ScratchFrame, hoh_dec.h)
 struct Dev {
   void* p = nullptr;
-  explicit Dev(size_t n) { if (hipMalloc(&p, n ? n : 16) != hipSuccess) p = nullptr; }
-  ~Dev() { if (p) (void)hipFree(p); }
+  Dev(ScratchFrame& f, size_t n) : p(f.alloc(n)) {}
   template <class T> T* as() { return (T*)p; }
 };
 
@@ -57,7 +57,8 @@ int entropy_table(const uint16_t* d_res, size_t n, int range, double* d_ent, uin
 int encode_one(hoh_ctx* c, const uint16_t* d_sym, uint32_t n, uint32_t range, uint32_t pb, std::vector<uint8_t>& out,
                hipStream_t s) {
   const size_t bound = hoh_entropy_bound(n, range, pb);
-  Dev d(bound);
+  ScratchFrame sf(c);
+  Dev d(sf, bound);
   if (!d.p) return HOH_E_HIP;
   uint64_t off = 0, oo = 0;
   uint32_t sz = 0;
@@ -75,8 +76,9 @@ int layer_encode_search(hoh_ctx* c, const uint16_t* data, size_t n, int w, int h
                         const uint8_t* nuke, uint8_t* out, size_t cap, size_t* written) {
   hipStream_t s = ctx_stream(c, nullptr);
   const int range = 1 << depth;
-  Dev dd(n * 2 + 16), dres(n * 2 + 16), dcl(n * 2 + 16), dnk(nuke ? n : 16), dcnt(16), dhist((size_t)range * 4),
-      dent((size_t)range * 8);
+  ScratchFrame sf(c);
+  Dev dd(sf, n * 2 + 16), dres(sf, n * 2 + 16), dcl(sf, n * 2 + 16), dnk(sf, nuke ? n : 16), dcnt(sf, 16), dhist(sf, (size_t)range * 4),
+      dent(sf, (size_t)range * 8);
   if (!dd.p || !dres.p || !dcl.p || !dnk.p || !dcnt.p || !dhist.p || !dent.p) return HOH_E_HIP;
   if (hipMemcpyAsync(dd.p, data, n * 2, hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;
   if (nuke && hipMemcpyAsync(dnk.p, nuke, n, hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;
@@ -101,7 +103,8 @@ int layer_encode_search(hoh_ctx* c, const uint16_t* data, size_t n, int w, int h
   const int xt = (w + 39) / 40, yt = (h + 39) / 40;
   if (xt > 1 || yt > 1) {                                             // :124-319
     const int T = xt * yt, npred = cruncher * 5 < 14 ? cruncher * 5 : 14;
-    Dev dcost((size_t)T * 14 * 8), dpl((size_t)T * 2), dpi((size_t)T), dmap((size_t)T * 2 + 16);
+    ScratchFrame sf_cells(c);
+    Dev dcost(sf_cells, (size_t)T * 14 * 8), dpl(sf_cells, (size_t)T * 2), dpi(sf_cells, (size_t)T), dmap(sf_cells, (size_t)T * 2 + 16);
     if (!dcost.p || !dpl.p || !dpi.p || !dmap.p) return HOH_E_HIP;
     for (int pass = 0; pass < (cruncher > 2 ? 2 : 1); pass++) {
       if ((r = entropy_table(dres.as<uint16_t>(), n, range, dent.as<double>(), dhist.as<uint32_t>(), s))) return r;
@@ -163,7 +166,8 @@ int hoh_predict_section(hoh_ctx* c, const uint16_t* data, int w, int h, int dept
     return hoh_predict_fastpath(c, data, w, h, depth, out);
   }
   const size_t n = (size_t)w * h;
-  Dev dd(n * 2), dout((size_t)tw * th * 2), dc(16), dtop((size_t)tw * 2), dbp((size_t)tw);
+  ScratchFrame sf(c);
+  Dev dd(sf, n * 2), dout(sf, (size_t)tw * th * 2), dc(sf, 16), dtop(sf, (size_t)tw * 2), dbp(sf, (size_t)tw);
   if (!dd.p || !dout.p || !dc.p || !dtop.p || !dbp.p) return HOH_E_HIP;
   if (hipMemcpyAsync(dd.p, data, n * 2, hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;
   launch_section_one(dd.as<uint16_t>(), w, h, depth, xt, yt, cx, cy, mask, dout.as<uint16_t>(), dc.as<uint64_t>(),
@@ -181,7 +185,8 @@ int hoh_predict_all(hoh_ctx* c, const uint16_t* data, int w, int h, int depth, i
   (void)hipSetDevice(ctx_device(c));
   hipStream_t s = ctx_stream(c, nullptr);
   const size_t n = (size_t)w * h, nm = (size_t)xt * yt;
-  Dev dd(n * 2), dout(n * 2), dm(nm * 2);
+  ScratchFrame sf(c);
+  Dev dd(sf, n * 2), dout(sf, n * 2), dm(sf, nm * 2);
   if (!dd.p || !dout.p || !dm.p) return HOH_E_HIP;
   if (hipMemcpyAsync(dd.p, data, n * 2, hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;
   if (hipMemcpyAsync(dm.p, tile_map, nm * 2, hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;
@@ -198,7 +203,8 @@ int hoh_unpredict_all(hoh_ctx* c, const uint16_t* res, size_t nres, const uint16
   (void)hipSetDevice(ctx_device(c));
   hipStream_t s = ctx_stream(c, nullptr);
   const size_t n = (size_t)w * h, nm = (size_t)xt * yt;
-  Dev dr(nres * 2 + 16), db(backref ? n * 2 : 16), dout(n * 2), dm(nm * 2), dtop((size_t)w * 2), dbp((size_t)w), de(16);
+  ScratchFrame sf(c);
+  Dev dr(sf, nres * 2 + 16), db(sf, backref ? n * 2 : 16), dout(sf, n * 2), dm(sf, nm * 2), dtop(sf, (size_t)w * 2), dbp(sf, (size_t)w), de(sf, 16);
   if (!dr.p || !db.p || !dout.p || !dm.p || !dtop.p || !dbp.p || !de.p) return HOH_E_HIP;
   if (nres && hipMemcpyAsync(dr.p, res, nres * 2, hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;
   if (backref && hipMemcpyAsync(db.p, backref, n * 2, hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;

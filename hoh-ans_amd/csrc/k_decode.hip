@@ -8,7 +8,7 @@
 //             per-stream cumulative table and a 512-bucket slot->symbol table.
 //  k_drans:   rANS decode (rans64.hpp:107-142).  With a side index: one workgroup per stream,
 //             lane = 1024-symbol segment from the encoder's checkpoint, tables and payload in
-//             LDS.  k_drans_serial: one lane per stream (no index).
+//             LDS.  k_drans_wave: one wave per stream (no index).
 //  k_dlz:     LZ streams -> match list (un_lz.hpp:150-170, Q11/Q12 handled).
 //  k_dunpred_fast: MED inverse (prediction.hpp:26-41 inverted, every row, Q9 fixed) + inverse
 //             subtract-green, one wave per tile, anti-diagonal wavefront over 64-row bands.
@@ -17,6 +17,9 @@
 #include <string.h>
 #include <stdlib.h>
 #include <algorithm>
+#include <atomic>
+
+extern std::atomic<uint64_t> g_device_allocs;   // hoh_api.cpp
 #include <vector>
 #include <stdio.h>
 
@@ -629,20 +632,124 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams) {
   if (bad) atomicOr(j.gerr, 4u);
 }
 
-// Without an index: one lane per stream, tables from the parse kernel (512 buckets).
-__global__ __launch_bounds__(64) void k_drans_serial(DecJob j, int nstreams) {
+// Serial decode of one whole stream by one wave (no index: a foreign .hoh, dhoh.cpp:297-396;
+// or decode_entropy's single stream, entropy_decoding.hpp:268-276).  The chain itself is one
+// lane's (rans64.hpp:107-142: each step needs the previous state), so the wave's other lanes
+// keep its inputs and outputs off the chain: the lookup tables are built in LDS (DrTables, 12 KB:
+// two dependent LDS reads per symbol instead of global ones), the payload is streamed into a
+// 256-word LDS ring 64 words at a time (issued a group ahead, one coalesced load per lane), and
+// each group's 64 symbols are staged in LDS and stored by all lanes (128 B per group).
+#define DL_RING 256
+#define DL_SMEM (2 * DR_NB * 4 + 2 * 512 * 4 + 513 * 4 + DL_RING * 4 + 64 * 2)
+__device__ bool lane_decode(const DecJob& j, const DecStream& d, const uint32_t* cum_g, uint16_t* out,
+                            unsigned char* smem) {
+  const int lane = threadIdx.x;
+  const uint32_t pb = d.pb, M = 1u << pb, mask = M - 1, range = d.range;
+  DrTables tb;
+  tb.bk = (uint2*)smem;
+  tb.sy = (uint2*)(smem + 2 * DR_NB * 4);
+  uint32_t* cum = (uint32_t*)(smem + 2 * DR_NB * 4 + 2 * 512 * 4);
+  uint32_t* ring = cum + 513;
+  uint16_t* ob = (uint16_t*)(ring + DL_RING);
+  __shared__ uint32_t s_bad;
+  for (uint32_t i = lane; i <= range; i += 64) cum[i] = cum_g[i];
+  const uint32_t nb = (M + 31) >> 5;
+  for (uint32_t b = lane; b < nb; b += 64) tb.bk[b] = make_uint2(0, 0);
+  if (lane == 0) s_bad = 0;
+  __syncthreads();
+  {
+    // compact index of the present symbols: lane l owns symbols 8l .. 8l+7 (range <= 512)
+    uint32_t pres = 0;
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      const uint32_t sy = 8 * lane + e;
+      if (sy < range && cum[sy + 1] > cum[sy]) pres |= 1u << e;
+    }
+    const uint32_t cnt = __popc(pres);
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(incl, o);
+      if (lane >= o) incl += t;
+    }
+    uint32_t k = incl - cnt;
+    for (int e = 0; e < 8; e++) {
+      if (!((pres >> e) & 1)) continue;
+      const uint32_t sy = 8 * lane + e, c0 = cum[sy], c1 = cum[sy + 1];
+      tb.sy[k] = make_uint2(c0 | ((c1 - c0) << 16), sy);
+      for (uint32_t b = (c0 + 31) >> 5; b <= (c1 - 1) >> 5; b++) tb.bk[b].y = k;
+      if (c0 & 31) atomicOr(&tb.bk[c0 >> 5].x, 1u << (c0 & 31));
+      k++;
+    }
+  }
+  // payload word k = bytes P + 4k .. P + 4k + 3 of the file (unaligned), 0 past the file
+  const uint64_t P = d.payload_off, szal = j.size & ~3ull;
+  const uint32_t al = (uint32_t)(P & 3), nw = d.words;
+  auto word = [&](uint32_t k) -> uint32_t {
+    if (k >= nw) return 0u;
+    const uint64_t a = (P & ~3ull) + (uint64_t)k * 4;
+    uint32_t lo = 0, hi = 0;
+    for (int e = 0; e < 8; e++) {
+      const uint64_t b = a + e;
+      if (b < j.size) {
+        const uint32_t v = j.in[b];
+        if (e < 4) lo |= v << (8 * e); else hi |= v << (8 * (e - 4));
+      }
+    }
+    if (a + 8 <= szal) { lo = *(const uint32_t*)(j.in + a); hi = *(const uint32_t*)(j.in + a + 4); }
+    return __builtin_amdgcn_alignbyte(hi, lo, al);
+  };
+  uint32_t fill = 0;
+  for (int r = 0; r < 2; r++) { ring[(fill + lane) & (DL_RING - 1)] = word(fill + lane); fill += 64; }
+  __syncthreads();
+  uint64_t x = (uint64_t)ring[0] | ((uint64_t)ring[1] << 32);
+  uint32_t wi = 2;
+  uint32_t pend = 0;
+  bool hp = false;
+  for (uint32_t g0 = 0; g0 < d.n; g0 += 64) {
+    if (hp) { ring[(fill + lane) & (DL_RING - 1)] = pend; fill += 64; hp = false; }
+    wi = __shfl(wi, 0);
+    if (fill - wi < 128) { pend = word(fill + lane); hp = true; }   // lands next group
+    __syncthreads();
+    if (lane == 0) {
+      const uint32_t g1 = min(d.n, g0 + 64);
+      for (uint32_t i = g0; i < g1; i++) {
+        const uint32_t nxt = ring[wi & (DL_RING - 1)];
+        const uint32_t slot = (uint32_t)x & mask;
+        uint32_t sym, c, f;
+        tb.lookup(slot, sym, c, f);
+        ob[i - g0] = (uint16_t)sym;
+        x = (uint64_t)f * (x >> pb) + (slot - c);             // Rans64DecAdvance
+        if (x < (1ull << 31)) { x = (x << 32) | nxt; wi++; }
+      }
+      if (wi > nw) s_bad = 1;
+    }
+    __syncthreads();
+    if (g0 + lane < d.n) out[g0 + lane] = ob[lane];
+  }
+  __syncthreads();
+  return lane != 0 || (!s_bad && x == (1ull << 31));
+}
+
+// Without an index: one wave per stream (lane_decode); streams outside its table format
+// (range > 512 or prob_bits > 15, never in a -s0 file) fall back to one lane with global tables.
+__global__ __launch_bounds__(64) void k_drans_wave(DecJob j, int nstreams) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dl_lds[];
   if (dec_abort(j)) return;
-  const int sid = blockIdx.x * 64 + threadIdx.x;
-  if (sid >= nstreams) return;
+  const int sid = blockIdx.x;
   const DecStream d = j.streams[sid];
   if (d.mode != SM_RANS) return;
+  uint16_t* out = j.dsym + d.out_off;
+  if (d.range <= 512 && d.pb <= 15) {
+    if (!lane_decode(j, d, j.cum + (size_t)sid * j.cum_stride, out, dl_lds)) atomicOr(j.gerr, 4u);
+    return;
+  }
+  if (threadIdx.x) return;
   const uint64_t wend = d.payload_off + (uint64_t)d.words * 4;
   uint64_t x = (uint64_t)ld_u32_unaligned(j.in, d.payload_off) | ((uint64_t)ld_u32_unaligned(j.in, d.payload_off + 4) << 32);
   uint64_t xe;
-  const uint32_t bshift = d.pb > 9 ? d.pb - 9 : 0;
-  if (!dec_run<false>(j, d, j.cum + (size_t)sid * j.cum_stride, j.bsym + (size_t)sid * 512, bshift, nullptr, x,
-                      d.payload_off + 8, wend, 0, d.n, OutCursor(j.dsym + d.out_off, skew_w(j, sid, d.n), 0), &xe) ||
-      xe != (1ull << 31))
+  if (!dec_run<false>(j, d, j.cum + (size_t)sid * j.cum_stride, j.bsym + (size_t)sid * 512, d.pb > 9 ? d.pb - 9 : 0,
+                      nullptr, x, d.payload_off + 8, wend, 0, d.n, OutCursor(out, 0, 0), &xe) || xe != (1ull << 31))
     atomicOr(j.gerr, 4u);
 }
 
@@ -1069,6 +1176,7 @@ static int dbuf(DecWork& w, int k, size_t bytes, void** p) {
     w.bufs[k] = nullptr;
     w.sizes[k] = 0;
     if (hipMalloc(&w.bufs[k], bytes) != hipSuccess) return 3;
+    g_device_allocs.fetch_add(1, std::memory_order_relaxed);
     w.sizes[k] = bytes;
   }
   *p = w.bufs[k];
@@ -1249,7 +1357,7 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
     hipLaunchKernelGGL(k_dmatch, dim3((S + 255) / 256), dim3(256), 0, s, j, S);
     hipLaunchKernelGGL(k_drans, dim3(S), dim3(DR_T), DR_FIXED + (size_t)DR_RW * DR_T * 4, s, j, S);
   } else {
-    hipLaunchKernelGGL(k_drans_serial, dim3((S + 63) / 64), dim3(64), 0, s, j, S);
+    hipLaunchKernelGGL(k_drans_wave, dim3(S), dim3(64), DL_SMEM, s, j, S);
   }
   ctx_mark(c, s, "drans", false);
   if (!indexed) hipLaunchKernelGGL(k_dstored, dim3(S), dim3(256), 0, s, j, S);
@@ -1277,13 +1385,19 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
 // ---------------------------------------------------------------- single stream (decode_entropy)
 
 __global__ __launch_bounds__(64) void k_dstream(DecJob j, uint64_t bp, uint64_t* res) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dl_lds[];
   const int lane = threadIdx.x;
   uint64_t p = bp;
   const bool ok = parse_stream(j, p, 0, 0, lane);
   __syncthreads();
-  if (lane != 0) return;
-  if (!ok) { res[0] = 1; return; }
+  if (!ok) { if (lane == 0) res[0] = 1; return; }
   const DecStream d = j.streams[0];
+  if (d.mode == SM_RANS && d.range <= 512 && d.pb <= 15) {      // the whole wave (lane_decode)
+    const bool good = lane_decode(j, d, j.cum, j.dsym, dl_lds);
+    if (lane == 0) { res[0] = good ? 0 : 1; res[1] = d.n; res[2] = p; }
+    return;
+  }
+  if (lane != 0) return;
   res[1] = d.n;
   if (d.mode == SM_RANS) {
     const uint64_t wend = d.payload_off + (uint64_t)d.words * 4;
@@ -1319,7 +1433,7 @@ int decode_stream_impl(hoh_ctx* c, const uint8_t* d_in, size_t size, size_t* bp,
   uint64_t* res = (uint64_t*)q;
   j.dsym = d_out;
   // the symbol count must fit: peek happens on the host (hoh_entropy_count) before the call
-  hipLaunchKernelGGL(k_dstream, dim3(1), dim3(64), 0, s, j, (uint64_t)*bp, res);
+  hipLaunchKernelGGL(k_dstream, dim3(1), dim3(64), DL_SMEM, s, j, (uint64_t)*bp, res);
   if (hipGetLastError() != hipSuccess) return 3;
   uint64_t* pin = ctx_pinned(c);
   if (hipMemcpyAsync(pin, res, 24, hipMemcpyDeviceToHost, s) != hipSuccess) return 3;

@@ -85,21 +85,29 @@ __device__ __forceinline__ void step15(Coder& c, const EncFast& e) {
   // emit = x >= x_max, i.e. (x_hi >> 16) >= f; (nh, nl) = emit ? (0, x_hi) : (x_hi, x_lo); the
   // decision is shifted into the mask by an add-with-carry of the compare itself: 4 instructions
   uint32_t nh, nl;
+  uint64_t co;                               // the add-with-carry's own carry-out (unused)
   asm("v_cmp_ge_u32_sdwa vcc, %[xh], %[f] src0_sel:WORD_1 src1_sel:DWORD\n\t"
+      "v_addc_co_u32_e64 %[m], %[co], %[m], %[m], vcc\n\t"
       "v_cndmask_b32_e64 %[nh], %[xh], 0, vcc\n\t"
-      "v_cndmask_b32_e32 %[nl], %[xl], %[xh], vcc\n\t"
-      "v_addc_co_u32_e32 %[m], vcc, %[m], %[m], vcc"
-      : [nh] "=&v"(nh), [nl] "=&v"(nl), [m] "+v"(c.mask)
+      "v_cndmask_b32_e32 %[nl], %[xl], %[xh], vcc"
+      : [nh] "=&v"(nh), [nl] "=&v"(nl), [m] "+v"(c.mask), [co] "=&s"(co)
       : [xh] "v"(c.xh), [xl] "v"(c.xl), [f] "v"(f)
       : "vcc");
-  // all intermediate values are integers < 2^53, so every f64 operation below is exact; the
-  // remainder stays in f64 (no int round trip on the dependent chain)
-  const double nhd = (double)nh;
-  const double qhd = __builtin_trunc(nhd * e.inv);                 // floor(nh / f)
-  const double rhd = fma(-qhd, (double)f, nhd);                    // nh - qh*f
-  const double nd = fma(rhd, 4294967296.0, (double)nl);
-  const uint32_t ql = (uint32_t)(nd * e.inv);                      // floor(n / f)
-  const uint32_t qh = (uint32_t)qhd;
+  // No int<->f64 conversion on the chain (they issue at half the f64 rate): the kernel runs with
+  // f64 rounding toward zero (k_rans_fast sets MODE), so fma(m, inv, 2^52) = 2^52 + floor(m*inv)
+  // exactly for every m*inv < 2^52, and its low word IS the quotient; integers m < 2^52 enter
+  // f64 as the bit pattern {m_lo, 0x43300000 | m_hi} = 2^52 + m, minus 2^52 (exact).
+  //   qh = floor(nh / f)               (nh < 2^31)
+  //   rh = nh - qh*f                   (qh < 2^16, f <= 2^15: one 24-bit multiply)
+  //   ql = floor((rh*2^32 + nl) / f)   (< 2^32)
+  // The quotients equal the Alverson reciprocal's: 1/f is rounded up two ulps, so m*inv >= m/f
+  // and (m/f)(1 + 2^-51) stays below floor(m/f) + 1 for m/f < 2^32 (f <= 2^15).
+  const double two52 = 4503599627370496.0;
+  const double nhd = __builtin_bit_cast(double, ((uint64_t)0x43300000u << 32) | nh) - two52;
+  const uint32_t qh = (uint32_t)__builtin_bit_cast(uint64_t, __builtin_fma(nhd, e.inv, two52));
+  const uint32_t rh = nh - __umul24(qh, f);
+  const double n2d = __builtin_bit_cast(double, ((uint64_t)(0x43300000u | rh) << 32) | nl) - two52;
+  const uint32_t ql = (uint32_t)__builtin_bit_cast(uint64_t, __builtin_fma(n2d, e.inv, two52));
   c.xl = nl + e.c + ql * (32768u - f);
   c.xh = __builtin_amdgcn_alignbit(qh, ql, 17);
   c.slot++;
@@ -123,6 +131,10 @@ __global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane, SidMa
   if (blk >= nblk) return;
   // the chain is the critical path of an image: win issue arbitration against co-resident waves
   __builtin_amdgcn_s_setprio(3);
+  // f64 rounding toward zero (MODE.FP_ROUND[3:2] = 3) for step15's floor-by-fma, this wave only.
+  // Set in asm so the compiler's mode tracking does not restore round-to-nearest before its own
+  // f64 instructions: the only other f64 operations here are the exact 2^52 subtractions.
+  asm volatile("s_setreg_imm32_b32 hwreg(HW_REG_MODE, 2, 2), 3");
   const int pi = blk * 64 + lane;
   if (pi >= nplane) return;
   const uint32_t sid = plane_sid(pi, j.spt, ma, na, mb);

@@ -54,6 +54,7 @@ def lib():
         L.hoh_ctx_destroy.argtypes = [vp]
         L.hoh_strerror.restype = C.c_char_p
         L.hoh_version.restype = C.c_char_p
+        L.hoh_device_alloc_count.restype = C.c_uint64
         L.hoh_set_profiling.argtypes = [vp, C.c_int]
         L.hoh_get_kernel_ms.argtypes = [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.c_int]
         L.hoh_get_kernel_stats.argtypes = [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_double),
@@ -109,6 +110,11 @@ def lib():
             L.hoh_entropy_bound.argtypes = [sz, sz, C.c_uint32]
         _L = L
     return _L
+
+
+def device_alloc_count():
+    """hipMalloc calls the library has made so far (process-wide)."""
+    return int(lib().hoh_device_alloc_count())
 
 
 def check(code, what):

@@ -46,6 +46,9 @@ int hoh_ctx_create(hoh_ctx** ctx, int device);
 void hoh_ctx_destroy(hoh_ctx* ctx);
 const char* hoh_strerror(int code);
 const char* hoh_version(void);
+/* Number of device allocations (hipMalloc) the library has made so far, process-wide.  Contexts
+ * keep grow-only workspaces, so repeated calls of one shape allocate nothing after the first. */
+uint64_t hoh_device_alloc_count(void);
 /* per-kernel device time of the last call, for measurement (ms); enable with hoh_set_profiling */
 void hoh_set_profiling(hoh_ctx* ctx, int on);
 int hoh_get_kernel_ms(hoh_ctx* ctx, const char** names, float* ms, int max);

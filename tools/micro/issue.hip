@@ -18,7 +18,14 @@ __global__ void iss(uint32_t* out, uint64_t* cyc, uint32_t a) {
     if (OP == 2) asm volatile("v_cvt_f64_u32 %0, %1" : "=v"(d[i]) : "v"(x[i])); \
     if (OP == 3) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(x[i]) : "v"(a)); \
     if (OP == 4) asm volatile("v_fma_f64 %0, %0, %1, %1" : "+v"(d[i]) : "v"(one)); \
-    if (OP == 5) asm volatile("v_cvt_u32_f64 %0, %1" : "=v"(x[i]) : "v"(d[i]));
+    if (OP == 5) asm volatile("v_cvt_u32_f64 %0, %1" : "=v"(x[i]) : "v"(d[i])); \
+    if (OP == 6) asm volatile("v_add_f64 %0, %0, %1" : "+v"(d[i]) : "v"(one)); \
+    if (OP == 7) asm volatile("v_mul_u32_u24_e32 %0, %0, %1" : "+v"(x[i]) : "v"(a)); \
+    if (OP == 8) asm volatile("v_alignbit_b32 %0, %0, %1, 17" : "+v"(x[i]) : "v"(a)); \
+    if (OP == 9) asm volatile("v_add3_u32 %0, %0, %1, %1" : "+v"(x[i]) : "v"(a)); \
+    if (OP == 10) asm volatile("v_cmp_ge_u32_sdwa vcc, %0, %1 src0_sel:WORD_1 src1_sel:DWORD\n\tv_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(x[i]) : "v"(a) : "vcc"); \
+    if (OP == 11) asm volatile("v_cndmask_b32_e64 %0, %0, %1, s[0:1]" : "+v"(x[i]) : "v"(a)); \
+    if (OP == 12) asm volatile("v_add_u32_e32 %0, %0, %0" : "+v"(x[0]));
     R8(OPX)
   }
   uint64_t t1; asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1) :: "memory");
@@ -47,5 +54,12 @@ int main() {
   run<3>("v_mul_lo_u32", d_out, d_cyc);
   run<4>("v_fma_f64", d_out, d_cyc);
   run<5>("v_cvt_u32_f64", d_out, d_cyc);
+  run<6>("v_add_f64", d_out, d_cyc);
+  run<7>("v_mul_u32_u24", d_out, d_cyc);
+  run<8>("v_alignbit", d_out, d_cyc);
+  run<9>("v_add3_u32", d_out, d_cyc);
+  run<10>("cmp_sdwa+cndmask", d_out, d_cyc);
+  run<11>("v_cndmask_e64", d_out, d_cyc);
+  run<12>("dep v_add_u32", d_out, d_cyc);
   return 0;
 }
