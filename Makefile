@@ -23,9 +23,9 @@ build/%.cpp.o: $(CSRC)/%.cpp $(HDRS)
 
 $(LIBDIR)/libhohgpu.so: $(OBJS)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -ldl -lpthread
 
-$(BINDIR)/%: tools/cli/%.cpp $(LIBDIR)/libhohgpu.so include/hoh_ans.h $(wildcard include/hoh/*.hpp)
+$(BINDIR)/%: tools/cli/%.cpp tools/cli/gpus.h $(LIBDIR)/libhohgpu.so include/hoh_ans.h $(wildcard include/hoh/*.hpp)
 	@mkdir -p $(BINDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -o $@ $< -L$(LIBDIR) -lhohgpu -Wl,-rpath,'$$ORIGIN/../lib'
 

@@ -89,6 +89,11 @@ def lib():
             ("hoh_encode_tiles_async", [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, sz, vp, vp, vp,
                                         vp]),
             ("hoh_decode_tiles_async", [vp, vp, sz, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, vp]),
+            ("hoh_mgpu_create", [C.POINTER(vp), C.c_int, ip]),
+            ("hoh_mgpu_destroy", [vp]),
+            ("hoh_mgpu_transport", [vp]),
+            ("hoh_mgpu_encode_image", [vp, vp, C.c_int, C.c_int, C.c_int, vp, sz, szp, szp]),
+            ("hoh_mgpu_decode_image", [vp, vp, sz, vp, sz, ip, ip]),
             ("hoh_encode_entropy", [vp, vp, sz, sz, C.c_uint32, vp, sz, szp]),
             ("hoh_decode_entropy", [vp, vp, sz, szp, vp, sz, szp]),
             ("hoh_entropy_count", [vp, sz, sz, szp]),
@@ -355,6 +360,53 @@ def natural_rgb_dev(W, H, seed=1, ctx=None, device="cuda", row0=0):
     check(lib().hoh_natural_rgb_rows(ctx.h, vp(t.data_ptr()), W, row0, H, seed, _stream_ptr(torch)),
           "hoh_natural_rgb_rows")
     return t
+
+
+class MultiGPU:
+    """choh / dhoh over several GPUs in one process (hoh_mgpu_*): a band of tile rows per device,
+    one RCCL gather over xGMI into the file on the first device.  A device may repeat (the blobs
+    then move by device copies: transport 0); distinct devices use RCCL (transport 1)."""
+
+    def __init__(self, devices):
+        self.h = vp()
+        dv = (C.c_int * len(devices))(*devices)
+        check(lib().hoh_mgpu_create(C.byref(self.h), len(devices), dv), "hoh_mgpu_create")
+        self.devices = list(devices)
+
+    def transport(self):
+        return lib().hoh_mgpu_transport(self.h)
+
+    def encode_image(self, rgb, speed=0):
+        """(H, W, 3) uint8 host array -> (file bytes, printed size)."""
+        import torch
+        a = np.ascontiguousarray(rgb, dtype=np.uint8)
+        H, W, _ = a.shape
+        out = torch.empty(lib().hoh_encode_bound(W, H), dtype=torch.uint8, device="cuda:%d" % self.devices[0])
+        n, printed = C.c_size_t(0), C.c_size_t(0)
+        check(lib().hoh_mgpu_encode_image(self.h, _p(a), W, H, speed, vp(out.data_ptr()), out.numel(), C.byref(n),
+                                          C.byref(printed)), "hoh_mgpu_encode_image")
+        return out[:n.value].cpu().numpy().tobytes(), printed.value
+
+    def decode_image(self, data):
+        import torch
+        b = torch.from_numpy(np.frombuffer(bytes(data), np.uint8).copy()).to("cuda:%d" % self.devices[0])
+        W, H = peek_header(bytes(data[:64]))[:2]
+        out = np.empty((H, W, 3), np.uint8)
+        w, h = C.c_int(), C.c_int()
+        check(lib().hoh_mgpu_decode_image(self.h, vp(b.data_ptr()), len(data), _p(out), out.size, C.byref(w),
+                                          C.byref(h)), "hoh_mgpu_decode_image")
+        return out
+
+    def close(self):
+        if self.h:
+            lib().hoh_mgpu_destroy(self.h)
+            self.h = vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 # ------------------------------------------------------------------ host-buffer API (reference names)

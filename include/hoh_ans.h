@@ -150,6 +150,27 @@ size_t hoh_file_prefix(int W, int H, const uint32_t* tile_sizes, int ntiles, uin
 /* tiling of choh.cpp:454-461: returns 1 if tiled */
 int hoh_tiling(int W, int H, int* x_tiles, int* y_tiles, int* tile_w, int* tile_h);
 
+/* ---- multi-GPU in one process (choh / dhoh over several devices) ----------------------- */
+
+/* One process drives ndev GPUs: a context and a HIP stream per device and, when the devices are
+ * distinct, one RCCL communicator each (ncclCommInitAll; librccl.so is loaded here, not at link
+ * time).  A device may be listed more than once (several shards on one GPU): the blobs then move
+ * by device copies instead of RCCL (hoh_mgpu_transport returns 0; 1 = RCCL). */
+typedef struct hoh_mgpu hoh_mgpu;
+int hoh_mgpu_create(hoh_mgpu** m, int ndev, const int* devices);
+void hoh_mgpu_destroy(hoh_mgpu* m);
+int hoh_mgpu_transport(const hoh_mgpu* m);
+/* choh.cpp:394-527 over all devices: device r encodes a band of tile rows (choh.cpp:464-500) of
+ * the host image h_rgb; one RCCL group gathers the blobs over xGMI behind hoh_file_prefix into
+ * the file d_out on the first device.  Same bytes and printed size as hoh_encode_image. */
+int hoh_mgpu_encode_image(hoh_mgpu* m, const uint8_t* h_rgb, int W, int H, int speed, uint8_t* d_out, size_t cap,
+                          size_t* out_size, size_t* printed);
+/* dhoh.cpp:297-396 over all devices: the file d_hoh (size bytes, on the first device) -> the host
+ * image h_rgb (W*H*3 bytes, cap at least that).  The tile table is parsed on the host, one RCCL
+ * group sends each device its tiles' bytes, each decodes its band. */
+int hoh_mgpu_decode_image(hoh_mgpu* m, const uint8_t* d_hoh, size_t size, uint8_t* h_rgb, size_t cap, int* W,
+                          int* H);
+
 /* ---- entropy stream level (host buffers; one call = one stream, batched inside) --------- */
 
 /* Replaces encode_entropy(uint16_t*, size_t, size_t, uint8_t*, uint32_t, uint8_t)

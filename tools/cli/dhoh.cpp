@@ -1,15 +1,18 @@
 // dhoh drop-in (dhoh.cpp:297-420): `dhoh in.hoh out.rgb` on the GPU.  Decodes tiled RGB .hoh
 // files as written by choh -s0 (the reference crashes on them) and writes the raw
 // interleaved RGB bytes.  Return codes: 3/4 not a .hoh, 5 unknown pixel format, and the
-// library's status code for anything it cannot decode.
+// library's status code for anything it cannot decode.  `--gpus N` / `--devices a,b,..`
+// (tools/cli/gpus.h) decode over several GPUs in this process (hoh_mgpu_decode_image).
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
 #include "../../include/hoh_ans.h"
+#include "gpus.h"
 
 int main(int argc, char** argv) {
+  const std::vector<int> devices = take_devices(argc, argv);
   if (argc == 2 && (!std::strcmp(argv[1], "--help") || !std::strcmp(argv[1], "-h"))) {
     std::printf("usage: dhoh infile.hoh outfile.rgb\n");
     return 0;
@@ -38,21 +41,28 @@ int main(int argc, char** argv) {
   if (r != HOH_OK) { std::fprintf(stderr, "dhoh: %s\n", hoh_strerror(r)); return r; }
   std::printf("width: %d\nheight: %d\n", W, H);
   hoh_ctx* ctx = nullptr;
-  r = hoh_ctx_create(&ctx, 0);
+  hoh_mgpu* mg = nullptr;
+  r = devices.size() > 1 ? hoh_mgpu_create(&mg, (int)devices.size(), devices.data()) : hoh_ctx_create(&ctx, 0);
   if (r != HOH_OK) { std::fprintf(stderr, "dhoh: %s\n", hoh_strerror(r)); return r; }
   const size_t raw = (size_t)W * H * 3;
   uint8_t *d_in = nullptr, *d_rgb = nullptr;
-  if (hipMalloc(&d_in, in.size()) != hipSuccess || hipMalloc(&d_rgb, raw) != hipSuccess) return HOH_E_HIP;
+  if (mg) (void)hipSetDevice(devices[0]);
+  if (hipMalloc(&d_in, in.size()) != hipSuccess || (!mg && hipMalloc(&d_rgb, raw) != hipSuccess)) return HOH_E_HIP;
   if (hipMemcpy(d_in, in.data(), in.size(), hipMemcpyHostToDevice) != hipSuccess) return HOH_E_HIP;
-  r = hoh_decode_image(ctx, d_in, in.size(), d_rgb, raw, &W, &H, nullptr);
-  if (r != HOH_OK) { std::fprintf(stderr, "dhoh: %s\n", hoh_strerror(r)); return r; }
   std::vector<uint8_t> out(raw);
-  if (hipMemcpy(out.data(), d_rgb, raw, hipMemcpyDeviceToHost) != hipSuccess) return HOH_E_HIP;
+  if (mg) {
+    r = hoh_mgpu_decode_image(mg, d_in, in.size(), out.data(), raw, &W, &H);
+  } else {
+    r = hoh_decode_image(ctx, d_in, in.size(), d_rgb, raw, &W, &H, nullptr);
+    if (r == HOH_OK && hipMemcpy(out.data(), d_rgb, raw, hipMemcpyDeviceToHost) != hipSuccess) r = HOH_E_HIP;
+  }
+  if (r != HOH_OK) { std::fprintf(stderr, "dhoh: %s\n", hoh_strerror(r)); return r; }
   FILE* o = std::fopen(argv[2], "wb");
   if (!o || std::fwrite(out.data(), 1, raw, o) != raw) { std::printf("could not write %s\n", argv[2]); return 3; }
   std::fclose(o);
   (void)hipFree(d_in);
-  (void)hipFree(d_rgb);
-  hoh_ctx_destroy(ctx);
+  if (d_rgb) (void)hipFree(d_rgb);
+  if (mg) hoh_mgpu_destroy(mg);
+  if (ctx) hoh_ctx_destroy(ctx);
   return 0;
 }
