@@ -1,8 +1,11 @@
 """GPU decode: lossless round trip of choh -s0 files (with and without the side index), decode
 of files made by the reference itself, and the stream / plane level drop-in entry points."""
+import os
+
 import numpy as np
 import pytest
 
+import hoh_ans
 from gen import make_plane, make_symbols
 
 pytestmark = pytest.mark.gpu
@@ -134,3 +137,16 @@ def test_subtract_green(hoh, orc):
     b = orc.subtract_green(img)
     for x, y in zip(a, b):
         assert np.array_equal(x, y)
+
+
+def test_entropy_roundtrip_text_pb12():
+    """entropy_roundtrip_test.sh's shape on the GPU: a text file's bytes as one stream (range 256,
+    prob_bits 12: the generic chain), bytes equal to the oracle's and a lossless round trip.  The
+    reference's own input (its source text) is not shipped; this repository's bench.py stands in."""
+    import oracle
+    data = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py"), "rb").read()
+    sym = np.frombuffer(data, np.uint8).astype(np.uint16)
+    got = hoh_ans.encode_entropy(sym, 256, 12)
+    assert bytes(got) == bytes(oracle.encode_entropy(sym, 256, 12))
+    dec, bp = hoh_ans.decode_entropy(got)
+    assert bytes(np.asarray(dec, np.uint8)) == data and bp == len(got)
