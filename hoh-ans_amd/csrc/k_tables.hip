@@ -105,26 +105,71 @@ __global__ __launch_bounds__(64) void k_tables(EncodeJob j, SidMap sm) {
   const uint32_t target = 1u << pb;
   for (uint32_t i = 1 + lane; i <= range; i += 64) cum[i] = (uint32_t)(((uint64_t)target * cum[i]) / total);
   __syncthreads();
+  // Symbols scaled to zero width steal one slot each (stattools.hpp:28-58).  The reference fixes
+  // them in index order, each time from the first symbol of smallest width > 1; stealing never
+  // touches a zero-width symbol and leaves the victim the unique smallest until it reaches width
+  // 1, so the candidates (width > 1) are drained in (width, index) order, each giving width - 1
+  // slots.  All Z steals are therefore placed at once: every candidate below a threshold width
+  // m* drops to 1, the first q of width m* (by index) too, the next one gives rem slots, where
+  // the threshold follows from the per-width capacities.  Widths then rebuild cum by a scan.
+  uint32_t Z = 0;
   for (uint32_t base = 0; base < range; base += 64) {
     const uint32_t i0 = base + lane;
-    uint64_t zm = __ballot(i0 < range && fr[i0] && cum[i0 + 1] == cum[i0]);
-    while (zm) {
-      const uint32_t i = base + (__ffsll((unsigned long long)zm) - 1);
-      zm &= zm - 1;
-      uint64_t key = ~0ull;
-      for (uint32_t jj = lane; jj < range; jj += 64) {
-        uint32_t f = cum[jj + 1] - cum[jj];
-        if (f > 1) { uint64_t k = ((uint64_t)f << 32) | jj; key = k < key ? k : key; }
+    Z += __popcll(__ballot(i0 < range && fr[i0] && cum[i0 + 1] == cum[i0]));
+  }
+  if (Z) {
+    uint32_t R = Z, mprev = 1, mstar = 0, q = 0, rem = 0;
+    for (;;) {
+      uint32_t m = ~0u;
+      for (uint32_t i = lane; i < range; i += 64) {
+        const uint32_t w = cum[i + 1] - cum[i];
+        if (w > mprev && w < m) m = w;
       }
-      key = wave_min_u64(key);
-      if (key == ~0ull) { if (lane == 0) s_err = 3; break; }
-      const uint32_t best = (uint32_t)key;
-      if (best < i) {
-        for (uint32_t jj = best + 1 + lane; jj <= i; jj += 64) cum[jj]--;
-      } else {
-        for (uint32_t jj = i + 1 + lane; jj <= best; jj += 64) cum[jj]++;
+      for (int o = 32; o > 0; o >>= 1) { const uint32_t u = __shfl_xor(m, o); m = u < m ? u : m; }
+      if (m == ~0u) { if (lane == 0) s_err = 3; break; }        // nothing left to steal from
+      uint32_t c = 0;
+      for (uint32_t base = 0; base < range; base += 64) {
+        const uint32_t i0 = base + lane;
+        c += __popcll(__ballot(i0 < range && cum[i0 + 1] - cum[i0] == m));
+      }
+      if ((uint64_t)c * (m - 1) >= R) { mstar = m; q = R / (m - 1); rem = R % (m - 1); break; }
+      R -= c * (m - 1);
+      mprev = m;
+    }
+    __syncthreads();
+    if (!s_err) {
+      // final widths into fr (fr[i] > 0 still marks presence for the zero test)
+      uint32_t rank = 0;                                     // width-m* symbols before this chunk
+      for (uint32_t base = 0; base < range; base += 64) {
+        const uint32_t i0 = base + lane;
+        const uint32_t w = i0 < range ? cum[i0 + 1] - cum[i0] : 0;
+        const bool atm = i0 < range && w == mstar;
+        const uint64_t bm = __ballot(atm);
+        const uint32_t r = rank + __popcll(bm & ((1ull << lane) - 1));
+        rank += __popcll(bm);
+        uint32_t nw = w;
+        if (i0 < range) {
+          if (fr[i0] && w == 0) nw = 1;
+          else if (w > 1 && w < mstar) nw = 1;
+          else if (atm) nw = r < q ? 1 : (r == q ? w - rem : w);
+        }
+        __syncthreads();
+        if (i0 < range) fr[i0] = nw;
       }
       __syncthreads();
+      // cum = exclusive scan of the final widths
+      const uint32_t ch = (range + 63) / 64;
+      const uint32_t a0 = lane * ch, a1 = min(range, a0 + ch);
+      uint32_t loc = 0;
+      for (uint32_t i = a0; i < a1; i++) loc += fr[i];
+      uint32_t inc = loc;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(inc, o);
+        if (lane >= o) inc += u;
+      }
+      uint32_t run2 = inc - loc;
+      __syncthreads();
+      for (uint32_t i = a0; i < a1; i++) { run2 += fr[i]; cum[i + 1] = run2; }
     }
   }
   __syncthreads();

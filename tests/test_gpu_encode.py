@@ -119,3 +119,25 @@ def test_choh_8192_golden(hoh, golden):
     assert n == f["out"]["len"]
     assert hashlib.sha256(data).hexdigest() == f["out"]["sha256"]
     assert printed == f["printed"]
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("pb", [9, 10, 12, 15])
+def test_normalize_steals_many_levels(seed, pb):
+    """normalize_freqs (stattools.hpp:13-70) with many symbols scaled to zero width, so the steals
+    drain several width levels (k_tables places them all at once): stream bytes equal the
+    oracle's for skewed histograms with long tails of rare symbols."""
+    import oracle
+    import hoh_ans
+    rng = np.random.default_rng(1000 + seed * 7 + pb)
+    rng_sz = 512
+    n = int(rng.integers(3000, 60000))
+    body = np.minimum(rng.geometric(rng.uniform(0.05, 0.5), n), 40).astype(np.int64)
+    tail = rng.choice(np.arange(41, rng_sz), size=int(rng.integers(50, 400)), replace=True)
+    mids = rng.choice(np.arange(41, rng_sz), size=int(rng.integers(0, 300)))
+    sym = np.concatenate([body, tail, np.repeat(mids, rng.integers(1, 6, mids.size))])
+    rng.shuffle(sym)
+    sym = sym.astype(np.uint16)
+    want = oracle.encode_entropy(sym, rng_sz, pb)
+    got = hoh_ans.encode_entropy(sym, rng_sz, pb)
+    assert bytes(got) == bytes(want)
