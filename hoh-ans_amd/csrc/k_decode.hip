@@ -598,6 +598,7 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams) {
         fetch4(fill, pend);                                  // lands at the first group
       }
       uint4* o4 = (uint4*)(out + s0);
+      uint32_t pk[32];                                       // 64 symbols: one whole 128-B line
       for (uint32_t g = 0; g < DSEG / 16; g++) {
         // land the words fetched a group ago (fill + 4 - wi <= DR_RW held when they were issued,
         // so no unread word is overwritten)
@@ -608,19 +609,23 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams) {
         }
         hp = fill + 4 - wi <= DR_RW;
         if (hp) fetch4(fill, pend);
-        uint32_t pk[8];
+        const uint32_t q = (g & 3) * 8;
 #pragma unroll
         for (int u = 0; u < 16; u++) {
           const uint32_t nw = rg[(wi & (DR_RW - 1)) * DR_T];
           const uint32_t slot = (uint32_t)x & mask;
           uint32_t sym, cc, f;
           tb.lookup(slot, sym, cc, f);
-          if (u & 1) pk[u >> 1] |= sym << 16; else pk[u >> 1] = sym;
+          if (u & 1) pk[q + (u >> 1)] |= sym << 16; else pk[q + (u >> 1)] = sym;
           x = (uint64_t)f * (x >> pb) + (slot - cc);       // Rans64DecAdvance
           if (x < (1ull << 31)) { x = (x << 32) | nw; wi++; }
         }
-        o4[2 * g] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-        o4[2 * g + 1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
+        if ((g & 3) == 3) {
+          // the lane's whole 128-B line at once: 32-B pieces from 64 lanes 512 B apart left
+          // partial lines for the memory side (WRITE_SIZE 1.6x the residual bytes)
+#pragma unroll
+          for (int e = 0; e < 8; e++) o4[2 * (g - 3) + e] = make_uint4(pk[4 * e], pk[4 * e + 1], pk[4 * e + 2], pk[4 * e + 3]);
+        }
       }
       if (x != want || wi > d.words) bad = true;
       continue;
@@ -815,6 +820,10 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v, uint32_t old) {
   return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xf, 0xf, false);
 }
 
+typedef unsigned short dus2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ dus2 as_d2(uint32_t v) { return __builtin_bit_cast(dus2, v); }
+__device__ __forceinline__ uint32_t as_u32d(dus2 v) { return __builtin_bit_cast(uint32_t, v); }
+
 __device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
   return max(min(a, b), min(max(a, b), c));
 }
@@ -855,9 +864,8 @@ __global__ __launch_bounds__(64) void k_dunpred_fast(DecJob j) {
   const DecTile ti = j.tiles[t];
   if (ti.err || !unpred_fast(j, t, ti)) return;
   uint8_t* ring = lds;                                        // [64][ORING_PITCH]
-  uint16_t* lastG = (uint16_t*)(lds + 64 * ORING_PITCH);
-  uint16_t* lastR = lastG + j.tw;
-  uint16_t* lastB = lastR + j.tw;
+  uint32_t* lastRB = (uint32_t*)(lds + 64 * ORING_PITCH);     // R' | B' << 16 of the band's last row
+  uint16_t* lastG = (uint16_t*)(lastRB + j.tw);
   const int lane = threadIdx.x;
   const int w = ti.w, h = ti.h, nst = w + 63;
   const uint16_t* plG = j.dsym + (size_t)(t * 3) * j.plane_cap;
@@ -901,8 +909,10 @@ __global__ __launch_bounds__(64) void k_dunpred_fast(DecJob j) {
     uint4 g0 = chunk(plG, F0), r0c = chunk(plR, F0), b0c = chunk(plB, F0);
     uint4 g1 = chunk(plG, F0 + 8), r1c = chunk(plR, F0 + 8), b1c = chunk(plB, F0 + 8);
     uint4 g2, r2c, b2c;
-    uint32_t cG = 0, cR = 0, cB = 0;      // this lane's value at the previous step (L)
-    uint32_t pG = 128, pR = 256, pB = 256; // T of the previous step (TL)
+    // R' and B' (9-bit planes) travel as one packed pair R' | B' << 16: the MED's uint16
+    // gradient wrap (Q8) is the packed 16-bit wrap, so both planes cost one set of packed ops
+    uint32_t cG = 0, cRB = 0;              // this lane's values at the previous step (L)
+    uint32_t pG = 128, pRB = 0x01000100u;  // T of the previous step (TL)
     int flushed = 0;
     auto group = [&](int s0, const uint4& ga, const uint4& gb, uint4& gn, const uint4& ra, const uint4& rb, uint4& rn,
                      const uint4& ba, const uint4& bb, uint4& bn) {
@@ -924,23 +934,27 @@ __global__ __launch_bounds__(64) void k_dunpred_fast(DecJob j) {
         const int st = s0 + u;
         const int x = st - lane;
         const uint32_t rG = (qG[u >> 1] >> ((u & 1) * 16)) & 0xffffu;
-        const uint32_t rR = (qR[u >> 1] >> ((u & 1) * 16)) & 0xffffu;
-        const uint32_t rB = (qB[u >> 1] >> ((u & 1) * 16)) & 0xffffu;
-        uint32_t oG = 128, oR = 256, oB = 256;        // lane 0: row above the band
-        if (r0 > 0 && lane == 0 && x < w) { oG = lastG[x]; oR = lastR[x]; oB = lastB[x]; }
-        const uint32_t TG = wave_shr1(cG, oG), TR = wave_shr1(cR, oR), TB = wave_shr1(cB, oB);
+        // R' residual in the low half, B' in the high half: one byte permute
+        const uint32_t rRB = __builtin_amdgcn_perm(qB[u >> 1], qR[u >> 1], (u & 1) ? 0x07060302u : 0x05040100u);
+        uint32_t oG = 128, oRB = 0x01000100u;          // lane 0: row above the band
+        if (r0 > 0 && lane == 0 && x < w) { oG = lastG[x]; oRB = lastRB[x]; }
+        const uint32_t TG = wave_shr1(cG, oG), TRB = wave_shr1(cRB, oRB);
         const bool xz = x <= 0;
-        const uint32_t LG = xz ? 128u : cG, LR = xz ? 256u : cR, LB = xz ? 256u : cB;
-        const uint32_t AG = xz ? 128u : pG, AR = xz ? 256u : pR, AB = xz ? 256u : pB;
+        const uint32_t LG = xz ? 128u : cG, LRB = xz ? 0x01000100u : cRB;
+        const uint32_t AG = xz ? 128u : pG, ARB = xz ? 0x01000100u : pRB;
         const uint32_t vG = (rG + med3u(TG, LG, (TG + LG - AG) & 0xffffu) + 128u) & 255u;
-        const uint32_t vR = (rR + med3u(TR, LR, (TR + LR - AR) & 0xffffu) + 256u) & 511u;
-        const uint32_t vB = (rB + med3u(TB, LB, (TB + LB - AB) & 0xffffu) + 256u) & 511u;
-        pG = TG; pR = TR; pB = TB;
-        cG = vG; cR = vR; cB = vB;
+        const dus2 t2 = as_d2(TRB), l2 = as_d2(LRB);
+        const dus2 g2 = t2 + l2 - as_d2(ARB);
+        const dus2 m2 = __builtin_elementwise_max(__builtin_elementwise_min(t2, l2),
+                                                  __builtin_elementwise_min(__builtin_elementwise_max(t2, l2), g2));
+        const uint32_t vRB = as_u32d(as_d2(rRB) + m2 + (dus2)(256)) & 0x01ff01ffu;
+        pG = TG; pRB = TRB;
+        cG = vG; cRB = vRB;
         if (rowok && x >= 0 && x < w) {
           uint8_t* o = orow + (x & 127) * 3;
-          o[0] = (uint8_t)(vR + vG); o[1] = (uint8_t)vG; o[2] = (uint8_t)(vB + vG);
-          if (lane == last) { lastG[x] = (uint16_t)vG; lastR[x] = (uint16_t)vR; lastB[x] = (uint16_t)vB; }
+          const uint32_t rb = vRB + vG * 0x10001u;    // R' + G | (B' + G) << 16, no carry across
+          o[0] = (uint8_t)rb; o[1] = (uint8_t)vG; o[2] = (uint8_t)(rb >> 16);
+          if (lane == last) { lastG[x] = (uint16_t)vG; lastRB[x] = vRB; }
         }
       }
       // columns < s0 + UP_P - 63 are complete in every row: flush whole 64-column chunks before
