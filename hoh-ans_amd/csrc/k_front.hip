@@ -19,6 +19,8 @@
 // ring allows (only untiled images) read their neighbours from memory instead.
 #include "hoh_internal.h"
 
+#include <stdlib.h>
+
 // Ring of RING positions (stored twice): a block's writes land while the slowest wave may still
 // read the previous block's neighbourhood, so the span in use is [q - 256 - max(w + 1, 67), q + 512)
 // and RING >= 768 + max(w + 1, 67).  Tiles up to 271 wide (every tiled image) use 1040 positions
@@ -436,9 +438,220 @@ void launch_palette(const EncodeJob& j, hipStream_t s) {
   hipLaunchKernelGGL(k_palette, dim3(j.ntiles < 128 ? j.ntiles : 128), dim3(NT), 0, s, j);
 }
 
+// ---------------------------------------------------------------- full 256 x 256 tiles
+//
+// Every tile of an image whose sides are multiples of 256 (the bench's 8192^2 and 16384^2) is a
+// full 256 x 256 tile, and k_front256 walks it with every neighbour in registers instead of an
+// LDS pixel ring behind block barriers.  Wave v of the tile's workgroup owns rows 64v .. 64v+63 and
+// walks them in raster order one 64-pixel chunk (a quarter row) at a time: L is a DPP wave shift
+// of the chunk (lane 0 takes lane 63 of the chunk to the left), T the same lane of the row above
+// (kept from the previous row; the stripe's first row reads it from memory), TL a shift of T.  The
+// LZ screen keeps the exact test of k_front (a window q..q+3 is a candidate iff it equals one of
+// the 64 windows before it): the chunk's 64 window fingerprints go into a wave-private table and
+// are looked up in the previous chunk's table, so each window is fingerprinted and inserted once
+// (k_front needs two of each); the two tables alternate, each cleared slot by slot by the lanes
+// that filled it.  Positions whose fingerprint occurs twice get the exact pixel comparison from a
+// per-wave LDS pixel ring.  Candidate words, residuals, histograms and tile flags are the same
+// as k_front's.
+#define F2_TAB 256            // slots of a chunk's fingerprint table (64 keys)
+#define F2_RING 256           // positions of a wave's pixel ring (the exact LZ check)
+
+__device__ __forceinline__ uint32_t wshl1(uint32_t v, uint32_t old) {   // lane l <- lane l+1, lane 63 <- old
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x130, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t wshr1(uint32_t v, uint32_t old) {   // lane l <- lane l-1, lane 0 <- old
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t lane_of(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+
+// lookup of key k in a (read-only) table: true if present
+__device__ __forceinline__ bool wt_find(const uint32_t* key, uint32_t k) {
+  uint32_t sl = (k >> 1) & (F2_TAB - 1);
+  for (int probe = 0; probe < F2_TAB; probe++) {
+    const uint32_t o = key[sl];
+    if (o == k) return true;
+    if (o == 0u) return false;
+    sl = (sl + 1) & (F2_TAB - 1);
+  }
+  return false;
+}
+
+// insert into a chunk table (open addressing); returns the slot (F2_TAB if none); a key met a
+// second time sets the slot's duplicate bit
+__device__ __forceinline__ uint32_t wt_put(uint32_t* key, uint32_t* dup, uint32_t k) {
+  uint32_t sl = (k >> 1) & (F2_TAB - 1);
+  for (int probe = 0; probe < F2_TAB; probe++) {
+    const uint32_t old = atomicCAS(&key[sl], 0u, k);
+    if (old == 0u) return sl;
+    if (old == k) { atomicOr(&dup[sl >> 5], 1u << (sl & 31)); return sl; }
+    sl = (sl + 1) & (F2_TAB - 1);
+  }
+  return F2_TAB;
+}
+
+__global__ __launch_bounds__(NT) void k_front256(EncodeJob j) {
+  __shared__ uint32_t tab[4][2][F2_TAB + 1];        // per wave: two alternating chunk tables
+  __shared__ uint32_t tdup[4][2][F2_TAB / 32];
+  __shared__ uint32_t pring[4][F2_RING];
+  __shared__ uint32_t hist[3 * 512 - 256];
+  __shared__ int s_notgrey, s_ncand;
+  const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int gt = j.t0 + t;
+  const int x0 = (gt % j.xt) * 256, y0 = (gt / j.xt) * 256;
+  const uint32_t npix = 256u * 256u;
+  for (int i = tid; i < 3 * 512 - 256; i += NT) hist[i] = 0;
+  for (int i = lane; i < 2 * (F2_TAB + 1); i += 64) tab[wv][i / (F2_TAB + 1)][i % (F2_TAB + 1)] = 0;
+  if (lane < 2 * (F2_TAB / 32)) tdup[wv][lane / (F2_TAB / 32)][lane % (F2_TAB / 32)] = 0;
+  if (tid == 0) { s_notgrey = 0; s_ncand = 0; }
+  uint16_t* res0 = j.sym + med_plane_off(j, t, 0);
+  uint16_t* res1 = j.sym + med_plane_off(j, t, 1);
+  uint16_t* res2 = j.sym + med_plane_off(j, t, 2);
+  uint64_t* cand = j.candbits + (size_t)t * (j.npix_cap / 64);
+  const uint8_t* img = j.rgb + ((size_t)y0 * j.W + x0) * 3;
+  const size_t pitch = (size_t)j.W * 3;
+  const bool lz = j.speed == 0;
+  uint32_t* ring = pring[wv];
+  // pixel (x = 64k + lane, y) of the tile: one unaligned dword that never leaves the tile (x = 0
+  // reads its own 3 bytes + the next pixel's first, others the previous pixel's last byte + theirs)
+  auto load_row = [&](int y, uint32_t* o) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int x = 64 * k + lane;
+      const uint8_t* p = img + (size_t)y * pitch + (size_t)x * 3;
+      uint32_t v;
+      __builtin_memcpy(&v, x ? p - 1 : p, 4);
+      o[k] = x ? (v >> 8) : (v & 0xffffffu);
+    }
+  };
+  const uint32_t GREY = 0x808080u;
+  const int ya = 64 * wv, yb = ya + 64;
+  uint32_t prow[4], cur[4], nxt[4];
+  if (ya > 0) load_row(ya - 1, prow);
+  else { prow[0] = prow[1] = prow[2] = prow[3] = GREY; }
+  load_row(ya, cur);
+  load_row(ya + 1, nxt);                              // ya + 1 < 256 always
+  __syncthreads();
+  uint32_t notgrey = 0;
+  int ncand = 0;
+  int cb = 0;                                         // table of the current chunk
+  uint32_t slot_prev = F2_TAB;                        // this lane's slot in the previous chunk's table
+  // the chunk before the stripe (row ya-1, quarter 3): its windows go into the "previous" table
+  // and its pixels into the ring, so the stripe's first chunk sees all 64 windows behind it
+  if (lz) {
+    if (ya > 0) {
+      const uint32_t pv = prow[3];
+      const uint32_t a1 = wshl1(pv, lane_of(cur[0], 0));
+      const uint32_t a2 = wshl1(a1, lane_of(cur[0], 1));
+      const uint32_t a3 = wshl1(a2, lane_of(cur[0], 2));
+      const uint32_t k = fp32(pv, a1, a2, a3);
+      slot_prev = wt_put(tab[wv][1], tdup[wv][1], k);
+      ring[(uint32_t)(ya * 256 - 64 + lane) & (F2_RING - 1)] = pv;
+    }
+    ring[(uint32_t)(ya * 256 + lane) & (F2_RING - 1)] = cur[0];
+  }
+  for (int y = ya; y < yb; y++) {
+    const bool hasT = y > 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t q = (uint32_t)y * 256u + 64u * k + lane;
+      const uint32_t v = cur[k];
+      const uint32_t g = (v >> 8) & 255u;
+      notgrey |= (v ^ (g * 0x010101u)) & 0xffffffu;
+      // neighbours (prediction.hpp:21-28: outside the tile the grey pixel 128,128,128)
+      const uint32_t lft = k ? lane_of(cur[k - 1], 63) : GREY;
+      const uint32_t tlf = k ? lane_of(prow[k - 1], 63) : GREY;
+      const uint32_t vL = wshr1(v, lft);              // x = 0 (k = 0, lane 0) gets grey
+      const uint32_t vT = hasT ? prow[k] : GREY;
+      const uint32_t vTL = hasT ? wshr1(prow[k], tlf) : GREY;
+      const uint32_t gL = (vL >> 8) & 255u, gT = (vT >> 8) & 255u, gTL = (vTL >> 8) & 255u;
+      const uint32_t gg = (gT + gL - gTL) & 0xffffu;
+      const uint32_t pg = max(min(gT, gL), min(max(gT, gL), gg));
+      const uint32_t rg = (g - pg + 128u) & 255u;
+      const us2 tt = as_us2(rb_form(vT)), ll = as_us2(rb_form(vL)), tl = as_us2(rb_form(vTL));
+      const us2 gr = tt + ll - tl;
+      const us2 mn = __builtin_elementwise_min(tt, ll), mx = __builtin_elementwise_max(tt, ll);
+      const us2 pr = __builtin_elementwise_max(mn, __builtin_elementwise_min(mx, gr));
+      const uint32_t rrb = as_u32(as_us2(rb_form(v)) - pr + (us2)(256)) & 0x01ff01ffu;
+      const uint32_t rr = rrb & 0xffffu, rb = rrb >> 16;
+      res0[q] = (uint16_t)rg;
+      res1[q] = (uint16_t)rr;
+      res2[q] = (uint16_t)rb;
+      atomicAdd(&hist[rg], 1u);
+      atomicAdd(&hist[256 + rr], 1u);
+      atomicAdd(&hist[768 + rb], 1u);
+      if (!lz) continue;
+      // the window q .. q+3 (the next chunk's first pixels for the last lanes)
+      const uint32_t nx = k < 3 ? cur[k + 1] : nxt[0];
+      const uint32_t v1 = wshl1(v, lane_of(nx, 0));
+      const uint32_t v2 = wshl1(v1, lane_of(nx, 1));
+      const uint32_t v3 = wshl1(v2, lane_of(nx, 2));
+      ring[(q + 64u) & (F2_RING - 1)] = (q + 64u < npix) ? nx : 0u;   // the ring runs a chunk ahead
+      const bool win = q + 3 < npix;
+      const uint32_t hq = win ? fp32(v, v1, v2, v3) : 0u;
+      uint32_t* tc = tab[wv][cb];
+      uint32_t* dc = tdup[wv][cb];
+      const uint32_t* tp = tab[wv][cb ^ 1];
+      const bool inprev = hq && wt_find(tp, hq);
+      const uint32_t sq = hq ? wt_put(tc, dc, hq) : F2_TAB;
+      const bool hit = inprev || (sq < F2_TAB && ((dc[sq >> 5] >> (sq & 31)) & 1));
+      const uint64_t flag = __ballot(hit);
+      uint64_t word = 0;
+      if (flag) {
+        // exact check (lz.hpp:37-42 with offset < 4), first back distance that matches
+        bool c = false;
+        if (hit) {
+          const uint32_t bmax = q < 64 ? q : 64;
+          for (uint32_t b = 1; b <= bmax && !c; b++) {
+            const uint32_t p = q - b;
+            c = ring[p & (F2_RING - 1)] == v && ring[(p + 1) & (F2_RING - 1)] == v1 &&
+                ring[(p + 2) & (F2_RING - 1)] == v2 && ring[(p + 3) & (F2_RING - 1)] == v3;
+          }
+        }
+        word = __ballot(c);
+      }
+      if (lane == 0) cand[q >> 6] = word;
+      ncand += lane == 0 ? __popcll(word) : 0;
+      // empty the previous chunk's table for the next chunk (wave-ordered: every lookup is done)
+      uint32_t* tpw = tab[wv][cb ^ 1];
+      tpw[slot_prev] = 0;                             // slot F2_TAB is a spare: no branch
+      if (lane < F2_TAB / 32) tdup[wv][cb ^ 1][lane] = 0;
+      slot_prev = sq;
+      cb ^= 1;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) { prow[k] = cur[k]; cur[k] = nxt[k]; }
+    if (y + 2 < 256) load_row(y + 2, nxt);
+  }
+  if (notgrey) atomicOr(&s_notgrey, 1);
+  if (ncand) atomicAdd(&s_ncand, ncand);
+  __syncthreads();
+  for (int i = tid; i < 3 * 512; i += NT) {
+    const int k = i / 512, sv = i % 512;
+    j.hist[(size_t)(t * j.spt + med_kind(j, k)) * 512 + sv] = k == 0 ? (sv < 256 ? hist[sv] : 0u) : hist[k * 512 - 256 + sv];
+  }
+  if (tid == 0) {
+    TileInfo ti;
+    ti.x0 = x0; ti.y0 = y0; ti.w = 256; ti.h = 256;
+    ti.colours = j.ncol[t];
+    uint32_t fl = 0;
+    if (!s_notgrey) fl |= TF_GREY;
+    if (!s_notgrey && ti.colours != -1 && ti.colours <= 2) fl |= TF_BINARY;
+    if (!s_notgrey && !(fl & TF_BINARY)) fl |= TF_UNREPRODUCIBLE;   // choh.cpp:196-205 copies garbage
+    if (s_notgrey && ti.colours != -1) fl |= TF_PALETTE_CAND;
+    ti.flags = fl;
+    ti.nmatch = 0;
+    ti.ncand = (uint32_t)s_ncand;
+    ti.size = 0; ti.lz_bytes = 0; ti.off = 0;
+    ti.mode = (fl & TF_GREY) ? 0 : 128;
+    ti.pad = 0;
+    j.tiles[t] = ti;
+  }
+}
+
 void launch_front(const EncodeJob& j, hipStream_t s) {
   hipLaunchKernelGGL(k_colours, dim3(j.ntiles), dim3(NT), 0, s, j);
-  if (j.tw <= RING_SMALL_MAX_W) hipLaunchKernelGGL(k_front<RING_SMALL>, dim3(j.ntiles), dim3(NT), 0, s, j);
+  if (j.tw == 256 && j.th == 256 && !getenv("HOH_FRONT_OLD")) hipLaunchKernelGGL(k_front256, dim3(j.ntiles), dim3(NT), 0, s, j);
+  else if (j.tw <= RING_SMALL_MAX_W) hipLaunchKernelGGL(k_front<RING_SMALL>, dim3(j.ntiles), dim3(NT), 0, s, j);
   else if (j.tw <= RING_MAX_W) hipLaunchKernelGGL(k_front<RING>, dim3(j.ntiles), dim3(NT), 0, s, j);
   else hipLaunchKernelGGL(k_front_wide, dim3(j.ntiles), dim3(NT), 0, s, j);
 }
