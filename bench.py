@@ -63,7 +63,7 @@ sys.path.insert(0, os.path.join(ROOT, "hoh-ans_amd"))
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 DOM = "rans_enc_fast"   # stage name of the dominant kernel (k_rans_fast)
-PMC_KERNELS = {"k_rans_fast": "rans_enc_fast", "k_front": "front", "k_drans": "drans",
+PMC_KERNELS = {"k_rans_fast": "rans_enc_fast", "k_front": "front", "k_front256": "front", "k_drans": "drans",
                "k_dunpred_fast": "dunpred_fast", "k_tables": "tables", "k_streambytes": "streambytes",
                "k_dunpred_lz": "dunpred_lz", "k_nuke": "nuke"}
 

@@ -19,8 +19,6 @@
 // ring allows (only untiled images) read their neighbours from memory instead.
 #include "hoh_internal.h"
 
-#include <stdlib.h>
-
 // Ring of RING positions (stored twice): a block's writes land while the slowest wave may still
 // read the previous block's neighbourhood, so the span in use is [q - 256 - max(w + 1, 67), q + 512)
 // and RING >= 768 + max(w + 1, 67).  Tiles up to 271 wide (every tiled image) use 1040 positions
@@ -650,7 +648,7 @@ __global__ __launch_bounds__(NT) void k_front256(EncodeJob j) {
 
 void launch_front(const EncodeJob& j, hipStream_t s) {
   hipLaunchKernelGGL(k_colours, dim3(j.ntiles), dim3(NT), 0, s, j);
-  if (j.tw == 256 && j.th == 256 && !getenv("HOH_FRONT_OLD")) hipLaunchKernelGGL(k_front256, dim3(j.ntiles), dim3(NT), 0, s, j);
+  if (j.tw == 256 && j.th == 256) hipLaunchKernelGGL(k_front256, dim3(j.ntiles), dim3(NT), 0, s, j);
   else if (j.tw <= RING_SMALL_MAX_W) hipLaunchKernelGGL(k_front<RING_SMALL>, dim3(j.ntiles), dim3(NT), 0, s, j);
   else if (j.tw <= RING_MAX_W) hipLaunchKernelGGL(k_front<RING>, dim3(j.ntiles), dim3(NT), 0, s, j);
   else hipLaunchKernelGGL(k_front_wide, dim3(j.ntiles), dim3(NT), 0, s, j);
