@@ -430,6 +430,8 @@ __device__ bool dec_run(const DecJob& j, const DecStream& d, const uint32_t* cum
 #define DR_NB 1024    // 32-slot buckets (prob_bits <= 15)
 #define DR_FIXED ((2 * DR_NB + 2 * 512) * 4)   // LDS bytes before the payload stage
 #define DR_RW 16      // payload ring words per thread (ringed k_drans)
+#define DR_SMEM (DR_FIXED + DR_RW * DR_T * 4 + 16)   // + the 4 wave totals of the table build (no static
+                                                      // LDS: table offsets fold into the ds offsets)
 
 __device__ __forceinline__ void dec_stored(const DecJob& j, int sid, const DecStream& d) {
   uint16_t* out = j.dsym + d.out_off;
@@ -442,20 +444,58 @@ __device__ __forceinline__ void dec_stored(const DecJob& j, int sid, const DecSt
 
 // Exact slot -> symbol lookup in two LDS reads.  Symbols present in the table get a compact
 // index k (ascending); per 32-slot bucket b: k0 = index of the symbol covering slot 32b and a
-// mask with bit i set where a symbol starts at slot 32b + i (i > 0); per k: {c | f << 16, sym}.
+// mask with bit i set where a symbol starts at slot 32b + i (i > 0); per k: {f, c | sym << 16}.
 // k(slot) = k0 + popcount(bits 1..slot&31 of the mask).  12 KB in all (a byte per slot was 32 KB).
 struct DrTables {
   uint2* bk;    // [DR_NB] {start mask, k0}
-  uint2* sy;    // [512]   {c | f << 16, symbol}
+  uint2* sy;    // [512]   {f, c | symbol << 16}
   __device__ __forceinline__ void lookup(uint32_t slot, uint32_t& sym, uint32_t& c, uint32_t& f) const {
     const uint2 e = bk[slot >> 5];
     const uint32_t k = e.y + __popc(__builtin_amdgcn_ubfe(e.x, 1, slot & 31));
     const uint2 t = sy[k];
-    c = t.x & 0xffffu;
-    f = t.x >> 16;
-    sym = t.y;
+    f = t.x;
+    c = t.y & 0xffffu;
+    sym = t.y >> 16;
   }
 };
+
+// One Rans64DecAdvance + renormalisation (rans64.hpp:107-142) on the split state (xh, xl) for
+// prob_bits 7..15, in ~17 VALU operations: the bucket address straight from x, the popcount
+// accumulating onto k0, x = f * (x >> pb) + (slot - c) as ONE v_mad_u64_u32
+// f * lo32(x >> pb) + ((f * (xh >> pb)) << 32 | slot - c) (the 24-bit multiply is exact: f <= 2^15
+// and xh >> pb < 2^24 because x < 2^63 and pb >= 7), the renorm select on the halves.
+// bk / sy are LDS byte addresses; bmask = (mask >> 2) & ~7 turns x into the bucket's byte
+// offset.  Returns the table word whose high half is the symbol.
+// LDS loads by raw byte address (the kernel has no static LDS, so its dynamic area starts at 0):
+// through the extern array every address carried an add of the array's link-time base
+#ifdef __HIP_DEVICE_COMPILE__
+__device__ __forceinline__ uint2 lds_u2(uint32_t a) { return *(const __attribute__((address_space(3))) uint2*)(size_t)a; }
+__device__ __forceinline__ uint32_t lds_u32(uint32_t a) { return *(const __attribute__((address_space(3))) uint32_t*)(size_t)a; }
+#else
+__device__ uint2 lds_u2(uint32_t);
+__device__ uint32_t lds_u32(uint32_t);
+#endif
+
+__device__ __forceinline__ uint32_t dstep(uint32_t bk, uint32_t sy, uint32_t bmask,
+                                          uint32_t mask, uint32_t pb, uint32_t& xh, uint32_t& xl,
+                                          uint32_t nw, uint32_t& wi) {
+  const uint32_t slot = xl & mask;
+  const uint2 e = lds_u2(bk + ((xl >> 2) & bmask));
+  // v_bfe_u32 reads only bits [4:0] of its width operand: slot & 31 without the AND
+  const uint32_t k = __popc(__builtin_amdgcn_ubfe(e.x, 1, slot)) + e.y;
+  const uint2 t = lds_u2(sy + k * 8);
+  const uint32_t d = slot - (t.y & 0xffffu);
+  const uint32_t yl = __builtin_amdgcn_alignbit(xh, xl, pb);
+  const uint64_t acc = ((uint64_t)__umul24(t.x, xh >> pb) << 32) | d;
+  uint64_t x, co;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(x), "=s"(co) : "v"(t.x), "v"(yl), "v"(acc));
+  const uint32_t nh = (uint32_t)(x >> 32), nl = (uint32_t)x;
+  const bool r = x < (1ull << 31);
+  xh = r ? nl : nh;
+  xl = r ? nw : nl;
+  wi += r;
+  return t.y;
+}
 
 // Indexed decode (rans64.hpp:107-142): one 256-thread workgroup per stream, thread = segment of
 // HOH_SEG symbols starting from the encoder's checkpoint.  LDS holds the lookup tables (12 KB) and
@@ -465,7 +505,11 @@ struct DrTables {
 // Output is the flat plane: each thread stores its segment 16 symbols (32 B) at a time.
 __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams) {
   extern __shared__ __attribute__((aligned(16))) uint32_t dr_lds[];
-  if (dec_abort(j)) return;
+  uint32_t* wtot = dr_lds + (DR_FIXED + DR_RW * DR_T * 4) / 4;
+  // dec_abort through the dynamic area (read before the barrier that follows the table clear)
+  if (threadIdx.x == 0) wtot[0] = *(volatile const uint32_t*)j.gerr;
+  __syncthreads();
+  if (wtot[0]) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int sid = blockIdx.x;
   const DecStream d = j.streams[sid];
@@ -477,7 +521,6 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams) {
   tb.sy = (uint2*)(dr_lds + 2 * DR_NB);                       // 2 * 512 words
   uint32_t* pw = dr_lds + DR_FIXED / 4;                       // payload rings (DR_RW words per thread)
   uint32_t* cum_s = pw;                                       // range + 1 words, before the rings
-  __shared__ uint32_t wtot[DR_T / 64];
   for (uint32_t i = tid; i <= range; i += DR_T) cum_s[i] = j.cum[(size_t)sid * j.cum_stride + i];
   const uint32_t nb = (M + 31) >> 5;
   for (uint32_t b = tid; b < nb; b += DR_T) tb.bk[b] = make_uint2(0, 0);
@@ -500,7 +543,7 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams) {
     uint32_t k = incl - cnt;
     for (int q = 0; q < wv; q++) k += wtot[q];
     auto put = [&](uint32_t s, uint32_t c0, uint32_t c1, uint32_t kk) {
-      tb.sy[kk] = make_uint2(c0 | ((c1 - c0) << 16), s);
+      tb.sy[kk] = make_uint2(c1 - c0, c0 | (s << 16));
       for (uint32_t b = (c0 + 31) >> 5; b <= (c1 - 1) >> 5; b++) tb.bk[b].y = kk;   // buckets it starts
       if (c0 & 31) atomicOr(&tb.bk[c0 >> 5].x, 1u << (c0 & 31));
     };
@@ -554,7 +597,7 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams) {
       s1 = min(d.n, s0 + DSEG);
       if (sg + 1 < nseg) { const Checkpoint c2 = j.ck[xs.ckpt_off + sg + 1]; want = (uint64_t)c2.xl | ((uint64_t)c2.xh << 32); }
     }
-    if (act && s1 - s0 == DSEG) {
+    if (act && s1 - s0 == DSEG && pb >= 7) {
       // Payload word k of the stream = bytes P+4k .. P+4k+3 of the file.  The lane's ring holds
       // words [fill-DR_RW, fill) in slots k % DR_RW (slot-major: lanes read consecutive banks).
       // A 16-symbol group reads at most 8 words (each symbol takes <= 15 bits, a renorm adds 32,
@@ -597,37 +640,39 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams) {
         fill += 8;
         fetch4(fill, pend);                                  // lands at the first group
       }
+      // LDS byte addresses (dynamic area at 0): tables at 0 and 2 * DR_NB * 4, this lane's ring
+      // slot s at DR_FIXED + tid*4 + s*1024
+      const uint32_t bmask = (mask >> 2) & ~7u, t4 = (uint32_t)tid * 4;
+      uint32_t xh = (uint32_t)(x >> 32), xl = (uint32_t)x;
       uint4* o4 = (uint4*)(out + s0);
-      uint32_t pk[32];                                       // 64 symbols: one whole 128-B line
-      for (uint32_t g = 0; g < DSEG / 16; g++) {
-        // land the words fetched a group ago (fill + 4 - wi <= DR_RW held when they were issued,
-        // so no unread word is overwritten)
-        if (hp) { put4(fill, pend); fill += 4; }
-        while (fill - wi < 8) {                              // a lane that read fast: fetch now
-          uint32_t t[4];
-          fetch4(fill, t); put4(fill, t); fill += 4;
-        }
-        hp = fill + 4 - wi <= DR_RW;
-        if (hp) fetch4(fill, pend);
-        const uint32_t q = (g & 3) * 8;
+      for (uint32_t g4 = 0; g4 < DSEG / 64; g4++) {
+        uint32_t pk[32];                                     // 64 symbols: one whole 128-B line
 #pragma unroll
-        for (int u = 0; u < 16; u++) {
-          const uint32_t nw = rg[(wi & (DR_RW - 1)) * DR_T];
-          const uint32_t slot = (uint32_t)x & mask;
-          uint32_t sym, cc, f;
-          tb.lookup(slot, sym, cc, f);
-          if (u & 1) pk[q + (u >> 1)] |= sym << 16; else pk[q + (u >> 1)] = sym;
-          x = (uint64_t)f * (x >> pb) + (slot - cc);       // Rans64DecAdvance
-          if (x < (1ull << 31)) { x = (x << 32) | nw; wi++; }
-        }
-        if ((g & 3) == 3) {
-          // the lane's whole 128-B line at once: 32-B pieces from 64 lanes 512 B apart left
-          // partial lines for the memory side (WRITE_SIZE 1.6x the residual bytes)
+        for (int gi = 0; gi < 4; gi++) {
+          // land the words fetched a group ago (fill + 4 - wi <= DR_RW held when they were
+          // issued, so no unread word is overwritten)
+          if (hp) { put4(fill, pend); fill += 4; }
+          while (fill - wi < 8) {                            // a lane that read fast: fetch now
+            uint32_t t[4];
+            fetch4(fill, t); put4(fill, t); fill += 4;
+          }
+          hp = fill + 4 - wi <= DR_RW;
+          if (hp) fetch4(fill, pend);
 #pragma unroll
-          for (int e = 0; e < 8; e++) o4[2 * (g - 3) + e] = make_uint4(pk[4 * e], pk[4 * e + 1], pk[4 * e + 2], pk[4 * e + 3]);
+          for (int u = 0; u < 16; u += 2) {
+            const uint32_t w0 = lds_u32(DR_FIXED + (t4 | ((wi & (DR_RW - 1)) << 10)));
+            const uint32_t a = dstep(0, 2 * DR_NB * 4, bmask, mask, pb, xh, xl, w0, wi);
+            const uint32_t w1 = lds_u32(DR_FIXED + (t4 | ((wi & (DR_RW - 1)) << 10)));
+            const uint32_t b = dstep(0, 2 * DR_NB * 4, bmask, mask, pb, xh, xl, w1, wi);
+            pk[gi * 8 + u / 2] = __builtin_amdgcn_perm(b, a, 0x07060302u);   // the two high halves
+          }
         }
+        // the lane's whole 128-B line at once: 32-B pieces from 64 lanes 512 B apart left
+        // partial lines for the memory side (WRITE_SIZE 1.6x the residual bytes)
+#pragma unroll
+        for (int e = 0; e < 8; e++) o4[8 * g4 + e] = make_uint4(pk[4 * e], pk[4 * e + 1], pk[4 * e + 2], pk[4 * e + 3]);
       }
-      if (x != want || wi > d.words) bad = true;
+      if (xh != (uint32_t)(want >> 32) || xl != (uint32_t)want || wi > d.words) bad = true;
       continue;
     }
     if (!act) continue;
@@ -681,7 +726,7 @@ __device__ bool lane_decode(const DecJob& j, const DecStream& d, const uint32_t*
     for (int e = 0; e < 8; e++) {
       if (!((pres >> e) & 1)) continue;
       const uint32_t sy = 8 * lane + e, c0 = cum[sy], c1 = cum[sy + 1];
-      tb.sy[k] = make_uint2(c0 | ((c1 - c0) << 16), sy);
+      tb.sy[k] = make_uint2(c1 - c0, c0 | (sy << 16));
       for (uint32_t b = (c0 + 31) >> 5; b <= (c1 - 1) >> 5; b++) tb.bk[b].y = k;
       if (c0 & 31) atomicOr(&tb.bk[c0 >> 5].x, 1u << (c0 & 31));
       k++;
@@ -1369,7 +1414,7 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   ctx_mark(c, s, "dparse", false);
   if (indexed) {
     hipLaunchKernelGGL(k_dmatch, dim3((S + 255) / 256), dim3(256), 0, s, j, S);
-    hipLaunchKernelGGL(k_drans, dim3(S), dim3(DR_T), DR_FIXED + (size_t)DR_RW * DR_T * 4, s, j, S);
+    hipLaunchKernelGGL(k_drans, dim3(S), dim3(DR_T), DR_SMEM, s, j, S);
   } else {
     hipLaunchKernelGGL(k_drans_wave, dim3(S), dim3(64), DL_SMEM, s, j, S);
   }

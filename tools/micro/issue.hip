@@ -7,8 +7,8 @@
 #define R8(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
 template <int OP>
 __global__ void iss(uint32_t* out, uint64_t* cyc, uint32_t a) {
-  uint32_t x[8]; double d[8];
-  for (int i = 0; i < 8; ++i) { x[i] = threadIdx.x + i + a; d[i] = x[i]; }
+  uint32_t x[8]; double d[8]; uint64_t y[8];
+  for (int i = 0; i < 8; ++i) { x[i] = threadIdx.x + i + a; d[i] = x[i]; y[i] = x[i]; }
   double one = (double)(a & 1) + 1.0;
   uint64_t t0; asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0) :: "memory");
   for (int it = 0; it < 64; ++it) {
@@ -25,11 +25,19 @@ __global__ void iss(uint32_t* out, uint64_t* cyc, uint32_t a) {
     if (OP == 9) asm volatile("v_add3_u32 %0, %0, %1, %1" : "+v"(x[i]) : "v"(a)); \
     if (OP == 10) asm volatile("v_cmp_ge_u32_sdwa vcc, %0, %1 src0_sel:WORD_1 src1_sel:DWORD\n\tv_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(x[i]) : "v"(a) : "vcc"); \
     if (OP == 11) asm volatile("v_cndmask_b32_e64 %0, %0, %1, s[0:1]" : "+v"(x[i]) : "v"(a)); \
-    if (OP == 12) asm volatile("v_add_u32_e32 %0, %0, %0" : "+v"(x[0]));
+    if (OP == 12) asm volatile("v_add_u32_e32 %0, %0, %0" : "+v"(x[0])); \
+    if (OP == 13) { uint64_t co; asm volatile("v_mad_u64_u32 %0, %1, %2, %2, %0" : "+v"(y[i]), "=s"(co) : "v"(a)); } \
+    if (OP == 14) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(x[i]) : "v"(a)); \
+    if (OP == 15) asm volatile("v_bcnt_u32_b32 %0, %0, %1" : "+v"(x[i]) : "v"(a)); \
+    if (OP == 16) asm volatile("v_lshrrev_b64 %0, 3, %0" : "+v"(y[i])); \
+    if (OP == 17) asm volatile("v_cmp_gt_u64_e32 vcc, %2, %1\n\tv_cndmask_b32_e32 %0, %0, %3, vcc" : "+v"(x[i]) : "v"(y[i]), "v"(y[(i + 1) & 7]), "v"(a) : "vcc"); \
+    if (OP == 18) asm volatile("v_bfe_u32 %0, %0, 1, %1" : "+v"(x[i]) : "v"(a)); \
+    if (OP == 19) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(x[i]) : "v"(a), "s"(0x07060302u)); \
+    if (OP == 20) asm volatile("v_mul_hi_u32_u24 %0, %0, %1" : "+v"(x[i]) : "v"(a));
     R8(OPX)
   }
   uint64_t t1; asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1) :: "memory");
-  uint32_t acc = 0; for (int i = 0; i < 8; ++i) acc += x[i] + (uint32_t)d[i];
+  uint32_t acc = 0; for (int i = 0; i < 8; ++i) acc += x[i] + (uint32_t)d[i] + (uint32_t)y[i];
   out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
   if ((threadIdx.x & 63) == 0) cyc[blockIdx.x * 16 + (threadIdx.x >> 6)] = t1 - t0;
 }
@@ -61,5 +69,13 @@ int main() {
   run<10>("cmp_sdwa+cndmask", d_out, d_cyc);
   run<11>("v_cndmask_e64", d_out, d_cyc);
   run<12>("dep v_add_u32", d_out, d_cyc);
+  run<13>("v_mad_u64_u32", d_out, d_cyc);
+  run<14>("v_mul_hi_u32", d_out, d_cyc);
+  run<15>("v_bcnt_u32", d_out, d_cyc);
+  run<16>("v_lshrrev_b64", d_out, d_cyc);
+  run<17>("cmp_u64+cndmask", d_out, d_cyc);
+  run<18>("v_bfe_u32", d_out, d_cyc);
+  run<19>("v_perm_b32", d_out, d_cyc);
+  run<20>("v_mul_hi_u32_u24", d_out, d_cyc);
   return 0;
 }
