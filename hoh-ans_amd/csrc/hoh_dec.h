@@ -23,7 +23,7 @@ struct DecStream {        // one stream of a .hoh, as parsed by the decoder
   uint32_t words;         // rANS payload words
   uint32_t err;
   int32_t ix;             // matching index stream, -1 if none
-  uint32_t pad;
+  uint32_t blk;           // 1: decoded into the blocked plane layout (blk_pos, k_decode.hip)
 };
 
 struct DecTile {

@@ -49,6 +49,7 @@ struct DecJob {
   int nix;
   int t0;                       // global index of the first tile (shard decode)
   const uint32_t* tsizes;       // shard decode: tile byte sizes instead of the file's table
+  int blk_ok;                   // plane_cap holds the blocked layout of a 256-wide tile
 };
 
 __device__ __forceinline__ uint64_t rd_varint(const uint8_t* b, uint64_t& p) {
@@ -345,6 +346,10 @@ __global__ __launch_bounds__(64) void k_dparse(DecJob j) {
       ok = parse_stream(j, q, t * SK_PER_TILE + 3 + k, (size_t)(t * 3 + k) * j.plane_cap, lane);
       const uint32_t depth = k ? 9 : 8;
       if (ok && j.streams[t * SK_PER_TILE + 3 + k].range != (1u << depth)) ok = false;
+      // full-width tile plane without LZ copies: the blocked layout k_dunpred_fast reads
+      if (ok && lane == 0 && ti.w == 256 && j.blk_ok &&
+          j.streams[t * SK_PER_TILE + 3 + k].n == (uint32_t)ti.w * (uint32_t)ti.h)
+        j.streams[t * SK_PER_TILE + 3 + k].blk = 1;
     }
   }
   if (!ok && !err) err = 1;
@@ -377,29 +382,26 @@ __device__ __forceinline__ uint32_t ld_u32_unaligned(const uint8_t* base, uint64
   return __builtin_amdgcn_alignbyte(hi, lo, sh);
 }
 
-// Plane residuals of tiles without LZ matches are stored "skewed" for the wavefront unpredict:
-// band b (rows 64b..64b+63), step st, lane r hold the residual of (x = st - r, y = 64b + r), so
-// the 64 lanes of k_dunpred_fast read 128 contiguous bytes per plane per step.
-__device__ __forceinline__ uint32_t skew_pos(uint32_t x, uint32_t y, uint32_t w) {
-  const uint32_t r = y & 63;
-  return ((y >> 6) * (w + 63) + x + r) * 64 + r;
+// Blocked plane layout (residual planes of 256-wide tiles without LZ copies, DecStream.blk): row
+// y = 64b + r of the tile, column x lives in band b at 8-element column block K = x/8 + ceil(r/8),
+// block-major with the 64 rows of the band interleaved inside a block:
+//   pos = b * BLK_BAND + (K * 64 + r) * 8 + x % 8.
+// Skewing the blocks by ceil(r/8) makes the 8 columns k_dunpred_fast's lane r needs at step s
+// (x = s - r .. s - r + 7) lie in blocks s/8 and s/8 + 1 for every lane, so each of its residual
+// loads is one contiguous 1 KB (64 lanes x 16 B) instead of 64 scattered 16-B pieces; k_drans's
+// thread for row r stores each 8-symbol block as 16 B next to its neighbour rows' (full lines).
+#define BLK_NK 40                      // column blocks per band (32 + the skew of 8)
+#define BLK_BAND (BLK_NK * 64 * 8)     // elements per band
+__device__ __forceinline__ uint32_t blk_pos(uint32_t i) {
+  const uint32_t y = i >> 8, x = i & 255, r = y & 63;
+  return (y >> 6) * BLK_BAND + (((x >> 3) + ((r + 7) >> 3)) * 64 + r) * 8 + (x & 7);
 }
-
-// Decoded planes are flat (raster order); OutCursor keeps the skewed variant for reference only.
-__device__ __forceinline__ uint32_t skew_w(const DecJob&, int, uint32_t) { return 0u; }
 
 struct OutCursor {
   uint16_t* out;
-  uint32_t w, x, y;
-  __device__ OutCursor(uint16_t* o, uint32_t w_, uint32_t i) : out(o), w(w_), x(w_ ? i % w_ : 0), y(w_ ? i / w_ : 0) {}
-  __device__ __forceinline__ void put(uint32_t i, uint16_t v) {
-    if (w) {
-      out[skew_pos(x, y, w)] = v;
-      if (++x == w) { x = 0; y++; }
-    } else {
-      out[i] = v;
-    }
-  }
+  uint32_t blk;
+  __device__ OutCursor(uint16_t* o, uint32_t b, uint32_t) : out(o), blk(b) {}
+  __device__ __forceinline__ void put(uint32_t i, uint16_t v) { out[blk ? blk_pos(i) : i] = v; }
 };
 
 // rANS decode (rans64.hpp:107-142) of symbols [s0, s1) of stream d from state x.  Payload words
@@ -435,10 +437,9 @@ __device__ bool dec_run(const DecJob& j, const DecStream& d, const uint32_t* cum
 
 __device__ __forceinline__ void dec_stored(const DecJob& j, int sid, const DecStream& d) {
   uint16_t* out = j.dsym + d.out_off;
-  const uint32_t sw = skew_w(j, sid, d.n);
   for (uint32_t i = threadIdx.x; i < d.n; i += blockDim.x) {
     const uint16_t v = (uint16_t)get_bits(j.in, d.payload_off * 8 + (uint64_t)i * d.maxbits, d.maxbits);
-    out[sw ? skew_pos(i % sw, i / sw, sw) : i] = v;
+    out[d.blk ? blk_pos(i) : i] = v;
   }
 }
 
@@ -471,7 +472,13 @@ struct DrTables {
 #ifdef __HIP_DEVICE_COMPILE__
 __device__ __forceinline__ uint2 lds_u2(uint32_t a) { return *(const __attribute__((address_space(3))) uint2*)(size_t)a; }
 __device__ __forceinline__ uint32_t lds_u32(uint32_t a) { return *(const __attribute__((address_space(3))) uint32_t*)(size_t)a; }
+__device__ __forceinline__ void lds_st32(uint32_t a, uint32_t v) { *(__attribute__((address_space(3))) uint32_t*)(size_t)a = v; }
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(size_t)(const __attribute__((address_space(3))) unsigned char*)p;
+}
 #else
+__device__ uint32_t lds_addr(const void*);
+__device__ void lds_st32(uint32_t, uint32_t);
 __device__ uint2 lds_u2(uint32_t);
 __device__ uint32_t lds_u32(uint32_t);
 #endif
@@ -552,10 +559,9 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams) {
   }
   __syncthreads();
   uint16_t* out = j.dsym + d.out_off;
-  const uint32_t sw = skew_w(j, sid, d.n);
   // generic decode of symbols [s0, s1) from state x (payload word wi of the stage, or the file)
   auto run = [&](uint64_t x, uint32_t wi, uint32_t s0, uint32_t s1, uint64_t* xe) -> bool {
-    OutCursor oc(out, sw, s0);
+    OutCursor oc(out, d.blk, s0);
     const uint64_t wend = (uint64_t)d.words;
     for (uint32_t i = s0; i < s1; i++) {
       const uint32_t slot = (uint32_t)x & mask;
@@ -644,7 +650,10 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams) {
       // slot s at DR_FIXED + tid*4 + s*1024
       const uint32_t bmask = (mask >> 2) & ~7u, t4 = (uint32_t)tid * 4;
       uint32_t xh = (uint32_t)(x >> 32), xl = (uint32_t)x;
-      uint4* o4 = (uint4*)(out + s0);
+      // this thread's row r = sg (256-wide tile): flat, or blocked (blk_pos) in 16-B blocks
+      uint4* o4 = d.blk ? (uint4*)(out + (sg >> 6) * BLK_BAND) + (sg & 63) + ((((sg & 63) + 7) >> 3) * 64)
+                        : (uint4*)(out + s0);
+      const uint32_t ostride = d.blk ? 64u : 1u;
       for (uint32_t g4 = 0; g4 < DSEG / 64; g4++) {
         uint32_t pk[32];                                     // 64 symbols: one whole 128-B line
 #pragma unroll
@@ -670,7 +679,7 @@ __global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams) {
         // the lane's whole 128-B line at once: 32-B pieces from 64 lanes 512 B apart left
         // partial lines for the memory side (WRITE_SIZE 1.6x the residual bytes)
 #pragma unroll
-        for (int e = 0; e < 8; e++) o4[8 * g4 + e] = make_uint4(pk[4 * e], pk[4 * e + 1], pk[4 * e + 2], pk[4 * e + 3]);
+        for (int e = 0; e < 8; e++) o4[(8 * g4 + e) * ostride] = make_uint4(pk[4 * e], pk[4 * e + 1], pk[4 * e + 2], pk[4 * e + 3]);
       }
       if (xh != (uint32_t)(want >> 32) || xl != (uint32_t)want || wi > d.words) bad = true;
       continue;
@@ -775,7 +784,7 @@ __device__ bool lane_decode(const DecJob& j, const DecStream& d, const uint32_t*
       if (wi > nw) s_bad = 1;
     }
     __syncthreads();
-    if (g0 + lane < d.n) out[g0 + lane] = ob[lane];
+    if (g0 + lane < d.n) out[d.blk ? blk_pos(g0 + lane) : g0 + lane] = ob[lane];
   }
   __syncthreads();
   return lane != 0 || (!s_bad && x == (1ull << 31));
@@ -873,10 +882,20 @@ __device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
   return max(min(a, b), min(max(a, b), c));
 }
 
-#define UP_P 8   // steps per residual group (one 16-B chunk pair per lane and plane)
+#define UP_P 8   // steps per residual group (one 16-B residual piece per lane and plane)
+// LDS row of the output column ring: two halves of 64 columns x 3 B, each followed by a 4-byte pad
+// (a pixel's dword store spills one byte past its slot: into the next column of its own half or
+// into the pad, never into the other half, which may still wait for its flush), then a dummy
+// slot for stores outside the tile; 99 dwords (odd: rows in different banks)
+#define ORING_PITCH 396
+#define OR_DUMMY 392
+__device__ __forceinline__ uint32_t oring_col(uint32_t c) { return (c & 127u) * 3u + ((c >> 4) & 4u); }
+// row above a band (k_dunpred_fast): entry x + LAST_OFF of lastG / lastRB holds column x
+#define LAST_OFF 8
+#define LAST_PAD 16
+#define LAST_N(tw) ((((size_t)(tw)) + LAST_PAD + 7) & ~(size_t)7)   // entries of lastRB (16-B multiple)
 
-// LDS row pitch (bytes) of the output column ring: 128 columns of RGB, odd dword count
-#define ORING_PITCH 388
+typedef uint32_t u4h __attribute__((ext_vector_type(4), aligned(2)));
 
 // 16-bit elements off .. off+7 of the 16 in w[0..7] (off lane-constant, 0..7): a 4-way select
 // of the word pairs, then a funnel shift by a half word
@@ -896,44 +915,65 @@ __device__ __forceinline__ void win8(const uint32_t* w, uint32_t off, uint32_t* 
 // Wavefront MED inverse (prediction.hpp:26-41 inverted on every row, Q9 fixed) of the three
 // planes of one tile + inverse subtract-green (channel.hpp:73-79), one wave per tile.
 // Lane r owns row 64b + r of band b and decodes x = st - r at step st; T and TL come from lane
-// r-1 through DPP (its values at steps st-1 and st-2), row -1 of a band from LDS.  The three
-// planes are independent chains interleaved in one instruction stream.  Residual planes are
-// flat (raster order): every UP_P steps a lane loads the two aligned 16-B chunks holding its
-// next UP_P residuals per plane (issued one group ahead) and funnel-shifts them into place.
-// RGB goes to a 128-column LDS ring; each 64-column chunk leaves as coalesced row segments once
-// all 64 rows have passed it.
-__global__ __launch_bounds__(64) void k_dunpred_fast(DecJob j) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  if (dec_abort(j)) return;
-  const int t = blockIdx.x;
-  const DecTile ti = j.tiles[t];
-  if (ti.err || !unpred_fast(j, t, ti)) return;
+// r-1 through DPP (its values at steps st-1 and st-2); lane 0 takes T from the row above the band
+// (LDS, read 8 columns at a time one group ahead by every lane at one broadcast address, so no
+// step branches on the lane).  Before its first column a lane holds the edge value (128, or
+// 256 | 256 << 16 for R'/B'), which makes L and TL right at x = 0 without selects.  The three
+// planes are independent chains interleaved in one instruction stream; R' and B' (9-bit planes)
+// travel as one packed pair R' | B' << 16 (the MED's uint16 gradient wrap, Q8, is the packed
+// 16-bit wrap).  Residuals are read one window of 32 steps ahead: BLK (256-wide tiles, blk_pos)
+// five 16-B blocks per plane, each load one contiguous 1 KB for the wave, the lane's 8 residuals
+// of a group cut out of two blocks at its constant offset (win8); flat planes (other widths)
+// four 16-B pieces per plane straight from the lane's 2-B aligned position (64 rows per load:
+// the texture path's line rate made these loads half the kernel's time).  RGB goes to a
+// 128-column LDS ring, one byte-aligned dword per pixel (a column outside the tile writes a
+// dummy slot); each 64-column chunk leaves as coalesced row segments once all 64 rows have
+// passed it.  (Storing each lane's 16-pixel window straight to its row as three 16-B pieces
+// needs no ring but scatters every store over 64 rows: 1.5x slower.)  The band's last row goes to
+// lastG / lastRB once per group from the lane that owns it.
+template <bool BLK>
+__device__ __forceinline__ void dunpred_fast_tile(const DecJob& j, const DecTile& ti, const uint16_t* plG,
+                                                  unsigned char* lds) {
   uint8_t* ring = lds;                                        // [64][ORING_PITCH]
-  uint32_t* lastRB = (uint32_t*)(lds + 64 * ORING_PITCH);     // R' | B' << 16 of the band's last row
-  uint16_t* lastG = (uint16_t*)(lastRB + j.tw);
+  uint32_t* lastRB = (uint32_t*)(lds + 64 * ORING_PITCH);     // R' | B' << 16 of the row above the band
+  uint16_t* lastG = (uint16_t*)(lastRB + LAST_N(j.tw));
   const int lane = threadIdx.x;
   const int w = ti.w, h = ti.h, nst = w + 63;
-  const uint16_t* plG = j.dsym + (size_t)(t * 3) * j.plane_cap;
   const size_t pitch = (size_t)j.W * 3;
   uint8_t* obase = j.rgb + ((size_t)ti.y0 * j.W + ti.x0) * 3;
+  const uint16_t* plR = plG + j.plane_cap;
+  const uint16_t* plB = plG + 2 * (size_t)j.plane_cap;
+  const uint32_t KG = 128u, KRB = 0x01000100u;
   const bool dw_ok = ((pitch | ((size_t)ti.x0 * 3) | (size_t)j.rgb) & 3) == 0;
-  uint8_t* orow = ring + (size_t)lane * ORING_PITCH;
+  const uint32_t orow = lds_addr(ring) + (uint32_t)lane * ORING_PITCH;   // LDS byte address
+  int fr_row[3], fr_lds[3];
+  size_t fr_glb[3];
+#pragma unroll
+  for (int q = 0; q < 3; q++) {
+    const int e = lane + 64 * q, rr = e / 48, d = e - 48 * rr;
+    fr_row[q] = rr; fr_lds[q] = rr * ORING_PITCH + 4 * d; fr_glb[q] = (size_t)rr * pitch + 4 * d;
+  }
+  for (int i = lane; i < w + LAST_PAD; i += 64) { lastRB[i] = KRB; lastG[i] = (uint16_t)KG; }   // row -1
+  __syncthreads();
   for (int r0 = 0; r0 < h; r0 += 64) {
     const int y = r0 + lane;
     const int last = min(63, h - r0 - 1);
     const bool rowok = y < h;
-    const long F = (long)min(y, h - 1) * w - lane;            // flat index of this lane at step 0
-    const uint32_t off = (uint32_t)(F & 7);
-    const long F0 = F - off;                                   // 16-B aligned
+    long F = (long)min(y, h - 1) * w - lane;                  // flat index of this lane at step 0
+    if (F < 0) F = 0;                                          // rows past the tile: any residuals
     // flush chunk k (columns 64k .. 64k+63, all rows of the band) from the ring
+    int flushed = 0;
     auto flush = [&](int k) {
       const int c0 = 64 * k, nc = min(64, w - c0), rows = last + 1;
-      const uint8_t* src0 = ring + (c0 & 127) * 3;
+      const uint8_t* src0 = ring + oring_col((uint32_t)c0);
       uint8_t* dst0 = obase + (size_t)r0 * pitch + (size_t)c0 * 3;
       if (dw_ok && nc == 64) {
-        for (int e = lane; e < rows * 48; e += 64) {
-          const int rr = e / 48, d = e - rr * 48;
-          ((uint32_t*)(dst0 + (size_t)rr * pitch))[d] = ((const uint32_t*)(src0 + (size_t)rr * ORING_PITCH))[d];
+        // 4 rows (192 dwords) per pass: lane l moves dwords l, l+64, l+128 of the block
+        for (int rb = 0; rb < rows; rb += 4) {
+#pragma unroll
+          for (int q = 0; q < 3; q++)
+            if (rb + fr_row[q] < rows)
+              *(uint32_t*)(dst0 + (size_t)rb * pitch + fr_glb[q]) = *(const uint32_t*)(src0 + rb * ORING_PITCH + fr_lds[q]);
         }
       } else {
         const int nb = nc * 3;
@@ -943,80 +983,134 @@ __global__ __launch_bounds__(64) void k_dunpred_fast(DecJob j) {
         }
       }
     };
-    auto chunk = [&](const uint16_t* pl, long f) -> uint4 {
-      return *(const uint4*)(pl + (f < 0 ? 0 : f));
+    auto res = [&](const uint16_t* pl, int s0) -> u4h { return *(const u4h*)(pl + F + s0); };
+    // the row above for lane 0: columns s0 .. s0+7 (past the row: not needed, not read)
+    auto above = [&](int s0, uint4& ag0, uint4& ag1, uint4& arb0, uint4& arb1) {
+      if (s0 < w) {
+        const uint4* g = (const uint4*)(lastG + s0 + LAST_OFF);
+        const uint4* rb = (const uint4*)(lastRB + s0 + LAST_OFF);
+        const uint4 gg = g[0];
+        ag0 = make_uint4(gg.x & 0xffffu, gg.x >> 16, gg.y & 0xffffu, gg.y >> 16);
+        ag1 = make_uint4(gg.z & 0xffffu, gg.z >> 16, gg.w & 0xffffu, gg.w >> 16);
+        arb0 = rb[0]; arb1 = rb[1];
+      }
     };
-    // residual chunks: R[k] holds the aligned 16-B chunk A_g = F0 + 8g of each plane; group g
-    // uses A_g and A_{g+1} and issues A_{g+2}, so each chunk is loaded once, one group ahead
-    // (three buffers rotate through an unroll by three: no pending load is ever copied)
-    const uint16_t* plR = plG + j.plane_cap;
-    const uint16_t* plB = plG + 2 * (size_t)j.plane_cap;
-    uint4 g0 = chunk(plG, F0), r0c = chunk(plR, F0), b0c = chunk(plB, F0);
-    uint4 g1 = chunk(plG, F0 + 8), r1c = chunk(plR, F0 + 8), b1c = chunk(plB, F0 + 8);
-    uint4 g2, r2c, b2c;
-    // R' and B' (9-bit planes) travel as one packed pair R' | B' << 16: the MED's uint16
-    // gradient wrap (Q8) is the packed 16-bit wrap, so both planes cost one set of packed ops
-    uint32_t cG = 0, cRB = 0;              // this lane's values at the previous step (L)
-    uint32_t pG = 128, pRB = 0x01000100u;  // T of the previous step (TL)
-    int flushed = 0;
-    auto group = [&](int s0, const uint4& ga, const uint4& gb, uint4& gn, const uint4& ra, const uint4& rb, uint4& rn,
-                     const uint4& ba, const uint4& bb, uint4& bn) {
-      asm volatile("" ::"v"(gb.x), "v"(gb.y), "v"(gb.z), "v"(gb.w), "v"(rb.x), "v"(rb.y), "v"(rb.z), "v"(rb.w));
-      asm volatile("" ::"v"(bb.x), "v"(bb.y), "v"(bb.z), "v"(bb.w));
-      uint32_t qG[4], qR[4], qB[4];
-      {
-        const uint32_t wg[8] = {ga.x, ga.y, ga.z, ga.w, gb.x, gb.y, gb.z, gb.w};
-        const uint32_t wr[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
-        const uint32_t wb[8] = {ba.x, ba.y, ba.z, ba.w, bb.x, bb.y, bb.z, bb.w};
-        win8(wg, off, qG); win8(wr, off, qR); win8(wb, off, qB);
-      }
-      {
-        const long fn = F0 + s0 + 2 * UP_P;
-        gn = chunk(plG, fn); rn = chunk(plR, fn); bn = chunk(plB, fn);
-      }
+    uint32_t cG = KG, cRB = KRB;           // this lane's values at the previous step (L)
+    uint32_t pG = KG, pRB = KRB;           // T of the previous step (TL)
+    // one group: steps s0 .. s0+7 with residuals (g, r, b); issues the residuals of group s0 + 24
+    // into (gn, rn, bn) and the row above of group s0 + 8
+    auto group = [&](int s0, const uint32_t (&qG)[4], const uint32_t (&qR)[4], const uint32_t (&qB)[4],
+                     const uint4& ag0, const uint4& ag1, const uint4& arb0, const uint4& arb1,
+                     uint4& ng0, uint4& ng1, uint4& nrb0, uint4& nrb1) {
+      above(s0 + UP_P, ng0, ng1, nrb0, nrb1);
+      const uint32_t oGs[8] = {ag0.x, ag0.y, ag0.z, ag0.w, ag1.x, ag1.y, ag1.z, ag1.w};
+      const uint32_t oRBs[8] = {arb0.x, arb0.y, arb0.z, arb0.w, arb1.x, arb1.y, arb1.z, arb1.w};
+      uint32_t keepG[UP_P], keepRB[UP_P];
 #pragma unroll
       for (int u = 0; u < UP_P; u++) {
-        const int st = s0 + u;
-        const int x = st - lane;
-        const uint32_t rG = (qG[u >> 1] >> ((u & 1) * 16)) & 0xffffu;
+        const int x = s0 + u - lane;
+        // G residual: the high half of the word is cut by the final & 255
+        const uint32_t rG = (u & 1) ? qG[u >> 1] >> 16 : qG[u >> 1];
         // R' residual in the low half, B' in the high half: one byte permute
         const uint32_t rRB = __builtin_amdgcn_perm(qB[u >> 1], qR[u >> 1], (u & 1) ? 0x07060302u : 0x05040100u);
-        uint32_t oG = 128, oRB = 0x01000100u;          // lane 0: row above the band
-        if (r0 > 0 && lane == 0 && x < w) { oG = lastG[x]; oRB = lastRB[x]; }
-        const uint32_t TG = wave_shr1(cG, oG), TRB = wave_shr1(cRB, oRB);
-        const bool xz = x <= 0;
-        const uint32_t LG = xz ? 128u : cG, LRB = xz ? 0x01000100u : cRB;
-        const uint32_t AG = xz ? 128u : pG, ARB = xz ? 0x01000100u : pRB;
-        const uint32_t vG = (rG + med3u(TG, LG, (TG + LG - AG) & 0xffffu) + 128u) & 255u;
-        const dus2 t2 = as_d2(TRB), l2 = as_d2(LRB);
-        const dus2 g2 = t2 + l2 - as_d2(ARB);
+        const uint32_t TG = wave_shr1(cG, oGs[u]), TRB = wave_shr1(cRB, oRBs[u]);
+        const uint32_t vG = (rG + med3u(TG, cG, (TG + cG - pG) & 0xffffu) + 128u) & 255u;
+        const dus2 t2 = as_d2(TRB), l2 = as_d2(cRB);
+        const dus2 g2 = t2 + l2 - as_d2(pRB);
         const dus2 m2 = __builtin_elementwise_max(__builtin_elementwise_min(t2, l2),
                                                   __builtin_elementwise_min(__builtin_elementwise_max(t2, l2), g2));
         const uint32_t vRB = as_u32d(as_d2(rRB) + m2 + (dus2)(256)) & 0x01ff01ffu;
+        const bool pre = x < 0;
         pG = TG; pRB = TRB;
-        cG = vG; cRB = vRB;
-        if (rowok && x >= 0 && x < w) {
-          uint8_t* o = orow + (x & 127) * 3;
-          const uint32_t rb = vRB + vG * 0x10001u;    // R' + G | (B' + G) << 16, no carry across
-          o[0] = (uint8_t)rb; o[1] = (uint8_t)vG; o[2] = (uint8_t)(rb >> 16);
-          if (lane == last) { lastG[x] = (uint16_t)vG; lastRB[x] = vRB; }
-        }
+        cG = pre ? KG : vG;
+        cRB = pre ? KRB : vRB;
+        keepG[u] = cG; keepRB[u] = cRB;
+        const uint32_t rb = vRB + vG * 0x10001u;      // R' + G | (B' + G) << 16, no carry across
+        // R, G, B, 0 as one dword at the column's slot of the lane's ring row
+        const uint32_t px = __builtin_amdgcn_perm(vG, rb, 0x0c020400u);
+        const bool ok = rowok && (uint32_t)x < (uint32_t)w;
+        uint32_t col = oring_col((uint32_t)x);
+        asm volatile("" : "+v"(col));                  // computed by every lane: a select, not a branch
+        lds_st32(orow + (ok ? col : (uint32_t)OR_DUMMY), px);
+      }
+      // the band's last row (its lane's values, edge values before column 0) for the next band
+      const int x0 = s0 - lane;
+      if (lane == last && x0 > -UP_P && x0 < w) {
+#pragma unroll
+        for (int u = 0; u < UP_P; u++) { lastG[x0 + u + LAST_OFF] = (uint16_t)keepG[u]; lastRB[x0 + u + LAST_OFF] = keepRB[u]; }
       }
       // columns < s0 + UP_P - 63 are complete in every row: flush whole 64-column chunks before
       // the ring slot is reused (column 64k + 128 arrives at step 64k + 128 at the earliest)
       const int done = s0 + UP_P - 63;
       while (64 * (flushed + 1) <= done && 64 * flushed < w) { flush(flushed); flushed++; }
     };
-    for (int s0 = 0; s0 < nst; s0 += 3 * UP_P) {
-      group(s0, g0, g1, g2, r0c, r1c, r2c, b0c, b1c, b2c);
-      if (s0 + UP_P >= nst) break;
-      group(s0 + UP_P, g1, g2, g0, r1c, r2c, r0c, b1c, b2c, b0c);
-      if (s0 + 2 * UP_P >= nst) break;
-      group(s0 + 2 * UP_P, g2, g0, g1, r2c, r0c, r1c, b2c, b0c, b1c);
+    // residuals of 32 steps per buffer (64 B of each plane per lane: four 16-B loads issued back
+    // to back, so only the first misses the L1), loaded one window ahead; row-above values
+    // alternate between two sets
+    // Blocked planes: blocks s0/8 .. s0/8 + 4 of the lane's row (one contiguous 1 KB per load),
+    // group g's 8 residuals start at element off = -lane & 7 of block s0/8 + g
+    struct Win { uint4 g[5], r[5], b[5]; };
+    const size_t bandoff = (size_t)(r0 >> 6) * BLK_BAND + (size_t)lane * 8;
+    const uint32_t boff = (uint32_t)(-lane) & 7u;
+    auto load = [&](Win& W, int s0) {
+      if (BLK) {
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+          const size_t e = bandoff + (size_t)min(s0 / 8 + k, BLK_NK - 1) * 512;
+          W.g[k] = *(const uint4*)(plG + e); W.r[k] = *(const uint4*)(plR + e); W.b[k] = *(const uint4*)(plB + e);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++) { const u4h v = res(plG, s0 + k * UP_P); W.g[k] = make_uint4(v.x, v.y, v.z, v.w); }
+#pragma unroll
+        for (int k = 0; k < 4; k++) { const u4h v = res(plR, s0 + k * UP_P); W.r[k] = make_uint4(v.x, v.y, v.z, v.w); }
+#pragma unroll
+        for (int k = 0; k < 4; k++) { const u4h v = res(plB, s0 + k * UP_P); W.b[k] = make_uint4(v.x, v.y, v.z, v.w); }
+      }
+    };
+    auto words = [&](const uint4* c, int gi, uint32_t (&q)[4]) {
+      if (BLK) {
+        const uint32_t w8[8] = {c[gi].x, c[gi].y, c[gi].z, c[gi].w, c[gi + 1].x, c[gi + 1].y, c[gi + 1].z, c[gi + 1].w};
+        win8(w8, boff, q);
+      } else {
+        q[0] = c[gi].x; q[1] = c[gi].y; q[2] = c[gi].z; q[3] = c[gi].w;
+      }
+    };
+    auto window = [&](int s0, const Win& W, uint4* a, uint4* c) {
+#pragma unroll
+      for (int gi = 0; gi < 4; gi++) {
+        uint32_t qG[4], qR[4], qB[4];
+        words(W.g, gi, qG); words(W.r, gi, qR); words(W.b, gi, qB);
+        if (gi & 1) group(s0 + gi * UP_P, qG, qR, qB, c[0], c[1], c[2], c[3], a[0], a[1], a[2], a[3]);
+        else group(s0 + gi * UP_P, qG, qR, qB, a[0], a[1], a[2], a[3], c[0], c[1], c[2], c[3]);
+      }
+    };
+    Win WA, WB;
+    uint4 av[4] = {}, cv[4] = {};
+    load(WA, 0);
+    above(0, av[0], av[1], av[2], av[3]);
+    for (int s0 = 0; s0 < nst; s0 += 8 * UP_P) {
+      load(WB, s0 + 4 * UP_P);
+      window(s0, WA, av, cv);
+      if (s0 + 4 * UP_P >= nst) break;
+      load(WA, s0 + 8 * UP_P);
+      window(s0 + 4 * UP_P, WB, av, cv);
     }
     while (64 * flushed < w) { flush(flushed); flushed++; }
     __syncthreads();
   }
+}
+
+__global__ __launch_bounds__(64) void k_dunpred_fast(DecJob j) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  if (dec_abort(j)) return;
+  const int t = blockIdx.x;
+  const DecTile ti = j.tiles[t];
+  if (ti.err || !unpred_fast(j, t, ti)) return;
+  const DecStream* st = j.streams + (size_t)t * SK_PER_TILE + 3;
+  const uint16_t* pl = j.dsym + (size_t)(t * 3) * j.plane_cap;
+  if (st[0].blk && st[1].blk && st[2].blk) dunpred_fast_tile<true>(j, ti, pl, lds);
+  else dunpred_fast_tile<false>(j, ti, pl, lds);
 }
 
 // pixels of [0, i) covered by LZ copies (matches sorted by pixel index)
@@ -1383,8 +1477,11 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   j.npix_cap = (uint32_t)(((size_t)j.tw * j.th + 63) / 64 * 64);
   j.lz_cap = (uint32_t)((j.npix_cap / 4 + j.npix_cap / 255 + 16 + 7) / 8 * 8);
   {
-    // flat planes + slack for k_dunpred_fast's chunk reads one group past the end
-    j.plane_cap = (uint32_t)(((size_t)j.npix_cap + 6 * UP_P + 64 + 63) / 64 * 64);
+    // flat planes + slack for k_dunpred_fast's residual reads three groups past a row's end
+    j.plane_cap = (uint32_t)(((size_t)j.npix_cap + 8 * UP_P + 128 + 63) / 64 * 64);
+    // 256-wide tiles: room for the blocked layout (its reads stay inside the tile's bands)
+    j.blk_ok = j.tw == 256;
+    if (j.blk_ok) j.plane_cap = std::max<uint32_t>(j.plane_cap, (uint32_t)(((size_t)j.th + 63) / 64 * BLK_BAND));
   }
   const int S = j.ntiles * SK_PER_TILE;
   DecWork& w = ctx_dec(c);
@@ -1422,7 +1519,7 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   if (!indexed) hipLaunchKernelGGL(k_dstored, dim3(S), dim3(256), 0, s, j, S);
   hipLaunchKernelGGL(k_dlz, dim3((j.ntiles + 63) / 64), dim3(64), 0, s, j);
   ctx_mark(c, s, "dlz", false);
-  hipLaunchKernelGGL(k_dunpred_fast, dim3(j.ntiles), dim3(64), (size_t)64 * ORING_PITCH + (size_t)3 * j.tw * 2, s, j);
+  hipLaunchKernelGGL(k_dunpred_fast, dim3(j.ntiles), dim3(64), (size_t)64 * ORING_PITCH + 6 * LAST_N(j.tw), s, j);
   j.lzband = (int)std::min<size_t>(64, (160 * 1024 - (size_t)j.tw * 4) / ((size_t)j.tw * 4) - 1);
   hipLaunchKernelGGL(k_dunpred_lz, dim3(std::min(j.ntiles, 256)), dim3(64), (size_t)(j.lzband + 1) * j.tw * 4, s, j);
   hipLaunchKernelGGL(k_dunpred_serial, dim3(std::min(j.ntiles, 64)), dim3(192), 0, s, j);
