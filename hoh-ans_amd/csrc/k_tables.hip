@@ -224,12 +224,25 @@ __global__ __launch_bounds__(64) void k_tables(EncodeJob j, SidMap sm) {
   const uint64_t expected_raw = ((uint64_t)pb * range + 8 - 1) / 8;
   const uint32_t cn32 = (pb - 1) / 4 + 2;
   const uint32_t cn = (uint8_t)cn32;
+  // first and last present symbols: the clamp scans below do nothing over the absent symbols at
+  // either end (size_bits stays 0, nothing is added), so they start there (the residual planes
+  // of an image have ~100+ absent symbols at each end, ~2/3 of the serial scan steps)
+  uint32_t first = range, lastnz = 0;
+  for (uint32_t base = 0; base < range; base += 64) {
+    const uint32_t i0 = base + lane;
+    const uint64_t bm = __ballot(i0 < range && fr[i0] != 0);
+    if (bm) {
+      if (first == range) first = base + (uint32_t)__builtin_ctzll(bm);
+      lastnz = base + 63 - (uint32_t)__builtin_clzll(bm);
+    }
+  }
+  if (first == range) { first = 0; lastnz = range - 1; }
   if (lane == 0) {
     uint64_t exp_cl = (uint64_t)(uint32_t)((uint32_t)(2 * ((int)maxbits - 1)) * cn32);
     exp_cl += (uint64_t)(uint32_t)(pb * 2);
     uint16_t lower[16], upper[16];
     for (int i = 0; i < 16; i++) { lower[i] = 0; upper[i] = 0; }
-    uint64_t size_bits = 0, climb = 0, lci = 0;
+    uint64_t size_bits = 0, climb = first, lci = 0;
     for (; climb < range; climb++) {
       while ((uint64_t)fr[climb] >= (uint64_t)(1u << size_bits)) {
         uint64_t idx;
@@ -243,7 +256,7 @@ __global__ __launch_bounds__(64) void k_tables(EncodeJob j, SidMap sm) {
     }
     while (lci < cn && lci < 16) lower[lci++] = (uint16_t)(range - 1);
     size_bits = 0;
-    uint64_t climb2 = range - 1, uci = 0;
+    uint64_t climb2 = lastnz, uci = 0;
     for (;; climb2--) {
       while ((uint64_t)fr[climb2] >= (uint64_t)(1u << size_bits)) {
         uint64_t idx;
