@@ -22,7 +22,11 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
   return v;
 }
 
+#define LZR 2048          // pixel ring of k_lz (positions p & (LZR - 1))
+#define LZR_CHUNK 1024
+
 __global__ __launch_bounds__(64) void k_lz(EncodeJob j) {
+  __shared__ uint32_t ring[LZR];
   const int t = blockIdx.x, lane = threadIdx.x;
   TileInfo ti = j.tiles[t];
   const uint32_t npix = (uint32_t)ti.w * ti.h;
@@ -39,6 +43,21 @@ __global__ __launch_bounds__(64) void k_lz(EncodeJob j) {
   const uint32_t thr = 4 + bonus;
   uint32_t nm = 0, pos = 0;
   bool overflow = false;
+  // The run lengths compare pixels q + k with q + k - b (b <= 64, k < 259): they come from an LDS
+  // ring holding tile positions [wend - LZR, wend), filled 1024 positions at a time as the scan
+  // moves (each pixel read from memory once per tile; natural tiles hold thousands of copies and
+  // the per-step global reads made this kernel ~16 ms per image)
+  uint32_t wend = 0;
+  auto fill_to = [&](uint32_t need) {
+    while (wend < need) {
+      for (uint32_t k = lane; k < LZR_CHUNK; k += 64) {
+        const uint32_t p = wend + k;
+        ring[p & (LZR - 1)] = p < npix ? img_px(j, ti.x0, ti.y0, ti.w, p) : 0xff000000u;
+      }
+      wend += LZR_CHUNK;
+    }
+    __syncthreads();
+  };
   if (ti.ncand) {
     while (pos < npix) {
       // next candidate q >= pos
@@ -55,10 +74,11 @@ __global__ __launch_bounds__(64) void k_lz(EncodeJob j) {
         }
       }
       if (q == 0xffffffffu) break;
+      fill_to(q + 260);
       const uint32_t b = lane + 1;
       uint32_t L = 0;
       if (b <= q) {
-        while (q + L < npix && L < 259 && img_px(j, ti.x0, ti.y0, ti.w, q + L) == img_px(j, ti.x0, ti.y0, ti.w, q + L - b)) L++;
+        while (q + L < npix && L < 259 && ring[(q + L) & (LZR - 1)] == ring[(q + L - b) & (LZR - 1)]) L++;
       }
       uint64_t key = ((uint64_t)L << 8) | (255u - b);
       key = wave_max_u64(key);
@@ -159,8 +179,9 @@ __device__ __forceinline__ void nuke_tile(const EncodeJob& j, int t, uint32_t* n
 
 // A small grid strides over the tiles (most have no match): a launch over every tile dispatches
 // ~1000 idle workgroups, which waits for free CUs when other images are in flight.
+#define NK_HIST (2 * HOH_NPLANE_S * 512)
 __global__ __launch_bounds__(256) void k_nuke(EncodeJob j) {
-  extern __shared__ uint32_t nk_bits[];                  // npix_cap / 32 words
+  extern __shared__ uint32_t nk_bits[];                  // npix_cap / 32 words, then NK_HIST counts
   __shared__ uint32_t wsum[4];
   for (int t = blockIdx.x; t < j.ntiles; t += gridDim.x) nuke_tile(j, t, nk_bits, wsum);
 }
@@ -172,11 +193,14 @@ __device__ __forceinline__ void nuke_tile(const EncodeJob& j, int t, uint32_t* n
   if (nm == 0 || (ti.flags & TF_OVERFLOW) || nm > j.lz_cap) return;
   const uint32_t npix = (uint32_t)ti.w * ti.h, nwords = (npix + 31) / 32;
   const uint32_t* mt = j.matches + (size_t)t * 3 * (j.lz_cap + 1);
+  uint32_t* nh = nk_bits + j.npix_cap / 32 + 1;          // removed counts, [slot][512]
   for (uint32_t i = tid; i < nwords; i += 256) nk_bits[i] = 0;
+  for (uint32_t i = tid; i < NK_HIST; i += 256) nh[i] = 0;
   __syncthreads();
-  for (uint32_t m = 0; m < nm; m++) {
+  // one thread per match (matches are disjoint): natural tiles hold thousands of short copies
+  for (uint32_t m = tid; m < nm; m += 256) {
     const uint32_t a = mt[3 * m], e = a + mt[3 * m + 1];
-    for (uint32_t p = a + tid; p < e; p += 256) atomicOr(&nk_bits[p >> 5], 1u << (p & 31));
+    for (uint32_t p = a; p < e; p++) atomicOr(&nk_bits[p >> 5], 1u << (p & 31));
   }
   __syncthreads();
   const bool grey = ti.flags & TF_GREY, pal = !grey && (ti.flags & TF_PALETTE_CAND);
@@ -209,9 +233,9 @@ __device__ __forceinline__ void nuke_tile(const EncodeJob& j, int t, uint32_t* n
 #pragma unroll
     for (int k = 0; k < 2 * HOH_NPLANE_S; k++) v[k] = (k < np && valid) ? r[k][p] : 0;
     const bool nuked = valid && ((nk_bits[p >> 5] >> (p & 31)) & 1);
-    if (nuked) {
+    if (nuked) {                                        // counted in LDS, applied once below
 #pragma unroll
-      for (int k = 0; k < 2 * HOH_NPLANE_S; k++) if (k < np) atomicSub(&hk[k][v[k]], 1u);
+      for (int k = 0; k < 2 * HOH_NPLANE_S; k++) if (k < np) atomicAdd(&nh[k * 512 + v[k]], 1u);
     }
     const bool keep = valid && !nuked;
     const uint64_t bal = __ballot(keep);
@@ -230,6 +254,12 @@ __device__ __forceinline__ void nuke_tile(const EncodeJob& j, int t, uint32_t* n
     outc += tot;
   }
   __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2 * HOH_NPLANE_S; k++)
+    if (k < np)
+      for (uint32_t i = tid; i < 512; i += 256)
+        if (nh[k * 512 + i]) hk[k][i] -= nh[k * 512 + i];    // this tile's histograms: one writer
+  __syncthreads();
 }
 
 void launch_lz(const EncodeJob& j, hipStream_t s) {
@@ -237,5 +267,6 @@ void launch_lz(const EncodeJob& j, hipStream_t s) {
 }
 
 void launch_nuke(const EncodeJob& j, hipStream_t s) {
-  hipLaunchKernelGGL(k_nuke, dim3(std::min(j.ntiles, 128)), dim3(256), (size_t)(j.npix_cap / 32 + 1) * 4, s, j);
+  // one workgroup per tile (natural images: most tiles have copies); tiles without copies leave
+  hipLaunchKernelGGL(k_nuke, dim3(j.ntiles), dim3(256), (size_t)(j.npix_cap / 32 + 1 + NK_HIST) * 4, s, j);
 }
