@@ -41,6 +41,7 @@ struct DecJob {
   uint32_t cum_stride;          // entries per stream in cum (>= range + 1)
   uint32_t* matches;            // [tile][lz_cap+1][4]: pixel index, length, back, nuked before
   int lzband;                   // rows per band of k_dunpred_lz (LDS-bound)
+  int lzstage;                  // k_dunpred_lz stages each band's residuals in LDS
   uint32_t* lzt;                // tiles with LZ copies (w >= 64), appended by k_dlz; count in gerr[2]
   uint8_t* rgb;                 // output image
   uint32_t* gerr;
@@ -1144,24 +1145,31 @@ __device__ __forceinline__ uint32_t unpred_px(uint32_t T, uint32_t L, uint32_t T
 // copied pixels) are staged in LDS first.  Needs w >= 64 (copies reach at most one row up).
 // A small persistent grid walks the list of LZ tiles k_dlz built (a launch over every tile
 // would dispatch ~1000 idle workgroups that each need the 66 KB band).
-__device__ __forceinline__ void dunpred_lz_tile(const DecJob& j, int t, uint32_t* lz_lds);
+__device__ __forceinline__ void dunpred_lz_tile(const DecJob& j, int t, uint32_t* lz_lds, int BR);
 
-__global__ __launch_bounds__(64) void k_dunpred_lz(DecJob j) {
+// Launched twice per decode (the LZ tile count is only known on the device): `many` = 0 runs
+// when at most LZ_FEW tiles have copies (LZ_FEW workers, 64-row bands: the fewest steps per
+// tile), `many` = 1 otherwise (a worker per tile, 32-row bands in 33 KB: four per CU, so the
+// tiles of a natural image, many of them nearly serial, run at once).
+#define LZ_FEW 256
+__global__ __launch_bounds__(64) void k_dunpred_lz(DecJob j, int br, int many) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lz_lds[];
   if (dec_abort(j)) return;
   const uint32_t cnt = *(volatile const uint32_t*)(j.gerr + 2);
+  if ((cnt > LZ_FEW) != (many != 0)) return;
   for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
-    dunpred_lz_tile(j, (int)j.lzt[i], lz_lds);
+    dunpred_lz_tile(j, (int)j.lzt[i], lz_lds, br);
     __syncthreads();
   }
 }
 
-__device__ __forceinline__ void dunpred_lz_tile(const DecJob& j, int t, uint32_t* lz_lds) {
+__device__ __forceinline__ void dunpred_lz_tile(const DecJob& j, int t, uint32_t* lz_lds, int BR) {
   const DecTile ti = j.tiles[t];
   if (ti.err || unpred_fast(j, t, ti) || ti.w < 64) return;
   const int lane = threadIdx.x;
-  const int w = ti.w, h = ti.h, BR = j.lzband;
+  const int w = ti.w, h = ti.h;
   uint32_t* band = lz_lds;                                   // (BR+1) rows x w
+  uint32_t* stage = band + (size_t)(BR + 1) * w;             // BR rows x w packed residuals (lzstage)
   const DecStream* st = j.streams + (size_t)t * SK_PER_TILE + 3;
   const uint32_t* mt = j.matches + (size_t)t * 4 * (j.lz_cap + 1);
   const uint32_t nm = ti.nmatch, npix = (uint32_t)w * h;
@@ -1180,6 +1188,12 @@ __device__ __forceinline__ void dunpred_lz_tile(const DecJob& j, int t, uint32_t
     const uint32_t kb0 = (uint32_t)r0 * w - nuked_before(mt, nm, (uint32_t)r0 * w);
     const uint32_t kb1 = (uint32_t)r1 * w - nuked_before(mt, nm, (uint32_t)r1 * w);
     __syncthreads();
+    // the band's residuals (one contiguous range of the compacted planes) packed into LDS with
+    // coalesced loads: the wavefront then waits on LDS, not on a global load per pixel
+    if (j.lzstage)
+      for (uint32_t i = (uint32_t)lane; i < kb1 - kb0; i += 64)
+        stage[i] = resG[kb0 + i] | ((uint32_t)resR[kb0 + i] << 8) | ((uint32_t)resB[kb0 + i] << 17);
+    __syncthreads();
     const int y = r0 + lane;
     const bool act = lane < BR && y < h;
     uint32_t prog = act ? 0u : (uint32_t)w;
@@ -1192,11 +1206,18 @@ __device__ __forceinline__ void dunpred_lz_tile(const DecJob& j, int t, uint32_t
     }
     uint32_t midx = 0xffffffffu, mlen = 0, mback = 0;
     if (m < nm) { midx = mt[4 * m]; mlen = mt[4 * m + 1]; mback = mt[4 * m + 2]; }
+    // the next match, loaded one match ahead (its latency hides behind the current one)
+    uint32_t nidx = 0xffffffffu, nlen = 0, nback = 0;
+    if (m + 1 < nm) { nidx = mt[4 * m + 4]; nlen = mt[4 * m + 5]; nback = mt[4 * m + 6]; }
     uint32_t left = PK_HALF;
     const uint32_t rowbase = (uint32_t)y * w;
     // the lane's next residual (index rowbase - nuked-before-row), loaded one use ahead so the
     // dependent loop never waits on memory for it
     auto ldres = [&](uint32_t k) -> uint32_t {
+      if (j.lzstage) {
+        if (kb1 == kb0) return 0u;
+        return stage[min(max(k, kb0), kb1 - 1) - kb0];
+      }
       const uint32_t kk = k < kb1 ? k : (kb1 ? kb1 - 1 : 0);
       return resG[kk] | ((uint32_t)resR[kk] << 8) | ((uint32_t)resB[kk] << 17);
     };
@@ -1210,9 +1231,15 @@ __device__ __forceinline__ void dunpred_lz_tile(const DecJob& j, int t, uint32_t
         const uint32_t x = prog, i = rowbase + x;
         if (m < nm && midx + mlen <= i) {
           m++;
-          while (m < nm && mt[4 * m] + mt[4 * m + 1] <= i) m++;
-          midx = 0xffffffffu;
-          if (m < nm) { midx = mt[4 * m]; mlen = mt[4 * m + 1]; mback = mt[4 * m + 2]; }
+          if (m < nm && nidx + nlen > i) {               // the usual case: the prefetched match
+            midx = nidx; mlen = nlen; mback = nback;
+          } else {
+            while (m < nm && mt[4 * m] + mt[4 * m + 1] <= i) m++;
+            midx = 0xffffffffu;
+            if (m < nm) { midx = mt[4 * m]; mlen = mt[4 * m + 1]; mback = mt[4 * m + 2]; }
+          }
+          nidx = 0xffffffffu;
+          if (m + 1 < nm) { nidx = mt[4 * m + 4]; nlen = mt[4 * m + 5]; nback = mt[4 * m + 6]; }
         }
         const bool copy = m < nm && midx <= i;
         bool ready = above > x;
@@ -1520,8 +1547,20 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   hipLaunchKernelGGL(k_dlz, dim3((j.ntiles + 63) / 64), dim3(64), 0, s, j);
   ctx_mark(c, s, "dlz", false);
   hipLaunchKernelGGL(k_dunpred_fast, dim3(j.ntiles), dim3(64), (size_t)64 * ORING_PITCH + 6 * LAST_N(j.tw), s, j);
-  j.lzband = (int)std::min<size_t>(64, (160 * 1024 - (size_t)j.tw * 4) / ((size_t)j.tw * 4) - 1);
-  hipLaunchKernelGGL(k_dunpred_lz, dim3(std::min(j.ntiles, 256)), dim3(64), (size_t)(j.lzband + 1) * j.tw * 4, s, j);
+  {
+    // On natural images most tiles hold copies, and a copy at a row's start that reads the end of
+    // the row above turns the wavefront into raster order (such a tile is nearly serial), so the
+    // tiles themselves are the parallelism; with few LZ tiles, 64-row bands take fewer steps.
+    const size_t rowb = (size_t)j.tw * 4, lds = 160 * 1024;
+    j.lzstage = 0;
+    const int br_few = (int)std::min<size_t>(64, lds / rowb - 2);
+    const int br_many = (int)std::min<size_t>(32, lds / rowb - 2);
+    j.lzband = br_few;
+    hipLaunchKernelGGL(k_dunpred_lz, dim3(std::min(j.ntiles, LZ_FEW)), dim3(64), (size_t)(br_few + 1) * rowb, s, j,
+                       br_few, 0);
+    if (j.ntiles > LZ_FEW)
+      hipLaunchKernelGGL(k_dunpred_lz, dim3(j.ntiles), dim3(64), (size_t)(br_many + 1) * rowb, s, j, br_many, 1);
+  }
   hipLaunchKernelGGL(k_dunpred_serial, dim3(std::min(j.ntiles, 64)), dim3(192), 0, s, j);
   ctx_mark(c, s, "dunpred", false);
   if (hipGetLastError() != hipSuccess) return 3;
