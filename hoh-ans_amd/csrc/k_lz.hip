@@ -23,7 +23,6 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 }
 
 #define LZR 2048          // pixel ring of k_lz (positions p & (LZR - 1))
-#define LZR_CHUNK 1024
 
 __global__ __launch_bounds__(64) void k_lz(EncodeJob j) {
   __shared__ uint32_t ring[LZR];
@@ -44,17 +43,17 @@ __global__ __launch_bounds__(64) void k_lz(EncodeJob j) {
   uint32_t nm = 0, pos = 0;
   bool overflow = false;
   // The run lengths compare pixels q + k with q + k - b (b <= 64, k < 259): they come from an LDS
-  // ring holding tile positions [wend - LZR, wend), filled 1024 positions at a time as the scan
-  // moves (each pixel read from memory once per tile; natural tiles hold thousands of copies and
-  // the per-step global reads made this kernel ~16 ms per image)
+  // ring holding the tile positions [wlo, wend) (wend - wlo <= LZR), loaded 64 at a time as the
+  // scan moves and only around candidates (each pixel read from memory at most once per tile;
+  // natural tiles hold thousands of copies and per-step global reads made this kernel ~16 ms
+  // per image)
   uint32_t wend = 0;
-  auto fill_to = [&](uint32_t need) {
+  auto fill_to = [&](uint32_t lo, uint32_t need) {
+    if (lo > wend) wend = lo & ~63u;                  // nothing needed in between
     while (wend < need) {
-      for (uint32_t k = lane; k < LZR_CHUNK; k += 64) {
-        const uint32_t p = wend + k;
-        ring[p & (LZR - 1)] = p < npix ? img_px(j, ti.x0, ti.y0, ti.w, p) : 0xff000000u;
-      }
-      wend += LZR_CHUNK;
+      const uint32_t p = wend + (uint32_t)lane;
+      ring[p & (LZR - 1)] = p < npix ? img_px(j, ti.x0, ti.y0, ti.w, p) : 0xff000000u;
+      wend += 64;
     }
     __syncthreads();
   };
@@ -74,7 +73,7 @@ __global__ __launch_bounds__(64) void k_lz(EncodeJob j) {
         }
       }
       if (q == 0xffffffffu) break;
-      fill_to(q + 260);
+      fill_to(q >= 64 ? q - 64 : 0, q + 260);
       const uint32_t b = lane + 1;
       uint32_t L = 0;
       if (b <= q) {
