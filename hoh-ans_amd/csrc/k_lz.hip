@@ -24,8 +24,10 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 
 #define LZR 2048          // pixel ring of k_lz (positions p & (LZR - 1))
 
+#define LZ_BITS_MAX 1024   // candidate words kept in LDS (tiles up to 65,536 pixels)
 __global__ __launch_bounds__(64) void k_lz(EncodeJob j) {
   __shared__ uint32_t ring[LZR];
+  __shared__ uint64_t cbits[LZ_BITS_MAX];
   const int t = blockIdx.x, lane = threadIdx.x;
   TileInfo ti = j.tiles[t];
   const uint32_t npix = (uint32_t)ti.w * ti.h;
@@ -57,12 +59,18 @@ __global__ __launch_bounds__(64) void k_lz(EncodeJob j) {
     }
     __syncthreads();
   };
+  // the candidate bitmap in LDS: the scan searches it once per step (natural tiles: thousands)
+  const bool lds_bits = nwords <= LZ_BITS_MAX;
+  if (ti.ncand && lds_bits) {
+    for (uint32_t i = lane; i < nwords; i += 64) cbits[i] = bits[i];
+    __syncthreads();
+  }
   if (ti.ncand) {
     while (pos < npix) {
       // next candidate q >= pos
       uint32_t q = 0xffffffffu;
       for (uint32_t wi = pos >> 6; wi < nwords; wi += 64) {
-        uint64_t wv = (wi + lane < nwords) ? bits[wi + lane] : 0;
+        uint64_t wv = (wi + lane < nwords) ? (lds_bits ? cbits[wi + lane] : bits[wi + lane]) : 0;
         if (wi + lane == (pos >> 6)) wv &= ~0ull << (pos & 63);
         uint64_t bal = __ballot(wv != 0);
         if (bal) {
@@ -77,7 +85,22 @@ __global__ __launch_bounds__(64) void k_lz(EncodeJob j) {
       const uint32_t b = lane + 1;
       uint32_t L = 0;
       if (b <= q) {
-        while (q + L < npix && L < 259 && ring[(q + L) & (LZR - 1)] == ring[(q + L - b) & (LZR - 1)]) L++;
+        // eight positions per LDS round trip (a flat region's copies run to the 259 cap)
+        const uint32_t lim = min(259u, npix - q);
+        bool go = true;
+        while (go && L < lim) {
+          uint32_t a[8], c[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) {
+            a[u] = ring[(q + L + u) & (LZR - 1)];
+            c[u] = ring[(q + L + u - b) & (LZR - 1)];
+          }
+#pragma unroll
+          for (int u = 0; u < 8; u++) {
+            if (go && L < lim && a[u] == c[u]) L++;
+            else go = false;
+          }
+        }
       }
       uint64_t key = ((uint64_t)L << 8) | (255u - b);
       key = wave_max_u64(key);
