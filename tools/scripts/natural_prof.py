@@ -26,10 +26,11 @@ for _ in range(reps):
     te.append(time.perf_counter() - t)
 dec = torch.empty(W * H * 3, dtype=torch.uint8, device="cuda")
 td = []
-for _ in range(reps):
+for _ in range(reps if speed == 0 else 0):          # the decoder takes -s0 files
     t = time.perf_counter()
     hoh_ans.decode_image(out, n, out_dev=dec, ctx=c, index=ix if speed == 0 else None)
     torch.cuda.synchronize()
     td.append(time.perf_counter() - t)
-print("natural %dx%d -s%d: %d B, encode %.2f ms, decode %.2f ms, lossless %s" %
-      (W, H, speed, n, min(te) * 1e3, min(td) * 1e3, bool(torch.equal(dec, rgb))), flush=True)
+print("natural %dx%d -s%d: %d B, encode %.2f ms, decode %s ms, lossless %s" %
+      (W, H, speed, n, min(te) * 1e3, "%.2f" % (min(td) * 1e3) if td else "-",
+       bool(torch.equal(dec, rgb)) if td else "-"), flush=True)
