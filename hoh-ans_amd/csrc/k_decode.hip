@@ -823,6 +823,9 @@ __global__ void k_dstored(DecJob j, int nstreams) {
   dec_stored(j, sid, d);
 }
 
+// a tile with this many copies reading the row above goes to the raster-order path (natural
+// 8192^2, -s0: threshold 4 / 16 / 64 / never -> decode 24.1 / 24.1 / 23.5 / 24.9 ms)
+#define LZ_XROW 64
 // LZ streams -> matches (un_lz.hpp:150-170); one lane per tile
 __global__ void k_dlz(DecJob j) {
   if (dec_abort(j)) return;
@@ -836,7 +839,7 @@ __global__ void k_dlz(DecJob j) {
   const uint16_t* bb = j.dsym + st[2].out_off;
   uint32_t* mt = j.matches + (size_t)t * 4 * (j.lz_cap + 1);
   const uint32_t npix = (uint32_t)ti.w * ti.h;
-  uint32_t idx = 0, g = 0, nm = 0, nuked = 0;
+  uint32_t idx = 0, g = 0, nm = 0, nuked = 0, xrow = 0;
   bool bad = false;
   for (uint32_t i = 0; i < st[0].n; i++) {
     const uint32_t v = fut[i];
@@ -847,6 +850,7 @@ __global__ void k_dlz(DecJob j) {
     g++;
     if (back == 0 || back > idx || idx + L > npix) { bad = true; break; }
     mt[4 * nm] = idx; mt[4 * nm + 1] = L; mt[4 * nm + 2] = back; mt[4 * nm + 3] = nuked;
+    xrow += (idx % (uint32_t)ti.w) < back;                // the copy reads the row above
     nm++;
     idx += L;
     nuked += L;
@@ -855,7 +859,9 @@ __global__ void k_dlz(DecJob j) {
   ti.nmatch = nm;
   if (bad) { ti.err = 1; atomicOr(j.gerr, 1u); }
   j.tiles[t] = ti;
-  if (!bad && nm && ti.w >= 64) j.lzt[atomicAdd(j.gerr + 2, 1u)] = (uint32_t)t;   // k_dunpred_lz's work list
+  // k_dunpred_lz's work list; bit 31: copies keep reading the row above, decode in raster order
+  if (!bad && nm && ti.w >= 64)
+    j.lzt[atomicAdd(j.gerr + 2, 1u)] = (uint32_t)t | (xrow >= LZ_XROW && ti.w <= 256 ? 0x80000000u : 0u);
 }
 
 __device__ __forceinline__ uint16_t dmed16(uint16_t a, uint16_t b, uint16_t c) {
@@ -1152,15 +1158,147 @@ __device__ __forceinline__ void dunpred_lz_tile(const DecJob& j, int t, uint32_t
 // tile), `many` = 1 otherwise (a worker per tile, 32-row bands in 33 KB: four per CU, so the
 // tiles of a natural image, many of them nearly serial, run at once).
 #define LZ_FEW 256
+__device__ __forceinline__ void dunpred_lzs_tile(const DecJob& j, int t, uint16_t* zrow);
 __global__ __launch_bounds__(64) void k_dunpred_lz(DecJob j, int br, int many) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lz_lds[];
   if (dec_abort(j)) return;
   const uint32_t cnt = *(volatile const uint32_t*)(j.gerr + 2);
   if ((cnt > LZ_FEW) != (many != 0)) return;
   for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
-    dunpred_lz_tile(j, (int)j.lzt[i], lz_lds, br);
+    const uint32_t e = j.lzt[i];
+    const int t = (int)(e & 0x7fffffffu);
+    if ((e >> 31) && (size_t)(br + 1) * j.tw * 4 >= (size_t)12 * j.tiles[t].w)
+      dunpred_lzs_tile(j, t, (uint16_t*)lz_lds);
+    else
+      dunpred_lz_tile(j, t, lz_lds, br);
     __syncthreads();
   }
+}
+
+__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+}
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
+// Raster-order decode of an LZ tile whose copies keep reading the end of the row above (the
+// wavefront would wait a row per row).  The wave runs the reference's loop (layer_decode's
+// unprediction + the LZ copy, lz.hpp) with every lane on the same pixel: wave-uniform control
+// flow and scalar state, the three planes interleaved (their chains are independent, and the
+// copies and the residual index are shared: copied pixels skip a residual in every plane).
+// Residuals come a row (<= 256) at a time, four registers per plane, matches 64 at a time, the
+// row above 64 columns at a time, all picked by readlane; a 64-column chunk's values collect in
+// one register per plane, which goes to LDS (the copies' and the next row's source) and, composed
+// (inverse subtract-green), to the image as one coalesced row segment.
+__device__ __forceinline__ void dunpred_lzs_tile(const DecJob& j, int t, uint16_t* zrow) {
+  const DecTile ti = j.tiles[t];
+  if (ti.err) return;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t w = (uint32_t)ti.w, h = (uint32_t)ti.h;
+  const uint16_t* rs[3];
+  uint32_t n = 0;
+  bool bad = false;
+#pragma unroll
+  for (int p = 0; p < 3; p++) {
+    rs[p] = j.dsym + (size_t)(t * 3 + p) * j.plane_cap;
+    const uint32_t np = j.streams[t * SK_PER_TILE + 3 + p].n;
+    if (p == 0) n = np; else bad |= np != n;
+  }
+  const uint32_t* mt = j.matches + (size_t)t * 4 * (j.lz_cap + 1);
+  const uint32_t nm = ti.nmatch;
+  uint8_t* obase = j.rgb + ((size_t)ti.y0 * j.W + ti.x0) * 3;
+  uint32_t k = 0;                                         // residual index, shared by the planes
+  uint32_t m = 0, mb = 0, mi = 0xffffffffu, ml = 0, mk = 0;  // match block: lane = match mb + lane
+  if (lane < nm) { mi = mt[4 * lane]; ml = mt[4 * lane + 1]; mk = mt[4 * lane + 2]; }
+  uint32_t midx = nm ? rdl(mi, 0) : 0xffffffffu, mend = nm ? midx + rdl(ml, 0) : 0u, mback = nm ? rdl(mk, 0) : 0u;
+  uint32_t cur = 0;
+  for (uint32_t y = 0; y < h; y++) {
+    uint16_t* crow = zrow + cur * 3 * w;                  // [plane][w], this row
+    const uint16_t* prow = zrow + (cur ^ 1) * 3 * w;      // the row above
+    const uint32_t rowi = y * w;
+    uint32_t Lv[3], Tp[3];
+    const uint32_t kb = k;
+    uint32_t r4[3][4];
+#pragma unroll
+    for (int p = 0; p < 3; p++) {
+      Lv[p] = Tp[p] = p ? 256u : 128u;
+#pragma unroll
+      for (int q = 0; q < 4; q++) r4[p][q] = kb + 64 * q + lane < n ? rs[p][kb + 64 * q + lane] : 0u;
+    }
+    for (uint32_t x0 = 0; x0 < w; x0 += 64) {
+      const uint32_t xe = min(w, x0 + 64);
+      uint32_t tv[3], cv[3];
+#pragma unroll
+      for (int p = 0; p < 3; p++) {
+        tv[p] = (y && x0 + lane < w) ? prow[p * w + x0 + lane] : (p ? 256u : 128u);
+        cv[p] = 0;
+      }
+      for (uint32_t x = x0; x < xe; x++) {
+        const uint32_t i = rowi + x;
+        while (mend <= i && m < nm) {                     // next match
+          m++;
+          if (m - mb >= 64) {
+            mb = m;
+            mi = 0xffffffffu; ml = 0; mk = 0;
+            if (mb + lane < nm) { mi = mt[4 * (mb + lane)]; ml = mt[4 * (mb + lane) + 1]; mk = mt[4 * (mb + lane) + 2]; }
+          }
+          if (m < nm) { midx = rdl(mi, m - mb); mend = midx + rdl(ml, m - mb); mback = rdl(mk, m - mb); }
+          else { midx = 0xffffffffu; mend = 0; }
+        }
+        uint32_t T[3], v[3];
+#pragma unroll
+        for (int p = 0; p < 3; p++) T[p] = rdl(tv[p], x - x0);
+        if (m < nm && midx <= i) {
+          const uint32_t src = i - mback;
+          if (src >= rowi + x0) {
+#pragma unroll
+            for (int p = 0; p < 3; p++) v[p] = rdl(cv[p], src - rowi - x0);
+          } else if (src >= rowi) {
+#pragma unroll
+            for (int p = 0; p < 3; p++) v[p] = uni(crow[p * w + src - rowi]);
+          } else if (src + w >= rowi) {
+#pragma unroll
+            for (int p = 0; p < 3; p++) v[p] = uni(prow[p * w + src + w - rowi]);
+          } else {                                        // two rows up: not a -s0 copy (back <= 64 <= w)
+            bad = true;
+#pragma unroll
+            for (int p = 0; p < 3; p++) v[p] = 0;
+          }
+        } else {
+          const uint32_t q = k - kb;
+          bad |= k >= n;
+          k++;
+          uint32_t r[3];
+          if (q < 128) {
+            if (q < 64) { for (int p = 0; p < 3; p++) r[p] = rdl(r4[p][0], q); }
+            else { for (int p = 0; p < 3; p++) r[p] = rdl(r4[p][1], q - 64); }
+          } else {
+            if (q < 192) { for (int p = 0; p < 3; p++) r[p] = rdl(r4[p][2], q - 128); }
+            else { for (int p = 0; p < 3; p++) r[p] = rdl(r4[p][3], q - 192); }
+          }
+#pragma unroll
+          for (int p = 0; p < 3; p++) {
+            const uint32_t c = p ? 512u : 256u;
+            const uint32_t pr = dmed16((uint16_t)T[p], (uint16_t)Lv[p], (uint16_t)(T[p] + Lv[p] - Tp[p]));
+            v[p] = (r[p] + pr + c / 2) & (c - 1);
+          }
+        }
+#pragma unroll
+        for (int p = 0; p < 3; p++) {
+          cv[p] = lane == x - x0 ? v[p] : cv[p];
+          Tp[p] = T[p];
+          Lv[p] = v[p];
+        }
+      }
+      if (x0 + lane < xe) {
+#pragma unroll
+        for (int p = 0; p < 3; p++) crow[p * w + x0 + lane] = (uint16_t)cv[p];
+        uint8_t* o = obase + ((size_t)y * j.W + x0 + lane) * 3;
+        o[0] = (uint8_t)(cv[1] + cv[0] - 256); o[1] = (uint8_t)cv[0]; o[2] = (uint8_t)(cv[2] + cv[0] - 256);
+      }
+    }
+    cur ^= 1;
+  }
+  if (bad || k != n) atomicOr(j.gerr, 1u);
 }
 
 __device__ __forceinline__ void dunpred_lz_tile(const DecJob& j, int t, uint32_t* lz_lds, int BR) {
