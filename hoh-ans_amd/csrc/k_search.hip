@@ -535,15 +535,20 @@ __device__ __forceinline__ uint64_t wmax64(uint64_t v) {
   return v;
 }
 
-// run length of the match of q against q - b (lz.hpp:37-45), at most 259
-__device__ __forceinline__ uint32_t run_len(const EncodeJob& j, const TileInfo& ti, uint32_t npix, uint32_t q, uint32_t b) {
-  uint32_t L = 0;
-  while (q + L < npix && L < 259 && tile_px(j, ti, q + L) == tile_px(j, ti, q + L - b)) L++;
-  return L;
-}
 
-// greedy scan (lz.hpp:32-95) over the candidates, one wave per tile, + the four LZ streams
-__global__ __launch_bounds__(64) void k_lzscan(EncodeJob j, int limit) {
+#define LZS_HB 16        // horizontal back-distance chunks of 64 whose fingerprints load at once
+#define LZS_VB 4         // vertical chunks (k * w <= 65536: 256 rows of a 256-wide tile)
+#define LZS_BITS 1024    // candidate words in LDS (tiles up to 65,536 pixels)
+// greedy scan (lz.hpp:32-95) over the candidates, one wave per tile, + the four LZ streams.
+// Per candidate one batch of global loads (its fingerprint, 16 chunks of 64 horizontal back
+// distances and the vertical ones) and then LDS only: the candidate bitmap is staged in LDS and
+// the run lengths compare pixels from an LDS ring of the positions [q - limit, q + 260) (filled
+// 64 positions at a time as the scan moves: each pixel read once per tile), eight positions per
+// LDS round trip; vertical backs beyond the ring read the image.  rp = ring size (0: -s4, whose
+// 16384-position window does not fit next to the other workgroups; pixels from the image).
+__global__ __launch_bounds__(64) void k_lzscan(EncodeJob j, int limit, int rp) {
+  extern __shared__ uint32_t pring[];
+  __shared__ uint64_t cb[LZS_BITS];
   const int t = blockIdx.x, lane = threadIdx.x;
   TileInfo ti = j.tiles[t];
   const uint32_t npix = (uint32_t)ti.w * ti.h, nwords = (npix + 63) / 64, w = ti.w;
@@ -558,12 +563,52 @@ __global__ __launch_bounds__(64) void k_lzscan(EncodeJob j, int limit) {
     else if (ti.colours <= 32) bonus = 2;
   }
   const uint32_t thr = 4 + bonus;
+  const bool lds_bits = nwords <= LZS_BITS;
+  if (ti.ncand && lds_bits) {
+    for (uint32_t i = lane; i < nwords; i += 64) cb[i] = bits[i];
+    __syncthreads();
+  }
+  const uint32_t rmask = (uint32_t)rp - 1;
+  uint32_t wend = 0;
+  auto fill_to = [&](uint32_t lo, uint32_t need) {
+    if (lo > wend) wend = lo & ~63u;
+    while (wend < need) {
+      const uint32_t p = wend + (uint32_t)lane;
+      pring[p & rmask] = p < npix ? tile_px(j, ti, p) : 0xff000000u;
+      wend += 64;
+    }
+    __syncthreads();
+  };
+  // run length of q against q - b (lz.hpp:37-45), at most 259
+  auto runl = [&](uint32_t q, uint32_t b) -> uint32_t {
+    const uint32_t lim = min(259u, npix - q);
+    uint32_t L = 0;
+    if (rp && b <= (uint32_t)limit) {
+      bool go = true;
+      while (go && L < lim) {
+        uint32_t a[8], c[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          a[u] = pring[(q + L + u) & rmask];
+          c[u] = pring[(q + L + u - b) & rmask];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          if (go && L < lim && a[u] == c[u]) L++;
+          else go = false;
+        }
+      }
+    } else {
+      while (L < lim && (rp ? pring[(q + L) & rmask] : tile_px(j, ti, q + L)) == tile_px(j, ti, q + L - b)) L++;
+    }
+    return L;
+  };
   uint32_t nm = 0, pos = 0;
   bool overflow = false;
   while (ti.ncand && pos < npix) {
     uint32_t q = 0xffffffffu;
     for (uint32_t wi = pos >> 6; wi < nwords; wi += 64) {
-      uint64_t wv = (wi + lane < nwords) ? bits[wi + lane] : 0;
+      uint64_t wv = (wi + lane < nwords) ? (lds_bits ? cb[wi + lane] : bits[wi + lane]) : 0;
       if (wi + lane == (pos >> 6)) wv &= ~0ull << (pos & 63);
       const uint64_t bal = __ballot(wv != 0);
       if (bal) {
@@ -574,33 +619,64 @@ __global__ __launch_bounds__(64) void k_lzscan(EncodeJob j, int limit) {
       }
     }
     if (q == 0xffffffffu) break;
-    const uint32_t f = F[q];
-    // horizontal: b = 1 .. min(limit, q), longest first, then the smallest b; stop at 259
     const uint32_t bm = q < (uint32_t)limit ? q : (uint32_t)limit;
+    const uint32_t kmax = min(65536u, q) / w;                         // vertical: k * w <= min(65536, q)
+    // one batch: f, the first 16 horizontal chunks, the vertical chunks
+    const uint32_t f = F[q];
+    uint32_t fv[LZS_HB], fw[LZS_VB];
+#pragma unroll
+    for (int c = 0; c < LZS_HB; c++) {
+      const uint32_t b = 1 + 64 * c + lane;
+      fv[c] = b <= bm ? F[q - b] : 0u;
+    }
+#pragma unroll
+    for (int c = 0; c < LZS_VB; c++) {
+      const uint32_t k = 1 + 64 * c + lane;
+      fw[c] = k <= kmax ? F[q - k * w] : 0u;
+    }
+    if (rp) fill_to(q >= (uint32_t)limit ? q - (uint32_t)limit : 0u, q + 260);
+    // horizontal: b = 1 .. min(limit, q), longest first, then the smallest b; stop at 259
     uint64_t best = 0;                                                // (L << 32) | (~b)
-    for (uint32_t b0 = 1; b0 <= bm; b0 += 64) {
-      const uint32_t b = b0 + lane;
-      uint64_t key = 0;
-      if (b <= bm && F[q - b] == f) {
-        const uint32_t L = run_len(j, ti, npix, q, b);
-        key = ((uint64_t)L << 32) | (uint32_t)(~b);
+    for (uint32_t g0 = 1; g0 <= bm && (best >> 32) < 259; g0 += 64 * LZS_HB) {
+      if (g0 > 1) {
+#pragma unroll
+        for (int c = 0; c < LZS_HB; c++) {
+          const uint32_t b = g0 + 64 * c + lane;
+          fv[c] = b <= bm ? F[q - b] : 0u;
+        }
       }
-      key = wmax64(key);
-      if (key > best) best = key;
-      if ((best >> 32) == 259) break;
+      uint32_t hb = 0;                                                // lane's hits, bit c = chunk c
+#pragma unroll
+      for (int c = 0; c < LZS_HB; c++) hb |= (uint32_t)(g0 + 64 * c + lane <= bm && fv[c] == f) << c;
+      for (int c = 0; c < LZS_HB; c++) {
+        const bool hit = (hb >> c) & 1;
+        if ((best >> 32) < 259 && __ballot(hit)) {
+          const uint32_t b = g0 + 64 * c + lane;
+          uint64_t key = 0;
+          if (hit) key = ((uint64_t)runl(q, b) << 32) | (uint32_t)(~b);
+          key = wmax64(key);
+          if (key > best) best = key;
+        }
+      }
     }
     // vertical (lz.hpp:54-74): whole rows up to 65536 back, strictly longer only
     if ((best >> 32) < 259) {
       uint64_t vb = 0;
-      for (uint32_t k0 = 1; k0 * w <= 65536u && k0 * w <= q; k0 += 64) {
-        const uint32_t k = k0 + lane, b = k * w;
+      auto vchunk = [&](uint32_t k, uint32_t fk) {
+        const uint32_t b = k * w;
+        const bool hit = k <= kmax && fk == f;
+        if (!__ballot(hit)) return;
         uint64_t key = 0;
-        if (b <= 65536u && b <= q && F[q - b] == f) {
-          const uint32_t L = run_len(j, ti, npix, q, b);
-          key = ((uint64_t)L << 32) | (uint32_t)(~b);
-        }
+        if (hit) key = ((uint64_t)runl(q, b) << 32) | (uint32_t)(~b);
         key = wmax64(key);
         if (key > vb) vb = key;
+      };
+      uint32_t vh = 0;
+#pragma unroll
+      for (int c = 0; c < LZS_VB; c++) vh |= (uint32_t)(fw[c] == f) << c;
+      for (uint32_t k0 = 1; k0 <= kmax; k0 += 64) {                   // beyond LZS_VB: narrow tiles
+        const uint32_t k = k0 + lane, c = (k0 - 1) / 64;
+        vchunk(k, c < LZS_VB ? ((vh >> c) & 1 ? f : ~f) : (k <= kmax ? F[q - k * w] : 0u));
       }
       if ((vb >> 32) > (best >> 32)) best = vb;
     }
@@ -937,7 +1013,10 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, void (*mark)(void*, const
   mark(mc, "search");
   hipLaunchKernelGGL(k_lzfp, dim3(16, j.ntiles), dim3(NT), 0, s, j);
   hipLaunchKernelGGL(k_lzcand, dim3(j.ntiles), dim3(NT), (size_t)ring * 4, s, j, limit, ring);
-  hipLaunchKernelGGL(k_lzscan, dim3(j.ntiles), dim3(64), 0, s, j, limit);
+  int rp = 1;
+  while (rp < limit + 324) rp <<= 1;
+  if (rp > 8192) rp = 0;                                              // -s4: pixels from the image
+  hipLaunchKernelGGL(k_lzscan, dim3(j.ntiles), dim3(64), (size_t)(rp ? rp : 1) * 4, s, j, limit, rp);
   launch_nuke(j, s);
   mark(mc, "lz");
   hipLaunchKernelGGL(k_setup_s, dim3(j.ntiles), dim3(128), 0, s, j);
