@@ -509,14 +509,22 @@ __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring)
     __syncthreads();
     bool c = false;
     if (f) {
+      // eight ring entries per LDS round trip, sixteen rows per batch of global loads
       const uint32_t bm = q < (uint32_t)limit ? q : (uint32_t)limit;
-      for (uint32_t b = 1; b <= bm; b++) {
-        if (fr[(q - b) & (ring - 1)] == f) { c = true; break; }
+      for (uint32_t b0 = 1; b0 <= bm && !c; b0 += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = fr[(q - b0 - u) & (ring - 1)];
+#pragma unroll
+        for (int u = 0; u < 8; u++) c |= b0 + u <= bm && v[u] == f;
       }
-      if (!c) {
-        for (uint32_t b = w; b <= 65536u && b <= q; b += w) {
-          if (b > bm && F[q - b] == f) { c = true; break; }
-        }
+      const uint32_t vlim = min(65536u, q);
+      for (uint32_t b0 = (bm / w + 1) * w; b0 <= vlim && !c; b0 += 16 * w) {
+        uint32_t v[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) v[u] = b0 + u * w <= vlim ? F[q - b0 - u * w] : 0u;
+#pragma unroll
+        for (int u = 0; u < 16; u++) c |= v[u] == f;
       }
     }
     const uint64_t word = __ballot(c);
