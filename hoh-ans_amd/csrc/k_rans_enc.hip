@@ -212,8 +212,7 @@ __global__ __launch_bounds__(64) void k_rans_gen(EncodeJob j, int nstreams, SidM
   const bool so = st.sizeonly;                  // size-only: count the words, store nothing
   const bool ckp = !so && ck != nullptr;
   uint64_t x = 1ull << 31;
-  for (uint32_t i = st.n; i > 0; i--) {
-    const EncGen g = tab[sp[i - 1]];
+  auto step = [&](const EncGen& g, uint32_t i) {           // symbol i - 1
     const uint64_t x_max = (((1ull << 31) >> pb) << 32) * g.freq;
     if (x >= x_max) {
       --widx;
@@ -226,6 +225,35 @@ __global__ __launch_bounds__(64) void k_rans_gen(EncodeJob j, int nstreams, SidM
       Checkpoint p;
       p.xl = (uint32_t)x; p.xh = (uint32_t)(x >> 32); p.widx = widx; p.pad = 0;
       ck[(i - 1) / HOH_SEG] = p;
+    }
+  };
+  // the top n % 8 symbols one at a time, then 8-symbol blocks whose symbols and table entries
+  // are gathered one block ahead (two buffers), so the chain waits on no load
+  uint32_t k = st.n;
+  for (; k > (st.n & ~7u); k--) step(tab[sp[k - 1]], k);
+  if (k) {
+    EncGen ga[8], gb[8];
+    auto fetch = [&](EncGen* g, uint32_t top) {           // symbols top-1 .. top-8
+      uint32_t sy[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) sy[u] = sp[top - 1 - u];
+#pragma unroll
+      for (int u = 0; u < 8; u++) g[u] = tab[sy[u]];
+    };
+    auto run = [&](const EncGen* g, uint32_t top) {
+#pragma unroll
+      for (int u = 0; u < 8; u++) step(g[u], top - u);
+    };
+    fetch(ga, k);
+    for (;;) {
+      fetch(gb, k > 8 ? k - 8 : 8);                      // unconditional (a conditional load would
+      run(ga, k);                                         // make the compiler wait at the join)
+      k -= 8;
+      if (!k) break;
+      fetch(ga, k > 8 ? k - 8 : 8);
+      run(gb, k);
+      k -= 8;
+      if (!k) break;
     }
   }
   widx -= 2;
