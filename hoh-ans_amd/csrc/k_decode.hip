@@ -826,11 +826,25 @@ __global__ void k_dstored(DecJob j, int nstreams) {
 // a tile with this many copies reading the row above goes to the raster-order path (natural
 // 8192^2, -s0: threshold 4 / 16 / 64 / never -> decode 24.1 / 24.1 / 23.5 / 24.9 ms)
 #define LZ_XROW 64
-// LZ streams -> matches (un_lz.hpp:150-170); one lane per tile
-__global__ void k_dlz(DecJob j) {
+// LZ streams -> matches (un_lz.hpp:150-170); one wave per tile, 64 future entries per step.
+// Serially idx += fut[i], and a non-255 entry is a match (its length and back distance are the
+// g-th entries of the other two streams, g = matches before it) that advances idx by L too: the
+// positions are an inclusive prefix sum of v + L (uint32, wrapping like the serial walk), g a
+// ballot count, `nuked` an exclusive prefix sum of L. Any bad match fails the tile (the serial
+// walk stopped at the first one; the tile's error is the same).
+__device__ __forceinline__ uint32_t wave_incl_u32(uint32_t x, uint32_t lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  return x;
+}
+
+__global__ __launch_bounds__(64) void k_dlz(DecJob j) {
   if (dec_abort(j)) return;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= j.ntiles) return;
+  const int t = blockIdx.x;
+  const uint32_t lane = threadIdx.x;
   DecTile ti = j.tiles[t];
   if (ti.err) return;
   const DecStream* st = j.streams + (size_t)t * SK_PER_TILE;
@@ -838,29 +852,46 @@ __global__ void k_dlz(DecJob j) {
   const uint16_t* len = j.dsym + st[1].out_off;
   const uint16_t* bb = j.dsym + st[2].out_off;
   uint32_t* mt = j.matches + (size_t)t * 4 * (j.lz_cap + 1);
-  const uint32_t npix = (uint32_t)ti.w * ti.h;
-  uint32_t idx = 0, g = 0, nm = 0, nuked = 0, xrow = 0;
+  const uint32_t npix = (uint32_t)ti.w * ti.h, w = (uint32_t)ti.w;
+  const uint32_t nf = st[0].n, gcap = min(min(st[1].n, st[2].n), j.lz_cap);
+  const uint64_t lt = (1ull << lane) - 1;
+  uint32_t idx0 = 0, g0 = 0, nuked0 = 0, xrow = 0;
   bool bad = false;
-  for (uint32_t i = 0; i < st[0].n; i++) {
-    const uint32_t v = fut[i];
-    if (v == 255) { idx += 255; continue; }
-    idx += v;
-    if (g >= st[1].n || g >= st[2].n || nm >= j.lz_cap) { bad = true; break; }
-    const uint32_t L = len[g] + 4, back = bb[g];
-    g++;
-    if (back == 0 || back > idx || idx + L > npix) { bad = true; break; }
-    mt[4 * nm] = idx; mt[4 * nm + 1] = L; mt[4 * nm + 2] = back; mt[4 * nm + 3] = nuked;
-    xrow += (idx % (uint32_t)ti.w) < back;                // the copy reads the row above
-    nm++;
-    idx += L;
-    nuked += L;
+  for (uint32_t i0 = 0; i0 < nf; i0 += 64) {
+    const uint32_t i = i0 + lane;
+    const uint32_t v = i < nf ? fut[i] : 0u;
+    const bool m = i < nf && v != 255;
+    const uint64_t mb = __ballot(m);
+    const uint32_t g = g0 + (uint32_t)__popcll(mb & lt);
+    uint32_t L = 0, back = 0;
+    if (m) {
+      if (g >= gcap) bad = true;
+      else { L = (uint32_t)len[g] + 4; back = bb[g]; }
+    }
+    const uint32_t c = v + L;                                   // 255 entries: v = 255, L = 0
+    const uint32_t ic = wave_incl_u32(c, lane), il = wave_incl_u32(L, lane);
+    if (m && !bad) {
+      const uint32_t idx = idx0 + ic - L;                       // the match's position
+      if (back == 0 || back > idx || idx + L > npix) bad = true;
+      else {
+        *(uint4*)(mt + 4 * g) = make_uint4(idx, L, back, nuked0 + il - L);
+        xrow += (idx % w) < back;                               // the copy reads the row above
+      }
+    }
+    idx0 += __shfl(ic, 63);
+    nuked0 += __shfl(il, 63);
+    g0 += (uint32_t)__popcll(mb);
+    if (__any(bad)) break;
   }
-  if (idx > npix) bad = true;
-  ti.nmatch = nm;
+  bad = __any(bad) || idx0 > npix;
+#pragma unroll
+  for (int o = 32; o; o >>= 1) xrow += __shfl_xor(xrow, o);
+  if (lane) return;
+  ti.nmatch = g0;
   if (bad) { ti.err = 1; atomicOr(j.gerr, 1u); }
   j.tiles[t] = ti;
   // k_dunpred_lz's work list; bit 31: copies keep reading the row above, decode in raster order
-  if (!bad && nm && ti.w >= 64)
+  if (!bad && g0 && ti.w >= 64)
     j.lzt[atomicAdd(j.gerr + 2, 1u)] = (uint32_t)t | (xrow >= LZ_XROW && ti.w <= 256 ? 0x80000000u : 0u);
 }
 
@@ -1682,7 +1713,7 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   }
   ctx_mark(c, s, "drans", false);
   if (!indexed) hipLaunchKernelGGL(k_dstored, dim3(S), dim3(256), 0, s, j, S);
-  hipLaunchKernelGGL(k_dlz, dim3((j.ntiles + 63) / 64), dim3(64), 0, s, j);
+  hipLaunchKernelGGL(k_dlz, dim3(j.ntiles), dim3(64), 0, s, j);
   ctx_mark(c, s, "dlz", false);
   hipLaunchKernelGGL(k_dunpred_fast, dim3(j.ntiles), dim3(64), (size_t)64 * ORING_PITCH + 6 * LAST_N(j.tw), s, j);
   {
