@@ -63,16 +63,19 @@ __device__ __forceinline__ void preds16(uint32_t L, uint32_t T, uint32_t TL, uin
   p.v[13] = avg3(TL, T, T); p.v[14] = avg3(T, T, TR); p.v[15] = avg3(T, TR, TR);
 }
 
-// p.v[k] for a lane-varying k without dynamic register indexing (4-level select tree)
+// p.v[k] for a lane-varying k without dynamic register indexing: a 4-level tree of bit blends
+// (v_bfi_b32). The masks pass through an empty asm so the compiler cannot see they are 0 / ~0:
+// written as selects, it folded the tree into a dynamically indexed private array (Preds and the
+// tree levels in scratch, ~12 dependent scratch round trips per pixel step of the cell walk).
+__device__ __forceinline__ uint32_t blend(uint32_t a, uint32_t b, uint32_t m) { return (a & ~m) | (b & m); }
 __device__ __forceinline__ uint32_t pick(const Preds& p, uint32_t k) {
-  uint32_t a[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) a[i] = (k & 1) ? p.v[2 * i + 1] : p.v[2 * i];
-  uint32_t b[4];
-#pragma unroll
-  for (int i = 0; i < 4; i++) b[i] = (k & 2) ? a[2 * i + 1] : a[2 * i];
-  const uint32_t c0 = (k & 4) ? b[1] : b[0], c1 = (k & 4) ? b[3] : b[2];
-  return (k & 8) ? c1 : c0;
+  uint32_t m0 = 0u - (k & 1u), m1 = 0u - ((k >> 1) & 1u), m2 = 0u - ((k >> 2) & 1u), m3 = 0u - ((k >> 3) & 1u);
+  asm volatile("" : "+v"(m0), "+v"(m1), "+v"(m2), "+v"(m3));
+  const uint32_t a0 = blend(p.v[0], p.v[1], m0), a1 = blend(p.v[2], p.v[3], m0), a2 = blend(p.v[4], p.v[5], m0),
+                 a3 = blend(p.v[6], p.v[7], m0), a4 = blend(p.v[8], p.v[9], m0), a5 = blend(p.v[10], p.v[11], m0),
+                 a6 = blend(p.v[12], p.v[13], m0), a7 = blend(p.v[14], p.v[15], m0);
+  const uint32_t b0 = blend(a0, a1, m1), b1 = blend(a2, a3, m1), b2 = blend(a4, a5, m1), b3 = blend(a6, a7, m1);
+  return blend(blend(b0, b1, m2), blend(b2, b3, m2), m3);
 }
 
 // first masked predictor of least |v - p| (prediction.hpp:138-146, :213-224)
@@ -166,8 +169,12 @@ __device__ double cell_cost(const uint16_t* D, int w, int h, int depth, int xt, 
       L = TL = half;
     }
     const uint16_t* row = D + (long)(y0 + ym) * w + x0;
-    for (int xm = 0; xm < tw && x0 + xm < w; xm++) {
-      const uint32_t v = row[xm];
+    const int vw = min(tw, w - x0);
+    // the cell's pixels one step ahead of their use (the walk is latency-bound on these loads)
+    uint32_t vn = vw > 0 ? row[0] : 0u;
+    for (int xm = 0; xm < vw; xm++) {
+      const uint32_t v = vn;
+      if (xm + 1 < vw) vn = row[xm + 1];
       const uint32_t T = top[xm];
       const int xr = xm + 1 == tw ? 0 : xm + 1;
       const uint32_t TR = top[xr];
@@ -175,7 +182,7 @@ __device__ double cell_cost(const uint16_t* D, int w, int h, int depth, int xt, 
       preds16(L, T, TL, TR, false, p);
       const int xl = xm == 0 ? tw - 1 : xm - 1;
       const uint32_t pr = midp(pick(p, bp[xm]), pick(p, bp[xl]));
-      const uint32_t r = (uint32_t)(((int)v - (int)pr + half + c) % c);
+      const uint32_t r = ((uint32_t)((int)v - (int)pr + half + c)) & (uint32_t)(c - 1);   // > 0: % c
       cost += ent[r];
       TL = T;
       top[xm] = (uint16_t)v;
