@@ -226,7 +226,7 @@ __device__ __forceinline__ uint32_t resid_all(const AllCtx& a, int x, int y) {
   Preds p;
   preds_all_at(a, x, y, p);
   const uint32_t pr = midp(pick(p, bA), pick(p, bB));
-  return (uint32_t)(((int)a.D[(long)y * a.w + x] - (int)pr + a.half + a.c) % a.c);
+  return ((uint32_t)((int)a.D[(long)y * a.w + x] - (int)pr + a.half + a.c)) & (uint32_t)(a.c - 1);   // > 0: % c
 }
 
 // one workgroup per (tile, plane)
