@@ -142,8 +142,8 @@ struct SearchLds {
   double ent[512];
   double cost[HOH_MAPCAP * 14];
   uint32_t hist[512];
-  uint16_t top[NT][40];
-  uint8_t bp[NT][40];
+  uint16_t top[NT][42];   // rows of 21 / 11 dwords (odd): the lanes' same-column accesses hit
+  uint8_t bp[NT][44];     // distinct banks (40 / 40 gave 4- / 2-way conflicts)
   uint16_t plist[HOH_MAPCAP];
   uint8_t pidx[HOH_MAPCAP];
 };
