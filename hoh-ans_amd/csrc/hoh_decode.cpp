@@ -98,6 +98,82 @@ int hoh_entropy_count(const uint8_t* in, size_t in_size, size_t bp, size_t* n) {
   return ok ? HOH_OK : HOH_E_CORRUPT;
 }
 
+// Framing walk of one stream (entropy_decoding.hpp:143-154 header, :174-250 table field widths,
+// :256 payload size; stored streams :278-290), no symbol decoding: the bit fields are counted,
+// not read.  Field reads start on a fresh byte (slag_bits = 0), so a run of b bits takes
+// ceil(b / 8) bytes.
+int hoh_entropy_parse(const uint8_t* in, size_t in_size, size_t bp, hoh_entropy_header* h) {
+  if (!in || !h) return HOH_E_ARG;
+  bool ok = true;
+  size_t p = bp;
+  const uint64_t range = rdv(in, in_size, p, ok) + 1;
+  const uint64_t count = rdv(in, in_size, p, ok);
+  if (!ok) return HOH_E_CORRUPT;
+  uint32_t mb = 0;
+  for (uint64_t v = range - 1; v; v >>= 1) mb++;
+  *h = hoh_entropy_header{};
+  h->range = range;
+  h->count = count;
+  h->symbol_bits = mb;
+  if (count == 0) {                                                    // header only (entropy_encoding.hpp:19-23)
+    h->table_end = h->stream_end = p;
+    return HOH_OK;
+  }
+  if (p >= in_size) return HOH_E_CORRUPT;
+  const uint8_t meta = in[p++];
+  h->entropy_mode = meta >> 7;
+  h->prob_bits = (meta & 0x3c) >> 2;
+  h->table_mode = meta & 3;
+  if (!h->entropy_mode) {                                              // stored (:278-290)
+    h->table_end = p;
+    h->payload_bytes = (count * mb + 7) / 8;
+    h->stream_end = p + h->payload_bytes;
+    return h->stream_end <= in_size ? HOH_OK : HOH_E_CORRUPT;
+  }
+  uint64_t bits = 0;
+  if (h->table_mode == 1) {
+    bits = range * mb;                                                 // raw widths (:180-195)
+  } else if (h->table_mode == 2) {                                     // clamped widths (:196-244)
+    const uint32_t pb = h->prob_bits;
+    const int nclamp = ((int)pb - 1) / 4 + 2;
+    std::vector<uint32_t> lo(nclamp), hi(nclamp);
+    uint64_t q = (uint64_t)p * 8;                                      // bit cursor
+    auto field = [&](uint32_t w) -> uint32_t {
+      uint32_t v = 0;
+      for (uint32_t i = 0; i < w; i++, q++) {
+        if (q / 8 >= in_size) { ok = false; return 0; }
+        v = (v << 1) | ((in[q / 8] >> (7 - q % 8)) & 1);
+      }
+      return v;
+    };
+    for (int i = 0; i < nclamp; i++) { lo[i] = field(mb); hi[i] = field(mb); }
+    if (ok && lo[0] == hi[0] && lo[0] < range) {
+      // single-symbol table: one field of the widest class, whose 2^pb value overflowed it
+      //  -- recognised as the GPU decoder does (k_dparse)
+      const uint32_t w = nclamp >= 3 ? 4 * (nclamp - 1) : 4;
+      bits += w > pb ? pb : w;
+    } else
+    for (uint64_t i = 0; i < range && ok; i++) {
+      uint32_t w = 0;
+      if (lo[0] <= i && hi[0] >= i) w = 1;
+      if (lo[1] <= i && hi[1] >= i) w = 4;
+      for (int j = 2; j < nclamp; j++)
+        if (lo[j] <= i && hi[j] >= i) w = 4 * j;
+      bits += w > pb ? pb : w;
+    }
+    if (!ok) return HOH_E_CORRUPT;
+    bits += (uint64_t)2 * nclamp * mb;
+  } else if (h->table_mode == 3) {
+    return HOH_E_CORRUPT;                                              // unimplemented there (:245-247)
+  }
+  p += (size_t)((bits + 7) / 8);
+  h->table_end = p;
+  if (p > in_size) return HOH_E_CORRUPT;
+  h->payload_bytes = rdv(in, in_size, p, ok);
+  h->stream_end = p + h->payload_bytes;
+  return ok && h->stream_end <= in_size ? HOH_OK : HOH_E_CORRUPT;
+}
+
 int hoh_decode_entropy(hoh_ctx* c, const uint8_t* in, size_t in_size, size_t* bp, uint16_t* out, size_t cap,
                        size_t* n) {
   if (!c || !in || !bp || !n || *bp >= in_size) return HOH_E_ARG;

@@ -97,6 +97,7 @@ def lib():
             ("hoh_encode_entropy", [vp, vp, sz, sz, C.c_uint32, vp, sz, szp]),
             ("hoh_decode_entropy", [vp, vp, sz, szp, vp, sz, szp]),
             ("hoh_entropy_count", [vp, sz, sz, szp]),
+            ("hoh_entropy_parse", [vp, sz, sz, vp]),
             ("hoh_layer_encode", [vp, vp, sz, C.c_int, C.c_int, C.c_int, sz, vp, vp, sz, szp]),
             ("hoh_layer_decode", [vp, vp, sz, sz, C.c_int, C.c_int, C.c_int, vp, vp]),
             ("hoh_predict_fastpath", [vp, vp, C.c_int, C.c_int, C.c_int, vp]),
@@ -451,6 +452,22 @@ def decode_entropy(data, byte_pointer=0, ctx=None):
     check(lib().hoh_decode_entropy(ctx.h, _p(b), b.size, C.byref(bp), _p(out), out.size, C.byref(n)),
           "hoh_decode_entropy")
     return out[:n.value], bp.value
+
+
+class EntropyHeader(C.Structure):
+    """hoh_entropy_header (include/hoh_ans.h)"""
+    _fields_ = [("range", C.c_uint64), ("count", C.c_uint64), ("entropy_mode", C.c_uint32),
+                ("prob_bits", C.c_uint32), ("table_mode", C.c_uint32), ("symbol_bits", C.c_uint32),
+                ("table_end", C.c_uint64), ("payload_bytes", C.c_uint64), ("stream_end", C.c_uint64)]
+
+
+def entropy_parse(data, byte_pointer=0):
+    """Framing of one stream without decoding it (host only; decode_entropy_simple,
+    entropy_decoding.hpp:8-132) -> dict of the hoh_entropy_header fields."""
+    b = np.frombuffer(bytes(data), np.uint8).copy()
+    h = EntropyHeader()
+    check(lib().hoh_entropy_parse(_p(b), b.size, byte_pointer, C.byref(h)), "hoh_entropy_parse")
+    return {f: int(getattr(h, f)) for f, _ in EntropyHeader._fields_}
 
 
 def layer_encode(plane, depth, nuke=None, ctx=None, speed=0):

@@ -8,6 +8,13 @@
 #include <cstdint>
 #include <vector>
 #include "hoh_gpu.hpp"
+// The reference header brings these in for its callers (entropy_encoding.hpp:4-6); keep that
+// when this header stands in the reference tree.
+#if __has_include("rans64.hpp") && __has_include("varint.hpp") && __has_include("stattools.hpp")
+#include "rans64.hpp"
+#include "varint.hpp"
+#include "stattools.hpp"
+#endif
 
 inline size_t encode_entropy(uint16_t* symbols, size_t symbol_size, size_t range, uint8_t* output_bytes,
                              uint32_t prob_bits, uint8_t /*diagnostics*/) {

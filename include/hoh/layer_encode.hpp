@@ -8,6 +8,10 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <cmath>
+#include "entropy_encoding.hpp"   // the reference header includes these (layer_encode.hpp:4-9)
+#include "entropy_decoding.hpp"
+#include "prediction.hpp"
 #include "hoh_gpu.hpp"
 
 inline size_t layer_encode(uint16_t* data, size_t size, int width, int height, int depth, size_t cruncher_mode,

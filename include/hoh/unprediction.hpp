@@ -6,6 +6,9 @@
 #include <cstddef>
 #include <cstdint>
 #include "hoh_gpu.hpp"
+#if __has_include("predictor_operations.hpp")   // included by the reference header (:4)
+#include "predictor_operations.hpp"
+#endif
 
 inline uint16_t* unpredict_all(uint16_t* data, size_t size, int width, int height, int depth, int x_tiles,
                                int y_tiles, uint16_t* tile_map, uint16_t* LEMPEL_BACKREF) {

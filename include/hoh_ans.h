@@ -186,6 +186,19 @@ int hoh_decode_entropy(hoh_ctx* ctx, const uint8_t* in, size_t in_size, size_t* 
                        uint16_t* out, size_t cap, size_t* n);
 int hoh_entropy_count(const uint8_t* in, size_t in_size, size_t byte_pointer, size_t* n);
 
+/* Framing of the stream at byte_pointer without decoding it (decode_entropy_simple,
+ * entropy_decoding.hpp:8-132): header fields, where the frequency table ends, the rANS payload
+ * size and where the whole stream ends (the Q1-corrected *byte_pointer).  Host only. */
+typedef struct hoh_entropy_header {
+  uint64_t range, count;               /* symbol range, symbol count (:143-144)               */
+  uint32_t entropy_mode, prob_bits;    /* metadata byte (:151-154): 1 = rANS, 0 = stored       */
+  uint32_t table_mode, symbol_bits;    /* table storage mode; bits per stored symbol (:146-149) */
+  uint64_t table_end;                  /* offset after the frequency table (rANS streams)      */
+  uint64_t payload_bytes;              /* rANS payload size (:256) or stored bytes             */
+  uint64_t stream_end;                 /* offset after the whole stream                        */
+} hoh_entropy_header;
+int hoh_entropy_parse(const uint8_t* in, size_t in_size, size_t byte_pointer, hoh_entropy_header* h);
+
 /* Batched device form: nstreams streams, stream i = d_syms[h_offsets[i] .. + h_counts[i]]
  * (h_offsets multiples of 8), all with the same range and prob_bits; stream i is written to
  * d_out + h_out_offsets[i] (caller-chosen, each with hoh_entropy_bound room); h_sizes[i]

@@ -30,6 +30,26 @@ int main() {
     return 1;
   }
   delete[] back;
+  // two streams back to back through decode_entropy_8bit / decode_entropy_simple
+  // (simple_entropy_decoder.cpp:28, un_lz.hpp:30-139: each call must leave *byte_pointer at the next stream)
+  std::vector<uint8_t> sym8(3000);
+  for (size_t i = 0; i < sym8.size(); i++) sym8[i] = (uint8_t)((i * 7 + (i >> 4)) % 40);
+  std::vector<uint8_t> two(2 * hoh_entropy_bound(sym8.size(), 256, 15));
+  const size_t n1 = encode_entropy(sym8.data(), sym8.size(), 256, two.data(), 15, 0);
+  const size_t n2 = encode_entropy(sym.data(), 700, 256, two.data() + n1, 15, 0);
+  bp = 0;
+  uint8_t* b8 = decode_entropy_8bit(two.data(), n1 + n2, &bp, &cnt, 0);
+  if (!n1 || !n2 || !b8 || cnt != sym8.size() || bp != n1 || std::memcmp(b8, sym8.data(), cnt)) {
+    std::printf("decode_entropy_8bit FAILED\n");
+    return 1;
+  }
+  delete[] b8;
+  size_t c2 = 0;
+  decode_entropy_simple(two.data(), n1 + n2, &bp, &c2, 1);
+  if (bp != n1 + n2 || c2 != 700) { std::printf("decode_entropy_simple FAILED (%zu %zu)\n", bp, c2); return 1; }
+  bp = 0;
+  decode_entropy_simple(two.data(), n1 + n2, &bp, &c2, 0);
+  if (bp != n1 || c2 != sym8.size()) { std::printf("decode_entropy_simple FAILED\n"); return 1; }
   // predictor round trip
   size_t bs = 0;
   uint16_t* res = channelpredict_fastpath(plane.data(), plane.size(), w, h, 8, &bs);
@@ -46,6 +66,7 @@ int main() {
   for (size_t i = 0; i < plane.size(); i++)
     if (dec[i] != (uint8_t)plane[i]) { std::printf("layer round trip FAILED at %zu\n", i); return 1; }
   delete[] dec;
+  decode_layer_simple(lay.data(), ln, 0, w, h, 8);
   std::printf("drop-in headers ok: stream %zu B, layer %zu B\n", n, ln);
   return 0;
 }
