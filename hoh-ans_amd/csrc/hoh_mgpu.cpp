@@ -9,7 +9,8 @@
 // RCCL (librccl.so, the communicators of ncclCommInitAll) is loaded at hoh_mgpu_create, so
 // single-GPU users of libhohgpu need no RCCL.  When a device appears twice in the list (several
 // shards on one GPU -- the way to exercise the gather on a one-GPU machine) RCCL cannot build a
-// communicator and the blobs move by device copies instead; the bytes are the same.
+// communicator and the blobs move by device copies instead; the bytes are the same.  The same
+// peer-copy transport serves distinct devices when librccl is absent or ncclCommInitAll fails.
 #include "hoh_internal.h"
 #include "../../include/hoh_ans.h"
 #include <rccl/rccl.h>
@@ -105,12 +106,11 @@ int hoh_mgpu_create(hoh_mgpu** out, int ndev, const int* devices) {
   bool distinct = true;
   for (int a = 0; a < ndev; a++)
     for (int b = a + 1; b < ndev; b++) distinct &= devices[a] != devices[b];
-  if (!e && distinct) {
-    if (!g_rccl.load()) e = HOH_E_UNSUPPORTED;
-    else {
-      m->comm.assign(ndev, nullptr);
-      if (g_rccl.init_all(m->comm.data(), ndev, devices) != ncclSuccess) { m->comm.clear(); e = HOH_E_HIP; }
-    }
+  // distinct devices: one RCCL communicator each; without librccl, or when ncclCommInitAll
+  // fails, the blobs move by peer copies instead (transport 0) -- the bytes are the same
+  if (!e && distinct && g_rccl.load()) {
+    m->comm.assign(ndev, nullptr);
+    if (g_rccl.init_all(m->comm.data(), ndev, devices) != ncclSuccess) m->comm.clear();
   }
   if (e) { hoh_mgpu_destroy(m); return e; }
   *out = m;
@@ -130,6 +130,16 @@ void hoh_mgpu_destroy(hoh_mgpu* m) {
 }
 
 int hoh_mgpu_transport(const hoh_mgpu* m) { return m && !m->comm.empty() ? 1 : 0; }
+
+// every device's stream drained: an error return after transfers were enqueued must not leave
+// them running into buffers the next call (or hoh_mgpu_destroy) reuses
+static int drain(hoh_mgpu* m, int e) {
+  for (int r = 0; r < m->n; r++) {
+    (void)hipSetDevice(m->dev[r]);
+    if (hipStreamSynchronize(m->st[r]) != hipSuccess && !e) e = HOH_E_HIP;
+  }
+  return e;
+}
 
 int hoh_mgpu_encode_image(hoh_mgpu* m, const uint8_t* h_rgb, int W, int H, int speed, uint8_t* d_out, size_t cap,
                           size_t* out_size, size_t* printed) {
@@ -182,7 +192,7 @@ int hoh_mgpu_encode_image(hoh_mgpu* m, const uint8_t* h_rgb, int W, int H, int s
     work(0);
     for (auto& t : th) t.join();
   }
-  for (int r = 0; r < n; r++) if (err[r]) return err[r];
+  for (int r = 0; r < n; r++) if (err[r]) return drain(m, err[r]);
   // the file: prefix, then the blobs in device order (tile order)
   std::vector<uint32_t> all;
   for (int r = 0; r < n; r++) all.insert(all.end(), ts[r].begin(), ts[r].end());
@@ -195,28 +205,25 @@ int hoh_mgpu_encode_image(hoh_mgpu* m, const uint8_t* h_rgb, int W, int H, int s
   if (printed) *printed = off[n];
   if (off[n] > cap) return HOH_E_CAP;
   (void)hipSetDevice(m->dev[0]);
-  if (hipMemcpyAsync(d_out, prefix.data(), pl, hipMemcpyHostToDevice, m->st[0]) != hipSuccess) return HOH_E_HIP;
+  // the prefix (a few KB, host vector) synchronously: nothing else touches those bytes
+  if (hipMemcpy(d_out, prefix.data(), pl, hipMemcpyHostToDevice) != hipSuccess) return HOH_E_HIP;
   if (bsz[0] && hipMemcpyAsync(d_out + off[0], m->blob[0].p, bsz[0], hipMemcpyDeviceToDevice, m->st[0]) != hipSuccess)
-    return HOH_E_HIP;
+    return drain(m, HOH_E_HIP);
   if (!m->comm.empty()) {
-    if (g_rccl.group_start() != ncclSuccess) return HOH_E_HIP;
+    if (g_rccl.group_start() != ncclSuccess) return drain(m, HOH_E_HIP);
     ncclResult_t rr = ncclSuccess;
     for (int r = 1; r < n && rr == ncclSuccess; r++) {
       if (!bsz[r]) continue;
       rr = g_rccl.send(m->blob[r].p, bsz[r], ncclUint8, 0, m->comm[r], m->st[r]);
       if (rr == ncclSuccess) rr = g_rccl.recv(d_out + off[r], bsz[r], ncclUint8, r, m->comm[0], m->st[0]);
     }
-    if (g_rccl.group_end() != ncclSuccess || rr != ncclSuccess) return HOH_E_HIP;
+    if (g_rccl.group_end() != ncclSuccess || rr != ncclSuccess) return drain(m, HOH_E_HIP);
   } else {
     for (int r = 1; r < n; r++)
       if (bsz[r] && hipMemcpyPeerAsync(d_out + off[r], m->dev[0], m->blob[r].p, m->dev[r], bsz[r], m->st[0]) != hipSuccess)
-        return HOH_E_HIP;
+        return drain(m, HOH_E_HIP);
   }
-  for (int r = 0; r < n; r++) {
-    (void)hipSetDevice(m->dev[r]);
-    if (hipStreamSynchronize(m->st[r]) != hipSuccess) return HOH_E_HIP;
-  }
-  return HOH_OK;
+  return drain(m, HOH_OK);
 }
 
 int hoh_mgpu_decode_image(hoh_mgpu* m, const uint8_t* d_hoh, size_t size, uint8_t* h_rgb, size_t cap, int* Wp,
@@ -259,7 +266,9 @@ int hoh_mgpu_decode_image(hoh_mgpu* m, const uint8_t* d_hoh, size_t size, uint8_
   };
   uint64_t v;
   if (!rv(v) || !rv(v) || p + 2 > tcap) return HOH_E_CORRUPT;              // W-1, H-1
-  p += 2;                                                                // x_tiles-1, y_tiles-1
+  // x_tiles-1, y_tiles-1 must be the tiling of W x H (as decode_image_impl checks)
+  if (xt != txt || yt != tyt || tb[p] != txt - 1 || tb[p + 1] != tyt - 1) return HOH_E_CORRUPT;
+  p += 2;
   std::vector<uint64_t> tsz(ntiles);
   uint64_t sum = 0;
   for (int i = 0; i + 1 < ntiles; i++) {
@@ -295,13 +304,13 @@ int hoh_mgpu_decode_image(hoh_mgpu* m, const uint8_t* d_hoh, size_t size, uint8_
       rr = g_rccl.send(d_hoh + boff[r], bsz[r], ncclUint8, r, m->comm[0], m->st[0]);
       if (rr == ncclSuccess) rr = g_rccl.recv(m->blob[r].p, bsz[r], ncclUint8, 0, m->comm[r], m->st[r]);
     }
-    if (g_rccl.group_end() != ncclSuccess || rr != ncclSuccess) return HOH_E_HIP;
+    if (g_rccl.group_end() != ncclSuccess || rr != ncclSuccess) return drain(m, HOH_E_HIP);
   } else {
     (void)hipSetDevice(m->dev[0]);
     for (int r = 1; r < n; r++)
       if (bsz[r] && hipMemcpyPeerAsync(m->blob[r].p, m->dev[r], d_hoh + boff[r], m->dev[0], bsz[r], m->st[0]) != hipSuccess)
-        return HOH_E_HIP;
-    if (hipStreamSynchronize(m->st[0]) != hipSuccess) return HOH_E_HIP;
+        return drain(m, HOH_E_HIP);
+    if (hipStreamSynchronize(m->st[0]) != hipSuccess) return drain(m, HOH_E_HIP);
   }
   auto work = [&](int r) {
     (void)hipSetDevice(m->dev[r]);
@@ -324,7 +333,7 @@ int hoh_mgpu_decode_image(hoh_mgpu* m, const uint8_t* d_hoh, size_t size, uint8_
     work(0);
     for (auto& t : thr) t.join();
   }
-  for (int r = 0; r < n; r++) if (err[r]) return err[r];
+  for (int r = 0; r < n; r++) if (err[r]) return drain(m, err[r]);
   return HOH_OK;
 }
 

@@ -197,36 +197,55 @@ __global__ __launch_bounds__(64) void k_lz(EncodeJob j) {
 // the three residual planes (four with the indexed plane; order kept) and their histograms.
 // One 256-thread workgroup per tile; the nuke bitmap is built in LDS from the match list, then the plane is walked in
 // 256-pixel blocks with a block-wide rank of the kept pixels.
-__device__ __forceinline__ void nuke_tile(const EncodeJob& j, int t, uint32_t* nk_bits, uint32_t* wsum);
+__device__ __forceinline__ void nuke_tile(const EncodeJob& j, int t, uint32_t* nk_bits, uint32_t* wsum, bool in_lds);
+
+// nuke bitmap + removed-count histograms in LDS need (npix_cap/32 + 1 + slots*512) words; a
+// single tile too large for that (untiled images over ~1.1 M px: the LDS holds 160 KB) takes the
+// same walk with the match list searched per pixel and the counts subtracted in global memory.
+__host__ __device__ static inline int nuke_slots(const EncodeJob& j) { return j.speed ? 2 * HOH_NPLANE_S : 4; }
+#define NK_LDS_MAX (160 * 1024 - 256)
 
 // A small grid strides over the tiles (most have no match): a launch over every tile dispatches
 // ~1000 idle workgroups, which waits for free CUs when other images are in flight.
-#define NK_HIST (2 * HOH_NPLANE_S * 512)
-__global__ __launch_bounds__(256) void k_nuke(EncodeJob j) {
-  extern __shared__ uint32_t nk_bits[];                  // npix_cap / 32 words, then NK_HIST counts
+__global__ __launch_bounds__(256) void k_nuke(EncodeJob j, int in_lds) {
+  extern __shared__ uint32_t nk_bits[];                  // npix_cap / 32 words, then the counts
   __shared__ uint32_t wsum[4];
-  for (int t = blockIdx.x; t < j.ntiles; t += gridDim.x) nuke_tile(j, t, nk_bits, wsum);
+  for (int t = blockIdx.x; t < j.ntiles; t += gridDim.x) nuke_tile(j, t, nk_bits, wsum, in_lds != 0);
 }
 
-__device__ __forceinline__ void nuke_tile(const EncodeJob& j, int t, uint32_t* nk_bits, uint32_t* wsum) {
+// matches are disjoint and in increasing position order (the greedy scan of k_lz / k_lzscan):
+// p is covered iff the last match starting at or before p reaches past it
+__device__ __forceinline__ bool nuked_search(const uint32_t* mt, uint32_t nm, uint32_t p) {
+  uint32_t lo = 0, hi = nm;                              // first match with start > p
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (mt[3 * mid] <= p) lo = mid + 1; else hi = mid;
+  }
+  return lo > 0 && p < mt[3 * (lo - 1)] + mt[3 * (lo - 1) + 1];
+}
+
+__device__ __forceinline__ void nuke_tile(const EncodeJob& j, int t, uint32_t* nk_bits, uint32_t* wsum,
+                                          bool in_lds) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const TileInfo ti = j.tiles[t];
   const uint32_t nm = ti.nmatch;
   if (nm == 0 || (ti.flags & TF_OVERFLOW) || nm > j.lz_cap) return;
   const uint32_t npix = (uint32_t)ti.w * ti.h, nwords = (npix + 31) / 32;
   const uint32_t* mt = j.matches + (size_t)t * 3 * (j.lz_cap + 1);
+  const int nslots = nuke_slots(j);
   uint32_t* nh = nk_bits + j.npix_cap / 32 + 1;          // removed counts, [slot][512]
-  for (uint32_t i = tid; i < nwords; i += 256) nk_bits[i] = 0;
-  for (uint32_t i = tid; i < NK_HIST; i += 256) nh[i] = 0;
-  __syncthreads();
-  // one thread per match (matches are disjoint): natural tiles hold thousands of short copies
-  for (uint32_t m = tid; m < nm; m += 256) {
-    const uint32_t a = mt[3 * m], e = a + mt[3 * m + 1];
-    for (uint32_t p = a; p < e; p++) atomicOr(&nk_bits[p >> 5], 1u << (p & 31));
+  if (in_lds) {
+    for (uint32_t i = tid; i < nwords; i += 256) nk_bits[i] = 0;
+    for (uint32_t i = tid; i < (uint32_t)nslots * 512; i += 256) nh[i] = 0;
+    __syncthreads();
+    // one thread per match (matches are disjoint): natural tiles hold thousands of short copies
+    for (uint32_t m = tid; m < nm; m += 256) {
+      const uint32_t a = mt[3 * m], e = a + mt[3 * m + 1];
+      for (uint32_t p = a; p < e; p++) atomicOr(&nk_bits[p >> 5], 1u << (p & 31));
+    }
+    __syncthreads();
   }
-  __syncthreads();
   const bool grey = ti.flags & TF_GREY, pal = !grey && (ti.flags & TF_PALETTE_CAND);
-  const int nslots = j.speed ? 2 * HOH_NPLANE_S : 4;
   // plane slots: -s0 the MED planes G R' B' (+ indexed); -s>=1 the six MED planes, then the six
   // searched planes, each with its stream's histogram.  The kept pixels' ranks are the same in
   // every plane, so each 256-pixel block ranks once and moves all present planes.
@@ -254,10 +273,14 @@ __device__ __forceinline__ void nuke_tile(const EncodeJob& j, int t, uint32_t* n
     uint16_t v[2 * HOH_NPLANE_S];
 #pragma unroll
     for (int k = 0; k < 2 * HOH_NPLANE_S; k++) v[k] = (k < np && valid) ? r[k][p] : 0;
-    const bool nuked = valid && ((nk_bits[p >> 5] >> (p & 31)) & 1);
+    const bool nuked = valid && (in_lds ? ((nk_bits[p >> 5] >> (p & 31)) & 1) : nuked_search(mt, nm, p));
     if (nuked) {                                        // counted in LDS, applied once below
 #pragma unroll
-      for (int k = 0; k < 2 * HOH_NPLANE_S; k++) if (k < np) atomicAdd(&nh[k * 512 + v[k]], 1u);
+      for (int k = 0; k < 2 * HOH_NPLANE_S; k++)
+        if (k < np) {
+          if (in_lds) atomicAdd(&nh[k * 512 + v[k]], 1u);
+          else atomicSub(&hk[k][v[k]], 1u);
+        }
     }
     const bool keep = valid && !nuked;
     const uint64_t bal = __ballot(keep);
@@ -276,11 +299,13 @@ __device__ __forceinline__ void nuke_tile(const EncodeJob& j, int t, uint32_t* n
     outc += tot;
   }
   __syncthreads();
+  if (in_lds) {
 #pragma unroll
-  for (int k = 0; k < 2 * HOH_NPLANE_S; k++)
-    if (k < np)
-      for (uint32_t i = tid; i < 512; i += 256)
-        if (nh[k * 512 + i]) hk[k][i] -= nh[k * 512 + i];    // this tile's histograms: one writer
+    for (int k = 0; k < 2 * HOH_NPLANE_S; k++)
+      if (k < np)
+        for (uint32_t i = tid; i < 512; i += 256)
+          if (nh[k * 512 + i]) hk[k][i] -= nh[k * 512 + i];  // this tile's histograms: one writer
+  }
   __syncthreads();
 }
 
@@ -290,5 +315,7 @@ void launch_lz(const EncodeJob& j, hipStream_t s) {
 
 void launch_nuke(const EncodeJob& j, hipStream_t s) {
   // one workgroup per tile (natural images: most tiles have copies); tiles without copies leave
-  hipLaunchKernelGGL(k_nuke, dim3(j.ntiles), dim3(256), (size_t)(j.npix_cap / 32 + 1 + NK_HIST) * 4, s, j);
+  const size_t lds = ((size_t)j.npix_cap / 32 + 1 + (size_t)nuke_slots(j) * 512) * 4;
+  const bool in_lds = lds <= NK_LDS_MAX;
+  hipLaunchKernelGGL(k_nuke, dim3(j.ntiles), dim3(256), in_lds ? lds : 0, s, j, (int)in_lds);
 }

@@ -155,7 +155,8 @@ int hoh_tiling(int W, int H, int* x_tiles, int* y_tiles, int* tile_w, int* tile_
 /* One process drives ndev GPUs: a context and a HIP stream per device and, when the devices are
  * distinct, one RCCL communicator each (ncclCommInitAll; librccl.so is loaded here, not at link
  * time).  A device may be listed more than once (several shards on one GPU): the blobs then move
- * by device copies instead of RCCL (hoh_mgpu_transport returns 0; 1 = RCCL). */
+ * by device copies instead of RCCL (hoh_mgpu_transport returns 0; 1 = RCCL).  Distinct devices
+ * fall back to the same peer copies when librccl cannot be loaded or ncclCommInitAll fails. */
 typedef struct hoh_mgpu hoh_mgpu;
 int hoh_mgpu_create(hoh_mgpu** m, int ndev, const int* devices);
 void hoh_mgpu_destroy(hoh_mgpu* m);

@@ -50,3 +50,20 @@ def test_sizes_parity_and_roundtrip(hoh, orc, W, H, noise):
             assert e.code == 6, e
             return
         assert np.array_equal(out.reshape(H, W, 3), img)
+
+
+LARGE_UNTILED = [(5000, 250, 0), (5000, 250, 1), (12000, 200, 0)]
+
+
+@pytest.mark.parametrize("W,H,speed", LARGE_UNTILED, ids=["%dx%d-s%d" % s for s in LARGE_UNTILED])
+def test_large_untiled_parity(hoh, orc, W, H, speed):
+    """Untiled images (H < 256) are one tile of W*H pixels: k_nuke's bitmap + count histograms
+    no longer fit the 160 KB LDS above ~1.1 M px and take the global-memory walk
+    (k_lz.hip nuke_tile).  Natural statistics, so most of the tile is LZ copies.  The file is
+    header-only (Q13); the printed size carries the whole encode."""
+    from hoh_ans.natural import natural_rgb
+    img = natural_rgb(W, H, 5)
+    ref, ref_printed = orc.choh(img, speed)
+    data, printed = hoh.choh(img, speed=speed)
+    assert printed == ref_printed
+    assert data == ref

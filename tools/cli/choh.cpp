@@ -49,13 +49,14 @@ int main(int argc, char** argv) {
   const size_t raw = (size_t)W * H * 3;
   if (in.size() < raw) { std::printf("input shorter than width*height*3\n"); return 3; }
   hoh_ctx* ctx = nullptr;
+  const int dev0 = devices.empty() ? 0 : devices[0];   // --devices 3 / one entry: that GPU
   hoh_mgpu* mg = nullptr;
-  int r = devices.size() > 1 ? hoh_mgpu_create(&mg, (int)devices.size(), devices.data()) : hoh_ctx_create(&ctx, 0);
+  int r = devices.size() > 1 ? hoh_mgpu_create(&mg, (int)devices.size(), devices.data()) : hoh_ctx_create(&ctx, dev0);
   if (r != HOH_OK) { std::fprintf(stderr, "choh: %s\n", hoh_strerror(r)); return r; }
   const size_t cap = hoh_encode_bound(W, H);
   uint8_t *d_in = nullptr, *d_out = nullptr;
+  (void)hipSetDevice(dev0);
   if (!mg && hipMalloc(&d_in, raw) != hipSuccess) return HOH_E_HIP;
-  if (mg) (void)hipSetDevice(devices[0]);
   if (hipMalloc(&d_out, cap) != hipSuccess) return HOH_E_HIP;
   if (!mg && hipMemcpy(d_in, in.data(), raw, hipMemcpyHostToDevice) != hipSuccess) return HOH_E_HIP;
   size_t n = 0, printed = 0;

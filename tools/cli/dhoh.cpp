@@ -41,12 +41,13 @@ int main(int argc, char** argv) {
   if (r != HOH_OK) { std::fprintf(stderr, "dhoh: %s\n", hoh_strerror(r)); return r; }
   std::printf("width: %d\nheight: %d\n", W, H);
   hoh_ctx* ctx = nullptr;
+  const int dev0 = devices.empty() ? 0 : devices[0];   // --devices 3 / one entry: that GPU
   hoh_mgpu* mg = nullptr;
-  r = devices.size() > 1 ? hoh_mgpu_create(&mg, (int)devices.size(), devices.data()) : hoh_ctx_create(&ctx, 0);
+  r = devices.size() > 1 ? hoh_mgpu_create(&mg, (int)devices.size(), devices.data()) : hoh_ctx_create(&ctx, dev0);
   if (r != HOH_OK) { std::fprintf(stderr, "dhoh: %s\n", hoh_strerror(r)); return r; }
   const size_t raw = (size_t)W * H * 3;
   uint8_t *d_in = nullptr, *d_rgb = nullptr;
-  if (mg) (void)hipSetDevice(devices[0]);
+  (void)hipSetDevice(dev0);
   if (hipMalloc(&d_in, in.size()) != hipSuccess || (!mg && hipMalloc(&d_rgb, raw) != hipSuccess)) return HOH_E_HIP;
   if (hipMemcpy(d_in, in.data(), in.size(), hipMemcpyHostToDevice) != hipSuccess) return HOH_E_HIP;
   std::vector<uint8_t> out(raw);
