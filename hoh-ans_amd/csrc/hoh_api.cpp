@@ -59,6 +59,7 @@ struct Scratch {                // see ScratchFrame (hoh_dec.h)
 
 struct hoh_ctx {
   int device = 0;
+  int cus = 256;                // compute units of the device
   Scratch scr;
   hipStream_t own = nullptr;
   Buf idx8, fpb, pinfo, lg;     // -s>=1 workspaces
@@ -152,6 +153,8 @@ int hoh_ctx_create(hoh_ctx** out, int device) {
   if (hipSetDevice(device) != hipSuccess) return HOH_E_NODEV;
   hoh_ctx* c = new hoh_ctx();
   c->device = device;
+  if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || c->cus <= 0)
+    c->cus = 256;
   if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) { delete c; return HOH_E_HIP; }
   if (hipHostMalloc((void**)&c->pinned, 4096) != hipSuccess) { delete c; return HOH_E_HIP; }
   *out = c;
@@ -317,6 +320,10 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   int xt, yt, tw, th;
   hoh_tiling(W, H, &xt, &yt, &tw, &th);
   if (tw > HOH_MAX_TILE_W || (size_t)tw * th > (1u << 24)) return HOH_E_UNSUPPORTED;
+  // -s>=1: k_search keeps a tile's 40-px predictor grid (HOH_MAPCAP cells) in LDS and writes a
+  // row's residuals four per thread; tiles are < 512 on a side, so only untiled images (one side
+  // under 256, the other wider than ~1000) exceed either
+  if (speed && ((size_t)((tw + 39) / 40) * ((th + 39) / 40) > HOH_MAPCAP || tw > 1024)) return HOH_E_UNSUPPORTED;
   if (t0 < 0 || ntiles <= 0 || t0 + ntiles > xt * yt) return HOH_E_ARG;
   Prof prof(c, s, async);
   EncodeJob j;
@@ -746,4 +753,5 @@ DecWork& ctx_dec(hoh_ctx* c) { return c->dec; }
 hipStream_t ctx_stream(hoh_ctx* c, void* s) { return pick(c, s); }
 uint64_t* ctx_pinned(hoh_ctx* c) { return c->pinned; }
 int ctx_device(hoh_ctx* c) { return c->device; }
+int ctx_cus(hoh_ctx* c) { return c->cus; }
 void ctx_mark(hoh_ctx* c, hipStream_t s, const char* name, bool reset) { prof_mark(c, s, name, reset); }

@@ -791,14 +791,20 @@ __device__ bool lane_decode(const DecJob& j, const DecStream& d, const uint32_t*
   return lane != 0 || (!s_bad && x == (1ull << 31));
 }
 
+// streams k_drans_multi decodes (a chain lane each)
+__device__ __forceinline__ bool multi_ok(const DecStream& d) {
+  return d.mode == SM_RANS && d.range <= 512 && d.pb <= 15 && d.pb >= 7;
+}
+
 // Without an index: one wave per stream (lane_decode); streams outside its table format
 // (range > 512 or prob_bits > 15, never in a -s0 file) fall back to one lane with global tables.
-__global__ __launch_bounds__(64) void k_drans_wave(DecJob j, int nstreams) {
+// With skip_multi the streams k_drans_multi takes are left to it.
+__global__ __launch_bounds__(64) void k_drans_wave(DecJob j, int nstreams, int skip_multi) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dl_lds[];
   if (dec_abort(j)) return;
   const int sid = blockIdx.x;
   const DecStream d = j.streams[sid];
-  if (d.mode != SM_RANS) return;
+  if (d.mode != SM_RANS || (skip_multi && multi_ok(d))) return;
   uint16_t* out = j.dsym + d.out_off;
   if (d.range <= 512 && d.pb <= 15) {
     if (!lane_decode(j, d, j.cum + (size_t)sid * j.cum_stride, out, dl_lds)) atomicOr(j.gerr, 4u);
@@ -811,6 +817,238 @@ __global__ __launch_bounds__(64) void k_drans_wave(DecJob j, int nstreams) {
   if (!dec_run<false>(j, d, j.cum + (size_t)sid * j.cum_stride, j.bsym + (size_t)sid * 512, d.pb > 9 ? d.pb - 9 : 0,
                       nullptr, x, d.payload_off + 8, wend, 0, d.n, OutCursor(out, 0, 0), &xe) || xe != (1ull << 31))
     atomicOr(j.gerr, 4u);
+}
+
+// ---------------------------------------------------------------- no index: many streams per wave
+// A foreign .hoh (no side index) leaves one serial chain per stream (rans64.hpp:107-142,
+// entropy_decoding.hpp:268-276).  k_drans_wave gives each stream a wave of its own and walks it on
+// lane 0 (3,072 waves for an 8192^2 image, ~700 cycles per symbol with three of them per SIMD);
+// k_drans_multi gives each chain a LANE: one wave decodes MS streams side by side, every chain
+// lane with its own lookup tables in LDS (DrTables, 12 KB) and a 16-word payload ring refilled a
+// 16-symbol group ahead exactly as k_drans's segment lanes do, so a step is dstep's ~17 VALU and
+// two dependent LDS reads, and 64 decoded symbols leave the lane as one 128-B line (flat) or
+// eight 16-B blocks (blocked layout).  Streams k_drans_multi takes: rANS, range <= 512,
+// 7 <= prob_bits <= 15 (every plane and LZ stream choh writes); k_dmlist lists them.
+// LDS map (byte addresses; no static LDS, so the dynamic area starts at 0): payload rings
+// [0, 4 KB) (slot s of lane l at s * 256 + 4 l), the abort / count words at 4 KB, bucket table of
+// chain m at 8 KB (m + 1) (8 KB aligned: its address is an OR), symbol table of chain m at
+// 8 KB (MS + 1) + 4 KB m.
+__host__ __device__ constexpr uint32_t dm_bk(int m) { return 8192u * (uint32_t)(m + 1); }
+__host__ __device__ constexpr uint32_t dm_sy(int ms, int m) { return 8192u * (uint32_t)(ms + 1) + 4096u * (uint32_t)m; }
+__host__ __device__ constexpr uint32_t dm_smem(int ms) { return dm_sy(ms, ms); }
+#define DM_SCR 4096u
+#define DM_MS 12
+
+// the streams k_drans_multi decodes; the others stay with k_drans_wave.  Long streams
+// (>= DM_LONG symbols: whole tile planes) are listed from the front (count in gerr[5]), short ones
+// (LZ streams, compacted planes) from the back (count in gerr[6]), so the first rounds of
+// k_drans_multi hold streams of similar length.
+#define DM_LONG 16384
+__global__ __launch_bounds__(256) void k_dmlist(DecJob j, int nstreams, uint32_t* list) {
+  if (dec_abort(j)) return;
+  const int s = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63;
+  bool ok = false, lng = false;
+  if (s < nstreams) {
+    const DecStream d = j.streams[s];
+    ok = multi_ok(d);
+    lng = ok && d.n >= DM_LONG;
+  }
+  const uint64_t bl = __ballot(lng), bs = __ballot(ok && !lng), below = (1ull << lane) - 1;
+  uint32_t base_l = 0, base_s = 0;
+  if (lane == 0 && bl) base_l = atomicAdd(j.gerr + 5, (uint32_t)__popcll(bl));
+  if (lane == 0 && bs) base_s = atomicAdd(j.gerr + 6, (uint32_t)__popcll(bs));
+  base_l = __shfl(base_l, 0);
+  base_s = __shfl(base_s, 0);
+  if (lng) list[base_l + __popcll(bl & below)] = (uint32_t)s;
+  else if (ok) list[nstreams - 1 - (base_s + __popcll(bs & below))] = (uint32_t)s;
+}
+
+// one decode step on chain lane tables at (bk, sy): dstep with the tables' bases ORed in
+__device__ __forceinline__ uint32_t dstep_m(uint32_t bk, uint32_t sy, uint32_t bmask, uint32_t mask, uint32_t pb,
+                                            uint32_t& xh, uint32_t& xl, uint32_t nw, uint32_t& wi) {
+  const uint32_t slot = xl & mask;
+  const uint2 e = lds_u2(((xl >> 2) & bmask) | bk);
+  const uint32_t k = __popc(__builtin_amdgcn_ubfe(e.x, 1, slot)) + e.y;
+  const uint2 t = lds_u2((k << 3) | sy);
+  const uint32_t d = slot - (t.y & 0xffffu);
+  const uint32_t yl = __builtin_amdgcn_alignbit(xh, xl, pb);
+  const uint64_t acc = ((uint64_t)__umul24(t.x, xh >> pb) << 32) | d;
+  uint64_t x, co;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(x), "=s"(co) : "v"(t.x), "v"(yl), "v"(acc));
+  const uint32_t nh = (uint32_t)(x >> 32), nl = (uint32_t)x;
+  const bool r = x < (1ull << 31);
+  xh = r ? nl : nh;
+  xl = r ? nw : nl;
+  wi += r;
+  return t.y;
+}
+
+// One chain lane: the whole stream d with its tables at LDS bytes (bkb, syb) and its payload
+// ring in slots t4 + 256 s.  Payload words are fetched as raw dwords one 16-symbol group ahead and
+// aligned when they land in the ring (aligning at the fetch made every fetch wait for its load).
+__device__ __forceinline__ bool dm_chain(const DecJob& j, const DecStream& d, uint32_t* dm_lds, uint32_t bkb,
+                                      uint32_t syb) {
+  const uint32_t t4 = (uint32_t)threadIdx.x * 4;
+  uint16_t* out = j.dsym + d.out_off;
+  const uint32_t pb = d.pb, mask = (1u << pb) - 1, bmask = (mask >> 2) & ~7u;
+  const uint64_t P = d.payload_off;
+  const uint32_t al = (uint32_t)(P & 3);
+  const uint64_t szal = j.size & ~3ull;
+  uint32_t tailw = 0;
+  for (uint64_t q = szal; q < j.size; q++) tailw |= (uint32_t)j.in[q] << (8 * (q & 3));
+  auto fetch5 = [&](uint32_t kw, uint32_t* A) {              // raw dwords covering words kw .. kw+3
+    const uint64_t a = (P & ~3ull) + (uint64_t)kw * 4;
+    if (a + 20 <= szal) {
+      typedef uint32_t u4a __attribute__((ext_vector_type(4), aligned(4)));
+      const u4a v = *(const u4a*)(j.in + a);
+      A[0] = v.x; A[1] = v.y; A[2] = v.z; A[3] = v.w;
+      A[4] = *(const uint32_t*)(j.in + a + 16);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 5; e++) {
+        const uint64_t b = a + 4 * e;
+        A[e] = b + 4 <= szal ? *(const uint32_t*)(j.in + b) : (b == szal ? tailw : 0u);
+      }
+    }
+  };
+  auto put4 = [&](uint32_t kw, const uint32_t* A) {
+#pragma unroll
+    for (int e = 0; e < 4; e++)
+      lds_st32(t4 | (((kw + e) & (DR_RW - 1)) << 8), __builtin_amdgcn_alignbyte(A[e + 1], A[e], al));
+  };
+  uint32_t wi = 2, xh, xl;
+  {
+    uint32_t A[5];
+    fetch5(0, A);
+    xl = __builtin_amdgcn_alignbyte(A[1], A[0], al);
+    xh = __builtin_amdgcn_alignbyte(A[2], A[1], al);         // Rans64DecInit
+  }
+  const uint32_t ngrp = pb >= 7 ? d.n >> 6 : 0;
+  if (ngrp) {
+    uint32_t fill = wi, pend[5];
+    bool hp = true;                                          // pend holds words fill .. fill+3
+    {
+      uint32_t a0[5], a1[5];
+      fetch5(fill, a0); fetch5(fill + 4, a1);
+      put4(fill, a0); put4(fill + 4, a1);
+      fill += 8;
+      fetch5(fill, pend);
+    }
+    for (uint32_t g = 0; g < ngrp; g++) {
+      uint32_t pk[32];                                       // 64 symbols: one 128-B line
+#pragma unroll
+      for (int gi = 0; gi < 4; gi++) {
+        if (hp) { put4(fill, pend); fill += 4; }
+        while (fill - wi < 8) {
+          uint32_t t[5];
+          fetch5(fill, t); put4(fill, t); fill += 4;
+        }
+        hp = fill + 4 - wi <= DR_RW;
+        if (hp) fetch5(fill, pend);
+#pragma unroll
+        for (int u = 0; u < 16; u += 2) {
+          const uint32_t w0 = lds_u32(t4 | ((wi & (DR_RW - 1)) << 8));
+          const uint32_t a = dstep_m(bkb, syb, bmask, mask, pb, xh, xl, w0, wi);
+          const uint32_t w1 = lds_u32(t4 | ((wi & (DR_RW - 1)) << 8));
+          const uint32_t b = dstep_m(bkb, syb, bmask, mask, pb, xh, xl, w1, wi);
+          pk[gi * 8 + u / 2] = __builtin_amdgcn_perm(b, a, 0x07060302u);
+        }
+      }
+      uint4* o4;
+      uint32_t ostride;
+      if (d.blk) {                                           // row r = g / 4, columns 64 (g % 4) ..
+        const uint32_t r = g >> 2, rr = r & 63;
+        o4 = (uint4*)(out + (r >> 6) * BLK_BAND) + rr + ((rr + 7) >> 3) * 64 + (g & 3) * 8 * 64;
+        ostride = 64;
+      } else {
+        o4 = (uint4*)(out + (size_t)g * 64);
+        ostride = 1;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; e++) o4[e * ostride] = make_uint4(pk[4 * e], pk[4 * e + 1], pk[4 * e + 2], pk[4 * e + 3]);
+    }
+  }
+  // the last n % 64 symbols (or a whole stream with prob_bits < 7): one step at a time, payload
+  // words from the file
+  DrTables tb;
+  tb.bk = (uint2*)((unsigned char*)dm_lds + bkb);
+  tb.sy = (uint2*)((unsigned char*)dm_lds + syb);
+  uint64_t x = ((uint64_t)xh << 32) | xl;
+  OutCursor oc(out, d.blk, 0);
+  for (uint32_t i = ngrp * 64; i < d.n; i++) {
+    const uint32_t slot = (uint32_t)x & mask;
+    uint32_t sym, c, f;
+    tb.lookup(slot, sym, c, f);
+    oc.put(i, (uint16_t)sym);
+    x = (uint64_t)f * (x >> pb) + (slot - c);                // Rans64DecAdvance
+    if (x < (1ull << 31)) {
+      if (wi >= d.words) return false;
+      x = (x << 32) | ld_u32_unaligned(j.in, P + (uint64_t)wi * 4);
+      wi++;
+    }
+  }
+  return x == (1ull << 31) && wi <= d.words;
+}
+
+template <int MS>
+__global__ __launch_bounds__(64) void k_drans_multi(DecJob j, const uint32_t* list, int nlist) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t dm_lds[];
+  const int lane = threadIdx.x;
+  uint32_t* scr = dm_lds + DM_SCR / 4;
+  if (lane == 0) {
+    scr[0] = *(volatile const uint32_t*)j.gerr;
+    scr[1] = *(volatile const uint32_t*)(j.gerr + 5);
+    scr[2] = *(volatile const uint32_t*)(j.gerr + 6);
+  }
+  __syncthreads();
+  if (scr[0]) return;
+  const uint32_t cl = scr[1], total = scr[1] + scr[2];
+  // logical entry i: long streams from the front of the list, short ones from its back
+  auto entry = [&](uint32_t i) -> uint32_t { return i < cl ? list[i] : list[nlist - 1 - (i - cl)]; };
+  for (uint32_t base = blockIdx.x * MS; base < total; base += gridDim.x * MS) {
+    const int ns = (int)min((uint32_t)MS, total - base);
+    // lookup tables of every chain (the lane_decode construction, the whole wave per stream)
+    for (int m = 0; m < ns; m++) {
+      const DecStream d = j.streams[entry(base + m)];
+      const uint32_t nb = ((1u << d.pb) + 31) >> 5;
+      uint2* bk = (uint2*)((unsigned char*)dm_lds + dm_bk(m));
+      for (uint32_t b = lane; b < nb; b += 64) bk[b] = make_uint2(0, 0);
+    }
+    __syncthreads();
+    for (int m = 0; m < ns; m++) {
+      const uint32_t sid = entry(base + m);
+      const DecStream d = j.streams[sid];
+      const uint32_t* cum = j.cum + (size_t)sid * j.cum_stride;
+      uint2* bk = (uint2*)((unsigned char*)dm_lds + dm_bk(m));
+      uint2* sy = (uint2*)((unsigned char*)dm_lds + dm_sy(MS, m));
+      uint32_t pres = 0, cv[9];
+#pragma unroll
+      for (int e = 0; e < 9; e++) cv[e] = 8 * lane + e <= d.range ? cum[8 * lane + e] : 0;
+#pragma unroll
+      for (int e = 0; e < 8; e++)
+        if (8 * lane + e < d.range && cv[e + 1] > cv[e]) pres |= 1u << e;
+      const uint32_t c = __popc(pres);
+      uint32_t incl = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o);
+        if (lane >= o) incl += t;
+      }
+      uint32_t k = incl - c;
+      for (int e = 0; e < 8; e++) {
+        if (!((pres >> e) & 1)) continue;
+        const uint32_t sv = 8 * lane + e, c0 = cv[e], c1 = cv[e + 1];
+        sy[k] = make_uint2(c1 - c0, c0 | (sv << 16));
+        for (uint32_t b = (c0 + 31) >> 5; b <= (c1 - 1) >> 5; b++) bk[b].y = k;
+        if (c0 & 31) atomicOr(&bk[c0 >> 5].x, 1u << (c0 & 31));
+        k++;
+      }
+    }
+    __syncthreads();
+    if (lane < ns && !dm_chain(j, j.streams[entry(base + lane)], dm_lds, dm_bk(lane), dm_sy(MS, lane)))
+      atomicOr(j.gerr, 4u);
+    __syncthreads();                                         // the tables are rebuilt next round
+  }
 }
 
 // stored streams: MSB-first fixed-width fields (the no-index path; with an index k_drans's
@@ -1669,6 +1907,12 @@ int decode_tiles_async_impl(hoh_ctx* c, const uint8_t* d_blob, size_t size, int 
   return decode_run(c, j, idx, s, &as);
 }
 
+// HOH_NOIX_WAVE=1: no-index decodes with k_drans_wave alone (the round-2 decoder, for comparison)
+static int noix_wave() {
+  static const int v = [] { const char* e = getenv("HOH_NOIX_WAVE"); return e ? atoi(e) : 0; }();
+  return v;
+}
+
 static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s, const AsyncDec* as) {
   j.npix_cap = (uint32_t)(((size_t)j.tw * j.th + 63) / 64 * 64);
   j.lz_cap = (uint32_t)((j.npix_cap / 4 + j.npix_cap / 255 + 16 + 7) / 8 * 8);
@@ -1708,8 +1952,19 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   if (indexed) {
     hipLaunchKernelGGL(k_dmatch, dim3((S + 255) / 256), dim3(256), 0, s, j, S);
     hipLaunchKernelGGL(k_drans, dim3(S), dim3(DR_T), DR_SMEM, s, j, S);
+  } else if (noix_wave()) {                                   // the one-wave-per-stream decoder alone
+    hipLaunchKernelGGL(k_drans_wave, dim3(S), dim3(64), DL_SMEM, s, j, S, 0);
   } else {
-    hipLaunchKernelGGL(k_drans_wave, dim3(S), dim3(64), DL_SMEM, s, j, S);
+    // every plane / LZ stream: a chain lane of k_drans_multi; anything else: k_drans_wave
+    void* q2;
+    if ((e = dbuf(w, 13, (size_t)S * 4, &q2))) return e;
+    uint32_t* mlist = (uint32_t*)q2;
+    hipLaunchKernelGGL(k_dmlist, dim3((S + 255) / 256), dim3(256), 0, s, j, S, mlist);
+    // one workgroup per CU (its LDS is a whole CU's), rounds of DM_MS streams per workgroup
+    const int nmax = std::min(S, 6 * j.ntiles);
+    const int grid = std::min((nmax + DM_MS - 1) / DM_MS, ctx_cus(c));
+    hipLaunchKernelGGL(k_drans_multi<DM_MS>, dim3(grid), dim3(64), dm_smem(DM_MS), s, j, (const uint32_t*)mlist, S);
+    hipLaunchKernelGGL(k_drans_wave, dim3(S), dim3(64), DL_SMEM, s, j, S, 1);
   }
   ctx_mark(c, s, "drans", false);
   if (!indexed) hipLaunchKernelGGL(k_dstored, dim3(S), dim3(256), 0, s, j, S);

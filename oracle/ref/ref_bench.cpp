@@ -5,7 +5,9 @@
 // (entropy_decoding.hpp:134, unprediction.hpp:6) -- dhoh itself cannot be timed: it crashes on
 // every tiled file.  Prints one JSON line.  Single thread, like the reference; the
 // optional 5th argument (first tile) lets bench.py run one process per core on disjoint tile
-// ranges for the all-cores leg.
+// ranges for the all-cores leg.  t_enc / t_dec cover encode_tile and the decode calls only: the
+// LZ locate below (find_lz_rgb, which finds where the planes start because the reference's
+// decode_entropy cannot skip a stream) is outside both clocks.
 #include <stdio.h>
 #include <stdlib.h>
 #include <stdint.h>
@@ -25,15 +27,21 @@ int main(int argc, char** argv) {
   if (argc < 5) { fprintf(stderr, "usage: ref_bench in.rgb W H max_tiles [first_tile]\n"); return 1; }
   int W = atoi(argv[2]), H = atoi(argv[3]), maxt = atoi(argv[4]);
   const int first = argc > 5 ? atoi(argv[5]) : 0;
-  FILE* f = fopen(argv[1], "rb");
-  if (!f) return 2;
-  size_t sz = (size_t)W * H * 3;
-  uint8_t* img = new uint8_t[sz];
-  if (fread(img, 1, sz, f) != sz) return 2;
-  fclose(f);
   int xt = W / 256, yt = H / 256, tw = (W + xt - 1) / xt, th = (H + yt - 1) / yt;
   int nt = xt * yt - first < maxt ? xt * yt - first : maxt;
   if (nt < 0) nt = 0;
+  // only the rows of this process's tiles are read (one process per core holds a band, not the
+  // whole image)
+  FILE* f = fopen(argv[1], "rb");
+  if (!f) return 2;
+  const int r0 = nt ? (first / xt) * th : 0;
+  const int r1 = nt ? ((first + nt - 1) / xt + 1) * th < H ? ((first + nt - 1) / xt + 1) * th : H : 0;
+  const size_t rowb = (size_t)W * 3;
+  uint8_t* band = new uint8_t[(size_t)(r1 - r0) * rowb + 1];
+  if (fseek(f, (long)((size_t)r0 * rowb), SEEK_SET) != 0) return 2;
+  if (fread(band, 1, (size_t)(r1 - r0) * rowb, f) != (size_t)(r1 - r0) * rowb) return 2;
+  fclose(f);
+  uint8_t* img = band - (size_t)r0 * rowb;          // indexed by absolute row below
   int saved = dup(1); int dn = open("/dev/null", O_WRONLY);
   double tenc = 0, tdec = 0;
   size_t raw = 0, comp = 0;

@@ -52,7 +52,7 @@ def test_sizes_parity_and_roundtrip(hoh, orc, W, H, noise):
         assert np.array_equal(out.reshape(H, W, 3), img)
 
 
-LARGE_UNTILED = [(5000, 250, 0), (5000, 250, 1), (12000, 200, 0)]
+LARGE_UNTILED = [(5000, 250, 0), (12000, 200, 0), (1000, 200, 1)]
 
 
 @pytest.mark.parametrize("W,H,speed", LARGE_UNTILED, ids=["%dx%d-s%d" % s for s in LARGE_UNTILED])
@@ -67,3 +67,12 @@ def test_large_untiled_parity(hoh, orc, W, H, speed):
     data, printed = hoh.choh(img, speed=speed)
     assert printed == ref_printed
     assert data == ref
+
+
+def test_untiled_search_grid_limit(hoh):
+    """-s>=1 on an untiled image whose 40-px predictor grid exceeds the search kernel's LDS map
+    (HOH_MAPCAP cells): refused with HOH_E_UNSUPPORTED, never a corrupt map."""
+    from hoh_ans.natural import natural_rgb
+    with pytest.raises(hoh.HohError) as e:
+        hoh.choh(natural_rgb(1500, 200, 5), speed=1)
+    assert e.value.code == 6
