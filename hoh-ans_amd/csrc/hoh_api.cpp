@@ -585,9 +585,10 @@ int encode_streams_impl(hoh_ctx* c, const uint16_t* d_syms, const uint64_t* off,
   if ((e = ensure(c->tab_gen, (size_t)nstreams * range * sizeof(EncGen)))) return e;
   if ((e = ensure(c->slabs, (size_t)nstreams * slab * 4))) return e;
   if ((e = ensure(c->misc, 64))) return e;
-  // prob_bits 15 with range <= 512 (every -s0 plane, config 2's single stream) takes the tuned
-  // chain k_rans_fast, the rest the reference reciprocal step (k_rans_gen)
-  const bool fast = pb == 15 && range <= HOH_FAST_RANGE;
+  // prob_bits 12..19 with range <= 512 (every -s0 plane, config 2's single stream, the -s>=1
+  // ladder) takes the tuned chain k_rans_fast (k_tables may still hand a stream back), the rest
+  // the reference reciprocal step (k_rans_gen)
+  const bool fast = pb >= 12 && pb <= 19 && range <= HOH_FAST_RANGE;
   if (fast && (e = ensure(c->tab_fast, (size_t)nstreams * HOH_FAST_RANGE * sizeof(EncFast)))) return e;
   std::vector<StreamInfo> st((size_t)nstreams);
   for (int i = 0; i < nstreams; i++) {
@@ -622,7 +623,7 @@ int encode_streams_impl(hoh_ctx* c, const uint16_t* d_syms, const uint64_t* off,
   if (hipMemcpyAsync(c->streams.p, st.data(), st.size() * sizeof(StreamInfo), hipMemcpyHostToDevice, s) != hipSuccess) return HOH_E_HIP;
   if (hipMemsetAsync(c->misc.p, 0, 64, s) != hipSuccess) return HOH_E_HIP;
   launch_tables(j, nstreams, s);
-  if (fast) launch_rans_fast(j, nstreams, s, SidMap{0, 0}, nstreams, SidMap{0, 0});
+  if (fast) launch_rans_fast(j, nstreams, s, SidMap{0, 0}, nstreams, SidMap{0, 0}, pb == 15 ? 0 : 1);
   launch_rans_gen(j, nstreams, s);            // skips the streams k_rans_fast coded
   launch_finalize(j, nstreams, s);
   launch_streambytes(j, nstreams, s);

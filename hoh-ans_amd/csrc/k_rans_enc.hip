@@ -113,6 +113,57 @@ __device__ __forceinline__ void step15(Coder& c, const EncFast& e) {
   c.slot++;
 }
 
+// Any prob_bits 12..19 (the -s>=1 ladder, layer_encode.hpp:326-391): the same quotients with
+// x_max = f << (63 - pb) tested as x_hi >= f << (31 - pb) (exact: f << (31 - pb) <= 2^31), the
+// low word nl + c + ql * (2^pb - f) and the high word (q * 2^pb) >> 32 = alignbit(qh, ql, 32 - pb).
+// Exactness of the f64 floors needs the numerators (< f * 2^32) times the 2.5-ulp relative error
+// of 1/f to stay below 1: f <= 2^18 (k_tables sends pb-19 streams with a larger f to k_rans_gen).
+// Size-only encodes (SO: the ladder's trial streams) only count the emitted words.
+struct PbShape {
+  uint32_t sh, M, a32;       // 31 - pb, 2^pb, 32 - pb
+};
+
+template <bool SO>
+__device__ __forceinline__ void stepg(Coder& c, const EncFast& e, const PbShape& g) {
+  if (!SO) c.win[c.slot] = c.xl;
+  const uint32_t f = e.f, fs = f << g.sh;
+  uint32_t nh, nl;
+  uint64_t co;
+  if (SO) {
+    asm("v_cmp_ge_u32_e32 vcc, %[xh], %[fs]\n\t"
+        "v_addc_co_u32_e64 %[m], %[co], %[m], 0, vcc\n\t"
+        "v_cndmask_b32_e64 %[nh], %[xh], 0, vcc\n\t"
+        "v_cndmask_b32_e32 %[nl], %[xl], %[xh], vcc"
+        : [nh] "=&v"(nh), [nl] "=&v"(nl), [m] "+v"(c.mask), [co] "=&s"(co)
+        : [xh] "v"(c.xh), [xl] "v"(c.xl), [fs] "v"(fs)
+        : "vcc");
+  } else {
+    asm("v_cmp_ge_u32_e32 vcc, %[xh], %[fs]\n\t"
+        "v_addc_co_u32_e64 %[m], %[co], %[m], %[m], vcc\n\t"
+        "v_cndmask_b32_e64 %[nh], %[xh], 0, vcc\n\t"
+        "v_cndmask_b32_e32 %[nl], %[xl], %[xh], vcc"
+        : [nh] "=&v"(nh), [nl] "=&v"(nl), [m] "+v"(c.mask), [co] "=&s"(co)
+        : [xh] "v"(c.xh), [xl] "v"(c.xl), [fs] "v"(fs)
+        : "vcc");
+  }
+  const double two52 = 4503599627370496.0;
+  const double nhd = __builtin_bit_cast(double, ((uint64_t)0x43300000u << 32) | nh) - two52;
+  const uint32_t qh = (uint32_t)__builtin_bit_cast(uint64_t, __builtin_fma(nhd, e.inv, two52));
+  const uint32_t rh = nh - __umul24(qh, f);
+  const double n2d = __builtin_bit_cast(double, ((uint64_t)(0x43300000u | rh) << 32) | nl) - two52;
+  const uint32_t ql = (uint32_t)__builtin_bit_cast(uint64_t, __builtin_fma(n2d, e.inv, two52));
+  c.xl = nl + e.c + ql * (g.M - f);
+  c.xh = __builtin_amdgcn_alignbit(qh, ql, g.a32);
+  if (!SO) c.slot++;
+}
+
+// KIND 0: prob_bits 15 (step15); 1: any prob_bits 12..19; 2: the same, size only
+template <int KIND>
+__device__ __forceinline__ void stepk(Coder& c, const EncFast& e, const PbShape& g) {
+  if (KIND == 0) step15(c, e);
+  else stepg<KIND == 2>(c, e, g);
+}
+
 __device__ __forceinline__ void ckpt(const Coder& c, Checkpoint* ck, uint32_t k) {
   if (!ck) return;                          // no side index for this job
   Checkpoint p;
@@ -121,6 +172,7 @@ __device__ __forceinline__ void ckpt(const Coder& c, Checkpoint* ck, uint32_t k)
 }
 
 // One lane per stream, 64 streams per wave, one wave per workgroup.
+template <int KIND>
 __global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane, SidMap ma, int na, SidMap mb, int nblk,
                                                   int rot) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -140,7 +192,11 @@ __global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane, SidMa
   const uint32_t sid = plane_sid(pi, j.spt, ma, na, mb);
   StreamInfo st = j.streams[sid];
   if (!st.fast || st.mode != SM_RANS || st.err || st.n == 0) return;
+  // another launch's stream: KIND 0 real pb-15 encodes, 1 real encodes at other prob_bits, 2 every
+  // size-only trial
+  if ((KIND == 2) != (st.sizeonly != 0) || (KIND != 2 && (KIND == 0) != (st.pb == 15))) return;
   const uint32_t n = st.n;
+  const PbShape g{31u - st.pb, 1u << st.pb, 32u - st.pb};
   const char* tb = (const char*)j.tab_fast;
   const uint32_t tbase = sid * (uint32_t)(HOH_FAST_RANGE * sizeof(EncFast));
   Coder c;
@@ -152,8 +208,8 @@ __global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane, SidMa
   const uint16_t* sp = j.sym + st.sym_off;
   // prologue: the top n % 32 symbols one at a time (descending); the rest is whole windows
   const uint32_t r = n & 31, nb = (n - r) / 8;   // nb 8-symbol blocks, a multiple of 4
-  for (uint32_t i = n; i > n - r; i--) step15(c, ent(tb, tbase + (uint32_t)sp[i - 1] * 16u));
-  flush_win(c);
+  for (uint32_t i = n; i > n - r; i--) stepk<KIND>(c, ent(tb, tbase + (uint32_t)sp[i - 1] * 16u), g);
+  if (KIND != 2) flush_win(c);
   if (((nb * 8) % HOH_SEG) == 0 && nb * 8 < n) ckpt(c, ck, nb * 8 / HOH_SEG);
   if (nb) {
     // table entries gathered 16 steps ahead (two 8-symbol blocks per buffer): with several images
@@ -170,10 +226,10 @@ __global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane, SidMa
     };
     auto run = [&](const EncFast* e, int p) {
 #pragma unroll
-      for (int k = 7; k >= 0; --k) step15(c, e[k]);
+      for (int k = 7; k >= 0; --k) stepk<KIND>(c, e[k], g);
       if (((2 * p + 1) & (HOH_SEG / 8 - 1)) == 0) ckpt(c, ck, (uint32_t)(2 * p + 1) * 8 / HOH_SEG);
 #pragma unroll
-      for (int k = 7; k >= 0; --k) step15(c, e[8 + k]);
+      for (int k = 7; k >= 0; --k) stepk<KIND>(c, e[8 + k], g);
       if (((2 * p) & (HOH_SEG / 8 - 1)) == 0) ckpt(c, ck, (uint32_t)(2 * p) * 8 / HOH_SEG);
     };
     uint4 h, l;
@@ -186,8 +242,13 @@ __global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane, SidMa
       if (p >= 2) { look(eA, h, l); if (p >= 3) syms(p - 3, h, l); }
       run(eB, p - 1);
       if (p >= 3) { look(eB, h, l); if (p >= 4) syms(p - 4, h, l); }
-      flush_win(c);
+      if (KIND != 2) flush_win(c);
     }
+  }
+  if (KIND == 2) {                         // size only: the emitted words + the two flushed ones
+    j.streams[sid].words = c.mask + 2;
+    j.streams[sid].widx_end = 0;
+    return;
   }
   flush_win(c);
   c.slab[--c.widx] = c.xh;                 // Rans64EncFlush: lo at the lower address
@@ -264,7 +325,7 @@ __global__ __launch_bounds__(64) void k_rans_gen(EncodeJob j, int nstreams, SidM
 
 static std::atomic<unsigned> g_rot{0};
 
-void launch_rans_fast(const EncodeJob& j, int nplane, hipStream_t s, SidMap a, int na, SidMap b) {
+void launch_rans_fast(const EncodeJob& j, int nplane, hipStream_t s, SidMap a, int na, SidMap b, int kind) {
   if (nplane <= 0) return;
   // The chain is issue-bound, so two chains on one SIMD run at half speed, and a launch ends with
   // its slowest chain; more than two chains per CU also slow each other.  One chain wave per
@@ -275,7 +336,12 @@ void launch_rans_fast(const EncodeJob& j, int nplane, hipStream_t s, SidMap a, i
   const int nblk = (nplane + 63) / 64;
   const int grid = nblk >= 1024 ? nblk : 1024;
   const int rot = grid == nblk ? 0 : (int)((g_rot.fetch_add(1) * 8u * (unsigned)((nblk + 7) / 8)) % (unsigned)grid);
-  hipLaunchKernelGGL(k_rans_fast, dim3(grid), dim3(64), 56 * 1024, s, j, nplane, a, na, b, nblk, rot);
+  if (kind == 0)
+    hipLaunchKernelGGL(k_rans_fast<0>, dim3(grid), dim3(64), 56 * 1024, s, j, nplane, a, na, b, nblk, rot);
+  else if (kind == 1)
+    hipLaunchKernelGGL(k_rans_fast<1>, dim3(grid), dim3(64), 56 * 1024, s, j, nplane, a, na, b, nblk, rot);
+  else   // size-only trial encodes: no window; one chain per SIMD (40 KB), all at once
+    hipLaunchKernelGGL(k_rans_fast<2>, dim3(grid), dim3(64), 40 * 1024, s, j, nplane, a, na, b, nblk, rot);
 }
 
 void launch_rans_gen(const EncodeJob& j, int nstreams, hipStream_t s, SidMap m) {

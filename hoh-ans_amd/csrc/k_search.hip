@@ -789,7 +789,7 @@ __global__ __launch_bounds__(128) void k_setup_s(EncodeJob j) {
       } else if (kind == KS_VAR) {
         st.sym_off = fin_plane_off(j, t, p);
         st.n = nclean; st.range = range; st.pb = kVarPb[(k - KS_VAR) % 8];
-        st.sizeonly = 1;
+        st.sizeonly = 1; st.fast = 1;                                // k_tables decides
         st.hist_src = t * SPT_S + KS_FIN + p + 1;
       }
       // KS_FIN stays absent until k_choose_s activates it
@@ -833,7 +833,7 @@ __global__ __launch_bounds__(64) void k_choose_s(EncodeJob j) {
     f.sizeonly = 0;
     f.slab_off = plane_slab_off_s(j, t, p);                          // the MED stream's slab: unused now
     f.slab_cap = j.npix_cap + 8;
-    f.mode = SM_EMPTY; f.words = 0; f.size = 0; f.err = 0;
+    f.mode = SM_EMPTY; f.words = 0; f.size = 0; f.err = 0; f.fast = 1;   // k_tables decides
     j.streams[(size_t)t * SPT_S + KS_FIN + p] = f;
   }
 }
@@ -1039,12 +1039,16 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, void (*mark)(void*, const
   launch_tables(j, S, s);
   mark(mc, "tables");
   launch_rans_fast(j, j.ntiles * 6, s, SidMap{3, KS_MED}, j.ntiles * 3, SidMap{3, KS_MED + 3});
+  // the prob_bits ladder's trial encodes (size only) on the f64-quotient chain as well
+  launch_rans_fast(j, j.ntiles * HOH_NPLANE_S * 8, s, SidMap{HOH_NPLANE_S * 8, KS_VAR}, j.ntiles * HOH_NPLANE_S * 8,
+                   SidMap{0, 0}, 2);
   launch_rans_gen(j, S, s);
   launch_finalize(j, S, s);
   mark(mc, "rans_enc");
   hipLaunchKernelGGL(k_choose_s, dim3((j.ntiles * HOH_NPLANE_S + 63) / 64), dim3(64), 0, s, j);
   const SidMap fin{HOH_NPLANE_S, KS_FIN};
   launch_tables(j, j.ntiles * HOH_NPLANE_S, s, fin);
+  launch_rans_fast(j, j.ntiles * HOH_NPLANE_S, s, fin, j.ntiles * HOH_NPLANE_S, SidMap{0, 0}, 1);
   launch_rans_gen(j, j.ntiles * HOH_NPLANE_S, s, fin);
   launch_finalize(j, j.ntiles * HOH_NPLANE_S, s, fin);
   mark(mc, "rans_enc_final");

@@ -141,3 +141,31 @@ def test_normalize_steals_many_levels(seed, pb):
     want = oracle.encode_entropy(sym, rng_sz, pb)
     got = hoh_ans.encode_entropy(sym, rng_sz, pb)
     assert bytes(got) == bytes(want)
+
+
+@pytest.mark.parametrize("pb", [12, 13, 14, 16, 17, 18, 19])
+def test_fast_chain_all_prob_bits(pb):
+    """The f64-quotient chain (k_rans_fast KIND 1) at every prob_bits of the -s>=1 ladder
+    (layer_encode.hpp:326-391) against the oracle (rans64.hpp:262-278): geometric, uniform and
+    peaked histograms (at prob_bits 19 a frequency above 2^18 hands the stream to k_rans_gen),
+    one-symbol streams and ranges 2..512."""
+    import oracle
+    import hoh_ans
+    rng = np.random.default_rng(77 + pb)
+    cases = []
+    for rg in (2, 16, 256, 512):
+        for kind in ("geo", "uni", "peak", "one"):
+            n = int(rng.integers(1, 70000))
+            if kind == "geo":
+                s = np.minimum(rng.geometric(rng.uniform(0.05, 0.6), n) - 1, rg - 1)
+            elif kind == "uni":
+                s = rng.integers(0, rg, n)
+            elif kind == "peak":
+                s = np.where(rng.random(n) < 0.9, 0, rng.integers(0, rg, n))
+            else:
+                s = np.full(n, rg - 1)
+            cases.append((s.astype(np.uint16), rg))
+    for s, rg in cases:
+        want = oracle.encode_entropy(s, rg, pb)
+        got = hoh_ans.encode_entropy(s, rg, pb)
+        assert bytes(got) == bytes(want), (pb, rg, s.size)
