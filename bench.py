@@ -215,6 +215,7 @@ def cpu_baseline(rgb_host, W, H, args):
                                 "sample": "first %d of %d tiles" % (nt1, ntiles),
                                 "enc_MBps": d["enc_MBps"], "dec_MBps": d["dec_MBps"]}
         res["all_cores_vs_single_x_cores"] = round(res["value"] / (st * len(procs)), 3)
+        res["effective_cores"] = round(res["value"] / st, 1)   # < cores: the host's CPU share is capped
         # the reference's own choh binary, -s0, one thread, whole image (dhoh cannot run: SURVEY Q1)
         choh = os.path.join(ROOT, "oracle", "_ref", "choh")
         if os.path.exists(choh) and not args.no_choh_binary:
@@ -272,6 +273,87 @@ def config2_leg(args):
                     "the GPU's rate comes from thousands of streams (configs[2])"}
 
 
+# ------------------------------------------------------------------------------ detail legs
+
+def golden_natural_sha(W, H, seed, speed=0):
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "golden_natural.json")) as f:
+            for r in json.load(f)["files"]:
+                sp = r["spec"]
+                if (sp["W"], sp["H"], sp["seed"], sp["speed"]) == (W, H, seed, speed):
+                    return r["out"]["sha256"]
+    except Exception:
+        pass
+    return None
+
+
+def extra_legs(args, slots, W, H, D, status, torch, hoh_ans, hd):
+    """N = 1 detail legs on the bench's own slots (contexts, streams, buffers), D images in flight,
+    one set-up pass per slot, then --leg-steps timed steps, lossless-checked afterwards:
+      no_index_pipeline: the same synthetic images, encoded without recording a side index and
+        decoded from the file alone (what a foreign .hoh gets: every stream one serial chain);
+      natural_s0_pipeline: configs[4]'s natural-statistic image (seed --seed, generated into every
+        slot's own buffer: other seeds hold palette tiles, which the format cannot decode, SURVEY
+        Q15), choh -s0 + dhoh with the side index; slot 0's file is compared with the reference
+        choh's SHA."""
+    out = {}
+    K = max(1, args.leg_steps)
+
+    def leg(inputs, use_index):
+        idx = [hoh_ans.Index() if use_index else None for _ in range(D)]
+
+        def enq(k, i):
+            s = slots[k]
+            with torch.cuda.stream(s.stream):
+                hoh_ans.encode_image_async(inputs[k], W, H, s.out, status[i, 0:2], ctx=s.ctx, index=idx[k])
+                hoh_ans.decode_image_async(s.out, s.out.numel(), W, H, s.dec, status[i, 2:4], ctx=s.ctx, index=idx[k])
+
+        def chk(total):
+            st = status[:total].cpu().numpy()
+            for i in range(total):
+                hoh_ans.check_status(st[i, 0:2], "leg encode (step %d)" % i)
+                hoh_ans.check_status(st[i, 2:4], "leg decode (step %d)" % i)
+
+        hd.run_pipeline(D, D, enq, lambda k, i: None)
+        torch.cuda.synchronize()
+        chk(D)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for c in range(0, K, status.shape[0]):      # status rows are reused per chunk of steps
+            hd.run_pipeline(D, min(status.shape[0], K - c), enq, lambda k, i: None)
+            torch.cuda.synchronize()
+            chk(min(status.shape[0], K - c))
+        el = time.perf_counter() - t
+        ok = all(bool(torch.equal(slots[k].dec, inputs[k])) for k in range(D))
+        n0 = int(status[min(status.shape[0], K) - 1 - ((min(status.shape[0], K) - 1) % D), 1].item())
+        return W * H * 3 * K / el / 1e6, ok, el / K * 1e3, n0
+
+    try:
+        v, ok, ms, _ = leg([s.rgb for s in slots], False)
+        out["no_index_pipeline_MBps"] = round(v, 1)
+        out["no_index_pipeline_ms_per_step"] = round(ms, 4)
+        out["no_index_pipeline_lossless"] = ok
+    except Exception as e:      # reported, never silently replaced
+        out["no_index_pipeline_error"] = repr(e)[:300]
+    try:
+        nat = [hoh_ans.natural_rgb_dev(W, H, args.seed, ctx=slots[k].ctx) for k in range(D)]
+        torch.cuda.synchronize()
+        v, ok, ms, n0 = leg(nat, True)
+        sha = hashlib.sha256(slots[0].out[:n0].cpu().numpy().tobytes()).hexdigest()
+        g = golden_natural_sha(W, H, args.seed)
+        out["natural_s0_MBps"] = round(v, 1)
+        out["natural_s0_ms_per_step"] = round(ms, 4)
+        out["natural_s0_lossless"] = ok
+        out["natural_s0_file_bytes"] = n0
+        out["natural_s0_bit_exact_vs_reference"] = (sha == g) if g else None
+        del nat
+    except Exception as e:
+        out["natural_s0_error"] = repr(e)[:300]
+    out["legs_note"] = ("%d images in flight, one set-up pass per slot, then %d timed steps each; inputs resident "
+                        "in HBM" % (D, K))
+    return out
+
+
 # ------------------------------------------------------------------------------ bench
 
 def main():
@@ -294,6 +376,9 @@ def main():
     ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 --pmc traffic passes")
     ap.add_argument("--sharded", action="store_true",
                     help="N = 1: run the N > 1 code path (tile encode, RCCL gather on a 1-rank group, tile decode)")
+    ap.add_argument("--no-legs", action="store_true",
+                    help="skip the detail legs (no-index pipeline, natural-statistic pipeline)")
+    ap.add_argument("--leg-steps", type=int, default=40, help="timed steps of each detail leg")
     ap.add_argument("--pmc-probe", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.size <= 0:
@@ -354,8 +439,8 @@ def main():
         t0, nt, y0, y1 = hd.shard(W, H, rank, world)
     rows = y1 - y0
     K = args.steps
-    warm = max(args.warmup, D)
-    status = torch.zeros((max(K, warm), 4), dtype=torch.int64, device=dev)
+    warm = args.warmup
+    status = torch.zeros((max(K, warm, D), 4), dtype=torch.int64, device=dev)
 
     class Slot:
         """One in-flight image: its own input (seed args.seed + k), library context (HIP stream +
@@ -429,9 +514,15 @@ def main():
 
     for s in slots:
         s.ctx.profiling(True)
-    run(warm)
+    # set-up pass (not warmup): one step per slot sizes its context's workspaces, so no slot
+    # allocates device memory inside the timed region; then exactly the requested warmup steps
+    run(D)
     torch.cuda.synchronize()
-    check_status(warm)
+    check_status(D)
+    if warm:
+        run(warm)
+        torch.cuda.synchronize()
+        check_status(warm)
     for s in slots:
         s.ctx.reset_stats()
         s.events = []
@@ -496,6 +587,9 @@ def main():
         n0 = n0 if n0 is not None else int(status[K - 1, 1].item())
         sha = hashlib.sha256(s0.out[:n0].cpu().numpy().tobytes()).hexdigest()
         comp_total = n0
+    legs = {}
+    if not sharded and not args.no_legs:      # after the checks: the legs reuse the slots' buffers
+        legs = extra_legs(args, slots, W, H, D, status, torch, hoh_ans, hd)
     else:
         n_rank = int(slots[0].sizes_host.numpy().astype(np.int64).sum())
         tt = torch.tensor([el, 0.0 if lossless else 1.0, t_enc, t_dec], dtype=torch.float64, device=dev)
@@ -573,6 +667,8 @@ def main():
                 "single_image_ms": round(single_ms, 3) if single_ms else None,
                 "no_index_decode_MBps": round(raw_total / noix_ms / 1e3, 1) if noix_ms else None,
                 "no_index_decode_lossless": noix_ok,
+                "setup_steps": D,
+                **legs,
                 "kernel_avg_ms_under_load": {k: round(v, 4) for k, v in kavg.items()},
                 "kernel_avg_ms_one_in_flight": {k: round(v, 4) for k, v in iso.items()},
                 "pmc_hbm_bytes_per_launch": pmc,

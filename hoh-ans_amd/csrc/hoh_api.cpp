@@ -412,6 +412,7 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
     launch_nuke(j, s);             prof.mark("lz");
     launch_tables(j, (int)S, s);   prof.mark("tables");
     launch_rans_fast(j, ntiles * 4, s, SidMap{3, SK_G}, ntiles * 3, SidMap{1, SK_I}); prof.mark("rans_enc_fast");
+    launch_rans_fast(j, ntiles * 3, s, SidMap{3, 0}, ntiles * 3, SidMap{0, 0}, 1);   // the LZ streams
     launch_rans_gen(j, (int)S, s); prof.mark("rans_enc_gen");
     launch_finalize(j, (int)S, s); prof.mark("finalize");
     launch_layout(j, s);           prof.mark("layout");
@@ -585,10 +586,10 @@ int encode_streams_impl(hoh_ctx* c, const uint16_t* d_syms, const uint64_t* off,
   if ((e = ensure(c->tab_gen, (size_t)nstreams * range * sizeof(EncGen)))) return e;
   if ((e = ensure(c->slabs, (size_t)nstreams * slab * 4))) return e;
   if ((e = ensure(c->misc, 64))) return e;
-  // prob_bits 12..19 with range <= 512 (every -s0 plane, config 2's single stream, the -s>=1
+  // prob_bits 7..19 with range <= 512 (every -s0 plane, config 2's single stream, the -s>=1
   // ladder) takes the tuned chain k_rans_fast (k_tables may still hand a stream back), the rest
   // the reference reciprocal step (k_rans_gen)
-  const bool fast = pb >= 12 && pb <= 19 && range <= HOH_FAST_RANGE;
+  const bool fast = pb >= 7 && pb <= 19 && range <= HOH_FAST_RANGE;
   if (fast && (e = ensure(c->tab_fast, (size_t)nstreams * HOH_FAST_RANGE * sizeof(EncFast)))) return e;
   std::vector<StreamInfo> st((size_t)nstreams);
   for (int i = 0; i < nstreams; i++) {

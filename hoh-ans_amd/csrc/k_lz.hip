@@ -167,6 +167,7 @@ __global__ __launch_bounds__(64) void k_lz(EncodeJob j) {
         st.n = k == 0 ? nf : nmk;
         st.range = 256;
         st.pb = 10;                                                   // lz.hpp:100-142
+        st.fast = 1;                                                  // k_tables decides
       } else if (k < SK_I) {
         st.sym_off = (size_t)(t * 3 + k - 3) * j.npix_cap;
         st.slab_off = (size_t)(t * 3 + k - 3) * pl_slab;

@@ -113,7 +113,8 @@ __device__ __forceinline__ void step15(Coder& c, const EncFast& e) {
   c.slot++;
 }
 
-// Any prob_bits 12..19 (the -s>=1 ladder, layer_encode.hpp:326-391): the same quotients with
+// Any prob_bits 7..19 (LZ streams at 10, predictor maps at 8, the -s>=1 ladder 12..19,
+// layer_encode.hpp:326-391, lz.hpp:100-142): the same quotients with
 // x_max = f << (63 - pb) tested as x_hi >= f << (31 - pb) (exact: f << (31 - pb) <= 2^31), the
 // low word nl + c + ql * (2^pb - f) and the high word (q * 2^pb) >> 32 = alignbit(qh, ql, 32 - pb).
 // Exactness of the f64 floors needs the numerators (< f * 2^32) times the 2.5-ulp relative error
@@ -334,7 +335,8 @@ void launch_rans_fast(const EncodeJob& j, int nplane, hipStream_t s, SidMap a, i
   // so that the chains of images in flight land on different CUs.  (Measured alternatives:
   // DESIGN.md §4.)
   const int nblk = (nplane + 63) / 64;
-  const int grid = nblk >= 1024 ? nblk : 1024;
+  // KIND 1 (LZ / map streams, the ladder's winners): short or few chains, no chip-wide grid
+  const int grid = (nblk >= 1024 || kind == 1) ? nblk : 1024;
   const int rot = grid == nblk ? 0 : (int)((g_rot.fetch_add(1) * 8u * (unsigned)((nblk + 7) / 8)) % (unsigned)grid);
   if (kind == 0)
     hipLaunchKernelGGL(k_rans_fast<0>, dim3(grid), dim3(64), 56 * 1024, s, j, nplane, a, na, b, nblk, rot);

@@ -764,6 +764,7 @@ __global__ __launch_bounds__(128) void k_setup_s(EncodeJob j) {
     st.n = k == 0 ? ti.nfut : nmk;
     st.range = 256;
     st.pb = 10;
+    st.fast = 1;                                                      // k_tables decides
   } else {
     int p, kind;
     if (k < KS_FIN) { kind = KS_MED; p = k - KS_MED; }
@@ -785,6 +786,7 @@ __global__ __launch_bounds__(128) void k_setup_s(EncodeJob j) {
           st.slab_off = map_slab_off_s(j, t, p);
           st.slab_cap = HOH_MAPCAP + 8;
           st.n = pi.xt * pi.yt; st.range = pi.used; st.pb = 8;        // layer_encode.hpp:308-315
+          st.fast = 1;
         }
       } else if (kind == KS_VAR) {
         st.sym_off = fin_plane_off(j, t, p);
@@ -1042,6 +1044,7 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, void (*mark)(void*, const
   // the prob_bits ladder's trial encodes (size only) on the f64-quotient chain as well
   launch_rans_fast(j, j.ntiles * HOH_NPLANE_S * 8, s, SidMap{HOH_NPLANE_S * 8, KS_VAR}, j.ntiles * HOH_NPLANE_S * 8,
                    SidMap{0, 0}, 2);
+  launch_rans_fast(j, S, s, SidMap{0, 0}, S, SidMap{0, 0}, 1);        // LZ and predictor-map streams
   launch_rans_gen(j, S, s);
   launch_finalize(j, S, s);
   mark(mc, "rans_enc");
