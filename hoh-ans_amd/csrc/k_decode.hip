@@ -17,6 +17,7 @@
 #include <string.h>
 #include <stdlib.h>
 #include <algorithm>
+#include <type_traits>
 #include <atomic>
 
 extern std::atomic<uint64_t> g_device_allocs;   // hoh_api.cpp
@@ -42,7 +43,11 @@ struct DecJob {
   uint32_t* matches;            // [tile][lz_cap+1][4]: pixel index, length, back, nuked before
   int lzband;                   // rows per band of k_dunpred_lz (LDS-bound)
   int lzstage;                  // k_dunpred_lz stages each band's residuals in LDS
-  uint32_t* lzt;                // tiles with LZ copies (w >= 64), appended by k_dlz; count in gerr[2]
+  uint32_t* lzt;                // tiles with LZ copies (w >= 64), appended by k_dlz; count in gerr[2];
+                                //   then the chain tiles of the tile width [ntiles, 2 ntiles) (count
+                                //   gerr[7]) and of the edge width [2 ntiles, 3 ntiles) (gerr[8])
+  uint8_t* bmap;                // chain tiles: per-pixel back distance, [tile][th][pitch(tw)]
+  uint32_t lz_xrow;             // copies reading the row above that make a tile a chain tile
   uint8_t* rgb;                 // output image
   uint32_t* gerr;
   const IndexStream* ix;        // optional side index
@@ -471,9 +476,16 @@ struct DrTables {
 // LDS loads by raw byte address (the kernel has no static LDS, so its dynamic area starts at 0):
 // through the extern array every address carried an add of the array's link-time base
 #ifdef __HIP_DEVICE_COMPILE__
-__device__ __forceinline__ uint2 lds_u2(uint32_t a) { return *(const __attribute__((address_space(3))) uint2*)(size_t)a; }
-__device__ __forceinline__ uint32_t lds_u32(uint32_t a) { return *(const __attribute__((address_space(3))) uint32_t*)(size_t)a; }
-__device__ __forceinline__ void lds_st32(uint32_t a, uint32_t v) { *(__attribute__((address_space(3))) uint32_t*)(size_t)a = v; }
+// The raw-address accessors use may_alias types: one LDS location is written and read at
+// different widths (u16 ring slots flushed as dwords, residual dwords read as u16), and with
+// type-based alias analysis the compiler may otherwise move a load above a store of another type.
+typedef uint16_t __attribute__((may_alias)) u16_ma;
+typedef uint32_t __attribute__((may_alias)) u32_ma;
+typedef uint2 __attribute__((may_alias)) u2_ma;
+typedef uint4 __attribute__((may_alias)) u4_ma;
+__device__ __forceinline__ uint2 lds_u2(uint32_t a) { return *(const __attribute__((address_space(3))) u2_ma*)(size_t)a; }
+__device__ __forceinline__ uint32_t lds_u32(uint32_t a) { return *(const __attribute__((address_space(3))) u32_ma*)(size_t)a; }
+__device__ __forceinline__ void lds_st32(uint32_t a, uint32_t v) { *(__attribute__((address_space(3))) u32_ma*)(size_t)a = v; }
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(size_t)(const __attribute__((address_space(3))) unsigned char*)p;
 }
@@ -1061,9 +1073,8 @@ __global__ void k_dstored(DecJob j, int nstreams) {
   dec_stored(j, sid, d);
 }
 
-// a tile with this many copies reading the row above goes to the raster-order path (natural
-// 8192^2, -s0: threshold 4 / 16 / 64 / never -> decode 24.1 / 24.1 / 23.5 / 24.9 ms)
-#define LZ_XROW 64
+// a tile with this many copies reading the row above is decoded as chains (k_dunpred_chain)
+#define LZ_XROW 16
 // LZ streams -> matches (un_lz.hpp:150-170); one wave per tile, 64 future entries per step.
 // Serially idx += fut[i], and a non-255 entry is a match (its length and back distance are the
 // g-th entries of the other two streams, g = matches before it) that advances idx by L too: the
@@ -1128,9 +1139,21 @@ __global__ __launch_bounds__(64) void k_dlz(DecJob j) {
   ti.nmatch = g0;
   if (bad) { ti.err = 1; atomicOr(j.gerr, 1u); }
   j.tiles[t] = ti;
-  // k_dunpred_lz's work list; bit 31: copies keep reading the row above, decode in raster order
-  if (!bad && g0 && ti.w >= 64)
-    j.lzt[atomicAdd(j.gerr + 2, 1u)] = (uint32_t)t | (xrow >= LZ_XROW && ti.w <= 256 ? 0x80000000u : 0u);
+  // copies that keep reading the row above make the wavefront serial: such tiles (and every LZ
+  // tile narrower than 64, whose copies reach two rows up) are chain tiles (k_dunpred_chain),
+  // listed by width class; the others are k_dunpred_lz's work list
+  if (bad) return;
+  if (!g0) {                                 // no copies: the planes must be whole (k_dunpred_fast)
+    const uint32_t np = (uint32_t)ti.w * ti.h;
+    if (st[3].n != np || st[4].n != np || st[5].n != np) { j.tiles[t].err = 1; atomicOr(j.gerr, 1u); }
+    return;
+  }
+  if (xrow >= j.lz_xrow || ti.w < 64) {
+    const int cls = ti.w == j.tw ? 1 : 2;
+    j.lzt[(size_t)cls * j.ntiles + atomicAdd(j.gerr + 6 + cls, 1u)] = (uint32_t)t;
+  } else {
+    j.lzt[atomicAdd(j.gerr + 2, 1u)] = (uint32_t)t;
+  }
 }
 
 __device__ __forceinline__ uint16_t dmed16(uint16_t a, uint16_t b, uint16_t c) {
@@ -1427,148 +1450,17 @@ __device__ __forceinline__ void dunpred_lz_tile(const DecJob& j, int t, uint32_t
 // tile), `many` = 1 otherwise (a worker per tile, 32-row bands in 33 KB: four per CU, so the
 // tiles of a natural image, many of them nearly serial, run at once).
 #define LZ_FEW 256
-__device__ __forceinline__ void dunpred_lzs_tile(const DecJob& j, int t, uint16_t* zrow);
 __global__ __launch_bounds__(64) void k_dunpred_lz(DecJob j, int br, int many) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lz_lds[];
   if (dec_abort(j)) return;
   const uint32_t cnt = *(volatile const uint32_t*)(j.gerr + 2);
   if ((cnt > LZ_FEW) != (many != 0)) return;
   for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
-    const uint32_t e = j.lzt[i];
-    const int t = (int)(e & 0x7fffffffu);
-    if ((e >> 31) && (size_t)(br + 1) * j.tw * 4 >= (size_t)12 * j.tiles[t].w)
-      dunpred_lzs_tile(j, t, (uint16_t*)lz_lds);
-    else
-      dunpred_lz_tile(j, t, lz_lds, br);
+    dunpred_lz_tile(j, (int)j.lzt[i], lz_lds, br);
     __syncthreads();
   }
 }
 
-__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t l) {
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
-}
-__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
-
-// Raster-order decode of an LZ tile whose copies keep reading the end of the row above (the
-// wavefront would wait a row per row).  The wave runs the reference's loop (layer_decode's
-// unprediction + the LZ copy, lz.hpp) with every lane on the same pixel: wave-uniform control
-// flow and scalar state, the three planes interleaved (their chains are independent, and the
-// copies and the residual index are shared: copied pixels skip a residual in every plane).
-// Residuals come a row (<= 256) at a time, four registers per plane, matches 64 at a time, the
-// row above 64 columns at a time, all picked by readlane; a 64-column chunk's values collect in
-// one register per plane, which goes to LDS (the copies' and the next row's source) and, composed
-// (inverse subtract-green), to the image as one coalesced row segment.
-__device__ __forceinline__ void dunpred_lzs_tile(const DecJob& j, int t, uint16_t* zrow) {
-  const DecTile ti = j.tiles[t];
-  if (ti.err) return;
-  const uint32_t lane = threadIdx.x;
-  const uint32_t w = (uint32_t)ti.w, h = (uint32_t)ti.h;
-  const uint16_t* rs[3];
-  uint32_t n = 0;
-  bool bad = false;
-#pragma unroll
-  for (int p = 0; p < 3; p++) {
-    rs[p] = j.dsym + (size_t)(t * 3 + p) * j.plane_cap;
-    const uint32_t np = j.streams[t * SK_PER_TILE + 3 + p].n;
-    if (p == 0) n = np; else bad |= np != n;
-  }
-  const uint32_t* mt = j.matches + (size_t)t * 4 * (j.lz_cap + 1);
-  const uint32_t nm = ti.nmatch;
-  uint8_t* obase = j.rgb + ((size_t)ti.y0 * j.W + ti.x0) * 3;
-  uint32_t k = 0;                                         // residual index, shared by the planes
-  uint32_t m = 0, mb = 0, mi = 0xffffffffu, ml = 0, mk = 0;  // match block: lane = match mb + lane
-  if (lane < nm) { mi = mt[4 * lane]; ml = mt[4 * lane + 1]; mk = mt[4 * lane + 2]; }
-  uint32_t midx = nm ? rdl(mi, 0) : 0xffffffffu, mend = nm ? midx + rdl(ml, 0) : 0u, mback = nm ? rdl(mk, 0) : 0u;
-  uint32_t cur = 0;
-  for (uint32_t y = 0; y < h; y++) {
-    uint16_t* crow = zrow + cur * 3 * w;                  // [plane][w], this row
-    const uint16_t* prow = zrow + (cur ^ 1) * 3 * w;      // the row above
-    const uint32_t rowi = y * w;
-    uint32_t Lv[3], Tp[3];
-    const uint32_t kb = k;
-    uint32_t r4[3][4];
-#pragma unroll
-    for (int p = 0; p < 3; p++) {
-      Lv[p] = Tp[p] = p ? 256u : 128u;
-#pragma unroll
-      for (int q = 0; q < 4; q++) r4[p][q] = kb + 64 * q + lane < n ? rs[p][kb + 64 * q + lane] : 0u;
-    }
-    for (uint32_t x0 = 0; x0 < w; x0 += 64) {
-      const uint32_t xe = min(w, x0 + 64);
-      uint32_t tv[3], cv[3];
-#pragma unroll
-      for (int p = 0; p < 3; p++) {
-        tv[p] = (y && x0 + lane < w) ? prow[p * w + x0 + lane] : (p ? 256u : 128u);
-        cv[p] = 0;
-      }
-      for (uint32_t x = x0; x < xe; x++) {
-        const uint32_t i = rowi + x;
-        while (mend <= i && m < nm) {                     // next match
-          m++;
-          if (m - mb >= 64) {
-            mb = m;
-            mi = 0xffffffffu; ml = 0; mk = 0;
-            if (mb + lane < nm) { mi = mt[4 * (mb + lane)]; ml = mt[4 * (mb + lane) + 1]; mk = mt[4 * (mb + lane) + 2]; }
-          }
-          if (m < nm) { midx = rdl(mi, m - mb); mend = midx + rdl(ml, m - mb); mback = rdl(mk, m - mb); }
-          else { midx = 0xffffffffu; mend = 0; }
-        }
-        uint32_t T[3], v[3];
-#pragma unroll
-        for (int p = 0; p < 3; p++) T[p] = rdl(tv[p], x - x0);
-        if (m < nm && midx <= i) {
-          const uint32_t src = i - mback;
-          if (src >= rowi + x0) {
-#pragma unroll
-            for (int p = 0; p < 3; p++) v[p] = rdl(cv[p], src - rowi - x0);
-          } else if (src >= rowi) {
-#pragma unroll
-            for (int p = 0; p < 3; p++) v[p] = uni(crow[p * w + src - rowi]);
-          } else if (src + w >= rowi) {
-#pragma unroll
-            for (int p = 0; p < 3; p++) v[p] = uni(prow[p * w + src + w - rowi]);
-          } else {                                        // two rows up: not a -s0 copy (back <= 64 <= w)
-            bad = true;
-#pragma unroll
-            for (int p = 0; p < 3; p++) v[p] = 0;
-          }
-        } else {
-          const uint32_t q = k - kb;
-          bad |= k >= n;
-          k++;
-          uint32_t r[3];
-          if (q < 128) {
-            if (q < 64) { for (int p = 0; p < 3; p++) r[p] = rdl(r4[p][0], q); }
-            else { for (int p = 0; p < 3; p++) r[p] = rdl(r4[p][1], q - 64); }
-          } else {
-            if (q < 192) { for (int p = 0; p < 3; p++) r[p] = rdl(r4[p][2], q - 128); }
-            else { for (int p = 0; p < 3; p++) r[p] = rdl(r4[p][3], q - 192); }
-          }
-#pragma unroll
-          for (int p = 0; p < 3; p++) {
-            const uint32_t c = p ? 512u : 256u;
-            const uint32_t pr = dmed16((uint16_t)T[p], (uint16_t)Lv[p], (uint16_t)(T[p] + Lv[p] - Tp[p]));
-            v[p] = (r[p] + pr + c / 2) & (c - 1);
-          }
-        }
-#pragma unroll
-        for (int p = 0; p < 3; p++) {
-          cv[p] = lane == x - x0 ? v[p] : cv[p];
-          Tp[p] = T[p];
-          Lv[p] = v[p];
-        }
-      }
-      if (x0 + lane < xe) {
-#pragma unroll
-        for (int p = 0; p < 3; p++) crow[p * w + x0 + lane] = (uint16_t)cv[p];
-        uint8_t* o = obase + ((size_t)y * j.W + x0 + lane) * 3;
-        o[0] = (uint8_t)(cv[1] + cv[0] - 256); o[1] = (uint8_t)cv[0]; o[2] = (uint8_t)(cv[2] + cv[0] - 256);
-      }
-    }
-    cur ^= 1;
-  }
-  if (bad || k != n) atomicOr(j.gerr, 1u);
-}
 
 __device__ __forceinline__ void dunpred_lz_tile(const DecJob& j, int t, uint32_t* lz_lds, int BR) {
   const DecTile ti = j.tiles[t];
@@ -1699,58 +1591,229 @@ __device__ __forceinline__ void dunpred_lz_tile(const DecJob& j, int t, uint32_t
   if (bad) atomicOr(j.gerr, 1u);
 }
 
-// Tiles with LZ copies narrower than 64 pixels (copies may reach two rows up): serial raster
-// walk per plane, one lane per plane, into dplane.
-__device__ __forceinline__ void dunpred_serial_tile(const DecJob& j, int t);
 
-// a small grid strides over the tiles (only LZ tiles narrower than 64 pixels work here)
-__global__ __launch_bounds__(192) void k_dunpred_serial(DecJob j) {
+// ---------------------------------------------------------------- LZ tiles as chains
+// A copy at a row's start that reads the end of the row above serialises a tile's rows (the
+// reference's raster order, un_lz.hpp:150-170 + unprediction.hpp:35-89): a tile with many of
+// them has no wavefront parallelism left, only its three planes, whose MED chains (L -> value ->
+// L) are independent once the copies are known.  k_dunpred_chain gives each (tile, plane) a LANE
+// (21 tiles per wave, lanes 3q + p) and walks the tile in raster order, one pixel per step for
+// every lane at once: the wave's tiles share a width, so the pixel index, the row loop and the
+// ring addresses are wave-uniform and a row starts with L = TL = half without a per-step select.
+// Per step and lane: the back distance from the tile's byte map (16 columns per load, one block
+// ahead), the copy source and T from a per-lane LDS ring of the last R values (R >= 2w, filled
+// with half first: row 0 reads half for T and TL), the residual from a 64-entry per-lane LDS ring
+// refilled 16 at a time a block ahead, MED, the select, the ring store and one u16 store of the
+// plane value (k_dcompose turns the three planes into RGB).
+__device__ __forceinline__ uint32_t bm_pitch(uint32_t w) { return (w + 15) & ~15u; }
+
+// per-pixel back distance of the chain tiles (0: predicted pixel), rows padded to 16 bytes
+__global__ __launch_bounds__(256) void k_dbackmap(DecJob j) {
   if (dec_abort(j)) return;
-  for (int t = blockIdx.x; t < j.ntiles; t += gridDim.x) dunpred_serial_tile(j, t);
+  const int cls = 1 + (int)(blockIdx.x >= (unsigned)j.ntiles);
+  const uint32_t e = blockIdx.x - (cls - 1) * j.ntiles;
+  if (e >= *(volatile const uint32_t*)(j.gerr + 6 + cls)) return;
+  const int t = (int)j.lzt[(size_t)cls * j.ntiles + e];
+  const DecTile ti = j.tiles[t];
+  const uint32_t w = ti.w, pitch = bm_pitch(w), tp = bm_pitch(j.tw);
+  uint8_t* bm = j.bmap + (size_t)t * j.th * tp;
+  uint4* b4 = (uint4*)bm;
+  for (uint32_t q = threadIdx.x; q < (uint32_t)ti.h * pitch / 16; q += 256) b4[q] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  const uint32_t* mt = j.matches + (size_t)t * 4 * (j.lz_cap + 1);
+  for (uint32_t m = threadIdx.x; m < ti.nmatch; m += 256) {
+    const uint4 v = *(const uint4*)(mt + 4 * m);                        // idx, length, back
+    for (uint32_t q = v.x; q < v.x + v.y; q++) bm[(q / w) * pitch + q % w] = (uint8_t)v.z;
+  }
 }
 
-__device__ __forceinline__ void dunpred_serial_tile(const DecJob& j, int t) {
+#ifdef __HIP_DEVICE_COMPILE__
+__device__ __forceinline__ uint32_t lds_u16(uint32_t a) { return *(const __attribute__((address_space(3))) u16_ma*)(size_t)a; }
+__device__ __forceinline__ void lds_st16(uint32_t a, uint32_t v) { *(__attribute__((address_space(3))) u16_ma*)(size_t)a = (uint16_t)v; }
+__device__ __forceinline__ uint4 lds_u4(uint32_t a) { return *(const __attribute__((address_space(3))) u4_ma*)(size_t)a; }
+__device__ __forceinline__ void lds_st4(uint32_t a, uint4 v) { *(__attribute__((address_space(3))) u4_ma*)(size_t)a = v; }
+#else
+__device__ uint32_t lds_u16(uint32_t);
+__device__ void lds_st16(uint32_t, uint32_t);
+__device__ uint4 lds_u4(uint32_t);
+__device__ void lds_st4(uint32_t, uint4);
+#endif
+
+// LDS map (byte addresses; no static LDS): value rings of CH_R u16 at lane * CH_VS, residual
+// rings of 64 entries + the mirror of entry 0 (entries k and k + 1 always adjacent) at
+// CH_RES_OFF + lane * CH_QS, the abort word last.  The lane strides are an odd number of dwords:
+// the lanes' rings start on different banks, so the wave's same-offset accesses (T, the ring
+// store, every step) are conflict-free (a 2 KB stride put all 63 lanes on one bank).
+#define CH_R 1024
+#define CH_VS (CH_R * 2 + 4)
+#define CH_QS 148
+#define CH_RES_OFF (64 * CH_VS)
+#define CH_SCR (CH_RES_OFF + 64 * CH_QS)
+#define CH_SMEM (CH_SCR + 16)
+
+// FULL: the wave's width is a multiple of 16, so 16-pixel blocks never straddle a row, their
+// ring slots are contiguous (constant ds offsets) and every block flushes its 16 values to the
+// plane with two 16-byte stores.  Within a block the next step's LDS reads (T, the copy source,
+// both candidate residuals) are issued before the current step's arithmetic, so the chain waits
+// on its VALU operations, not on LDS round trips.
+template <bool FULL>
+__global__ __launch_bounds__(64) void k_dunpred_chain(DecJob j, int cls) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t ch_lds[];
+  const uint32_t lane = threadIdx.x, q = lane / 3, p = lane - 3 * q;
+  uint32_t* scr = (uint32_t*)((unsigned char*)ch_lds + CH_SCR);
+  if (lane == 0) { scr[0] = *(volatile const uint32_t*)j.gerr; scr[1] = *(volatile const uint32_t*)(j.gerr + 6 + cls); }
+  __syncthreads();
+  const uint32_t base = blockIdx.x * 21, cnt = scr[1];
+  if (scr[0] || base >= cnt) return;
+  const bool act = lane < 63 && base + q < cnt;
+  const int t = (int)j.lzt[(size_t)cls * j.ntiles + base + (act ? q : 0)];
   const DecTile ti = j.tiles[t];
-  if (ti.err || unpred_fast(j, t, ti) || ti.w >= 64) return;
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int w = ti.w, h = ti.h;
-  const int depth = wv ? 9 : 8, c = 1 << depth, half = c / 2;
-  const uint16_t* res = j.dsym + (size_t)(t * 3 + wv) * j.plane_cap;
-  const DecStream d = j.streams[t * SK_PER_TILE + 3 + wv];
-  const uint32_t* mt = j.matches + (size_t)t * 4 * (j.lz_cap + 1);
-  uint16_t* plane = j.dplane + (size_t)(t * 3 + wv) * j.npix_cap;
-  if (lane == 0) {
-    uint32_t k = 0, m = 0, nm = ti.nmatch;   // residuals are consumed by the non-matched pixels
-    bool bad = false;
-    for (int y = 0; y < h && !bad; y++) {
-      for (int x = 0; x < w; x++) {
-        const uint32_t i = (uint32_t)y * w + x;
-        while (m < nm && mt[4 * m] + mt[4 * m + 1] <= i) m++;
-        uint16_t v;
-        if (m < nm && mt[4 * m] <= i) {
-          v = plane[i - mt[4 * m + 2]];
-        } else {
-          if (k >= d.n) { bad = true; break; }
-          const uint16_t r = res[k++];
-          const uint16_t L = x ? plane[i - 1] : (uint16_t)half;
-          const uint16_t T = y ? plane[i - w] : (uint16_t)half;
-          const uint16_t TL = (x && y) ? plane[i - w - 1] : (uint16_t)half;
-          const uint16_t p = dmed16(T, L, (uint16_t)(T + L - TL));
-          v = (uint16_t)((r + p - half + c) & (c - 1));
+  const uint32_t w = __builtin_amdgcn_readfirstlane(ti.w);             // one width per wave
+  const uint32_t h = act ? (uint32_t)ti.h : 0u;
+  uint32_t hmax = h;
+#pragma unroll
+  for (int o = 32; o; o >>= 1) hmax = max(hmax, (uint32_t)__shfl_xor(hmax, o));
+  const uint32_t c = p ? 512u : 256u, half = c >> 1, cm = c - 1;
+  const DecStream st = j.streams[t * SK_PER_TILE + 3 + p];
+  const uint16_t* res = j.dsym + (size_t)(t * 3 + p) * j.plane_cap;
+  uint16_t* outp = j.dplane + (size_t)(t * 3 + p) * j.npix_cap;
+  const uint32_t pitch = bm_pitch(w);
+  const uint8_t* bm = j.bmap + (size_t)t * j.th * bm_pitch(j.tw);
+  const uint32_t rb = lane * CH_VS, qb = CH_RES_OFF + lane * CH_QS;   // this lane's rings
+  for (uint32_t e = 0; e < CH_R; e += 2) lds_st32(rb + 2 * e, half | (half << 16));
+  // 16 residuals (two 16-byte loads) into ring entries s0 .. s0 + 15 as dwords
+  auto land16 = [&](uint32_t s0, const uint4& a, const uint4& b4) {
+    const uint32_t v[8] = {a.x, a.y, a.z, a.w, b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+    for (int e = 0; e < 8; e++) lds_st32(qb + 2 * s0 + 4 * e, v[e]);
+    if (s0 == 0) lds_st16(qb + 128, a.x);                              // mirror of entry 0
+  };
+  // residual ring: entries [k, kfill) resident, the next 16 in flight (pend) when hp
+  uint32_t k = 0, kfill = 32;
+  uint4 pend0, pend1;
+  {
+    const uint4* r4 = (const uint4*)res;
+    land16(0, r4[0], r4[1]);
+    land16(16, r4[2], r4[3]);
+    pend0 = r4[4]; pend1 = r4[5];
+  }
+  bool hp = true;
+  uint4 bnext = *(const uint4*)bm;                                     // row 0, columns 0..15
+  for (uint32_t y = 0; y < hmax; y++) {
+    uint32_t L = half, Tp = half;                                      // row start: L = TL = half
+    const bool live = y < h;
+    for (uint32_t x0 = 0; x0 < w; x0 += 16) {
+      const uint4 bcur = bnext;
+      {
+        const uint32_t ny = x0 + 16 < w ? y : y + 1, nx = x0 + 16 < w ? x0 + 16 : 0;
+        bnext = live && ny < h ? *(const uint4*)(bm + (size_t)ny * pitch + nx) : make_uint4(0, 0, 0, 0);
+      }
+      if (!live) continue;
+      if (hp) {                                                        // land the residuals fetched a block ago
+        land16(kfill & 63, pend0, pend1);
+        kfill += 16;
+      }
+      hp = kfill + 16 - k <= 64;
+      if (hp) {
+        const uint4* r4 = (const uint4*)(res + kfill);
+        pend0 = r4[0]; pend1 = r4[1];
+      }
+      const uint32_t i0 = y * w + x0;
+      const uint32_t bw[4] = {bcur.x, bcur.y, bcur.z, bcur.w};
+      if (FULL) {
+        const uint32_t pos0 = i0 & (CH_R - 1);
+        const uint32_t tA = rb + 2 * ((pos0 - w) & (CH_R - 1));        // T of step u at tA + 2u
+        const uint32_t wA = rb + 2 * pos0;                             // this block's slots
+        // the 16 steps, specialised on whether a copy source can wrap around the ring (b <= 255)
+        auto block = [&](auto nowrap_c) {
+          constexpr bool NOWRAP = decltype(nowrap_c)::value;
+          auto srcA = [&](int u, uint32_t b) -> uint32_t {
+            return NOWRAP ? wA + 2 * u - 2 * b : rb + 2 * ((pos0 + (uint32_t)u - b) & (CH_R - 1));
+          };
+          // step 0 reads its copy source after every earlier write, so even b = 1 comes from the
+          // ring (at a row's start that is the end of the row above, not L = half)
+          uint32_t b = bw[0] & 255u;
+          uint32_t T = lds_u16(tA), vC = lds_u16(srcA(0, b ? b : 1));
+          uint32_t ra = lds_u16(qb + 2 * (k & 63)), rbv = lds_u16(qb + 2 * (k & 63) + 2);
+          bool pcopy = true;                                           // r = ra for step 0 (k is current)
+#pragma unroll
+          for (int u = 0; u < 16; u++) {
+            // the next step's reads first (its copy source, when it is not this step's pixel, was
+            // written by an earlier step; its residual is entry k or k + 1)
+            uint32_t bn = 0, Tn = 0, vCn = 0, ran = 0, rbn = 0;
+            if (u < 15) {
+              bn = (bw[(u + 1) >> 2] >> (8 * ((u + 1) & 3))) & 255u;
+              Tn = lds_u16(tA + 2 * (u + 1));
+              vCn = lds_u16(srcA(u + 1, bn < 2 ? 2 : bn));
+              ran = lds_u16(qb + 2 * (k & 63));
+              rbn = lds_u16(qb + 2 * (k & 63) + 2);
+            }
+            const uint32_t r = pcopy ? ra : rbv;
+            const uint32_t pr = med3u(T, L, (T + L - Tp) & 0xffffu);
+            uint32_t vm = (r + pr + half) & cm, vc = (u > 0 && b == 1) ? L : vC;
+            // both values, then a select: left to itself the compiler branches around the MED
+            // (exec-mask juggling on every step of a divergent wave)
+            asm volatile("" : "+v"(vm), "+v"(vc));
+            const uint32_t v = b ? vc : vm;
+            k += b ? 0u : 1u;
+            pcopy = b != 0;
+            lds_st16(wA + 2 * u, v);
+            Tp = T;
+            L = v;
+            b = bn; T = Tn; vC = vCn; ra = ran; rbv = rbn;
+          }
+        };
+        if (pos0 >= 256) block(std::true_type{});                       // i - b >= 1 for every b <= 255
+        else block(std::false_type{});
+        // the block's 16 values to the plane (two 16-byte stores)
+        uint32_t d[8];
+#pragma unroll
+        for (int e = 0; e < 8; e++) d[e] = lds_u32(wA + 4 * e);
+        uint4* o4 = (uint4*)(outp + i0);
+        o4[0] = make_uint4(d[0], d[1], d[2], d[3]);
+        o4[1] = make_uint4(d[4], d[5], d[6], d[7]);
+      } else {
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+          if (x0 + u < w) {
+            const uint32_t i = i0 + u;
+            const uint32_t b = (bw[u >> 2] >> (8 * (u & 3))) & 255u;
+            const uint32_t vC = lds_u16(rb + 2 * ((i - b) & (CH_R - 1)));
+            const uint32_t T = lds_u16(rb + 2 * ((i - w) & (CH_R - 1)));
+            const uint32_t r = lds_u16(qb + 2 * (k & 63));
+            const uint32_t pr = med3u(T, L, (T + L - Tp) & 0xffffu);
+            const uint32_t vm = (r + pr + half) & cm;
+            const uint32_t v = b ? vC : vm;
+            k += b ? 0u : 1u;
+            lds_st16(rb + 2 * (i & (CH_R - 1)), v);
+            outp[i] = (uint16_t)v;
+            Tp = T;
+            L = v;
+          }
         }
-        plane[i] = v;
       }
     }
-    if (bad || k != d.n) atomicOr(j.gerr, 1u);
   }
-  __syncthreads();
+  if (act && k != st.n) atomicOr(j.gerr, 1u);
+}
+
+// RGB of the chain tiles from their three decoded planes (inverse subtract-green)
+__global__ __launch_bounds__(256) void k_dcompose(DecJob j) {
+  if (dec_abort(j)) return;
+  const int cls = 1 + (int)(blockIdx.y);
+  const uint32_t e = blockIdx.x;
+  if (e >= *(volatile const uint32_t*)(j.gerr + 6 + cls)) return;
+  const int t = (int)j.lzt[(size_t)cls * j.ntiles + e];
+  const DecTile ti = j.tiles[t];
   const uint16_t* G = j.dplane + (size_t)(t * 3) * j.npix_cap;
-  const uint16_t* R = G + j.npix_cap;
-  const uint16_t* B = R + j.npix_cap;
-  for (int i = threadIdx.x; i < w * h; i += 192) {
-    const int yy = i / w, xx = i % w;
+  const uint16_t* Rp = G + j.npix_cap;
+  const uint16_t* Bp = Rp + j.npix_cap;
+  const uint32_t w = ti.w, npix = w * ti.h;
+  for (uint32_t i = threadIdx.x; i < npix; i += 256) {
+    const uint32_t yy = i / w, xx = i - yy * w;
     uint8_t* o = j.rgb + ((size_t)(ti.y0 + yy) * j.W + ti.x0 + xx) * 3;
-    o[0] = (uint8_t)(R[i] + G[i] - 256); o[1] = (uint8_t)G[i]; o[2] = (uint8_t)(B[i] + G[i] - 256);
+    const uint32_t g = G[i];
+    o[0] = (uint8_t)(Rp[i] + g - 256); o[1] = (uint8_t)g; o[2] = (uint8_t)(Bp[i] + g - 256);
   }
 }
 
@@ -1907,6 +1970,12 @@ int decode_tiles_async_impl(hoh_ctx* c, const uint8_t* d_blob, size_t size, int 
   return decode_run(c, j, idx, s, &as);
 }
 
+// HOH_LZ_XROW: copies reading the row above that make an LZ tile a chain tile (measurement knob)
+static uint32_t lz_xrow() {
+  static const uint32_t v = [] { const char* e = getenv("HOH_LZ_XROW"); return e ? (uint32_t)atoi(e) : (uint32_t)LZ_XROW; }();
+  return v;
+}
+
 // HOH_NOIX_WAVE=1: no-index decodes with k_drans_wave alone (the round-2 decoder, for comparison)
 static int noix_wave() {
   static const int v = [] { const char* e = getenv("HOH_NOIX_WAVE"); return e ? atoi(e) : 0; }();
@@ -1936,7 +2005,9 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   if ((e = dbuf(w, 5, (size_t)j.ntiles * 4 * (j.lz_cap + 1) * 4, &q))) return e; j.matches = (uint32_t*)q;
   if ((e = dbuf(w, 6, 64, &q))) return e; j.gerr = (uint32_t*)q;
   if ((e = dbuf(w, 7, (size_t)j.ntiles * 3 * j.npix_cap * 2, &q))) return e; j.dplane = (uint16_t*)q;
-  if ((e = dbuf(w, 14, (size_t)j.ntiles * 4, &q))) return e; j.lzt = (uint32_t*)q;
+  if ((e = dbuf(w, 14, (size_t)j.ntiles * 3 * 4, &q))) return e; j.lzt = (uint32_t*)q;
+  if ((e = dbuf(w, 15, (size_t)j.ntiles * j.th * ((j.tw + 15) & ~15) + 16, &q))) return e; j.bmap = (uint8_t*)q;
+  j.lz_xrow = lz_xrow();
   j.ix = index_streams(idx);
   j.ck = index_ckpts(idx);
   j.nix = index_nstreams(idx);
@@ -1970,6 +2041,30 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   if (!indexed) hipLaunchKernelGGL(k_dstored, dim3(S), dim3(256), 0, s, j, S);
   hipLaunchKernelGGL(k_dlz, dim3(j.ntiles), dim3(64), 0, s, j);
   ctx_mark(c, s, "dlz", false);
+  // chain tiles (the two width classes): back-distance maps, the chains, RGB -- on a second
+  // stream, concurrently with the wavefront unpredict below (disjoint tiles; both are
+  // latency-bound and leave most of the chip idle)
+  if (!w.side) {
+    if (hipStreamCreateWithFlags(&w.side, hipStreamNonBlocking) != hipSuccess) return 3;
+    if (hipEventCreateWithFlags(&w.fork, hipEventDisableTiming) != hipSuccess) return 3;
+    if (hipEventCreateWithFlags(&w.join, hipEventDisableTiming) != hipSuccess) return 3;
+  }
+  if (hipEventRecord(w.fork, s) != hipSuccess || hipStreamWaitEvent(w.side, w.fork, 0) != hipSuccess) return 3;
+  {
+    const hipStream_t s2 = w.side;
+    const int ga = (j.ntiles + 20) / 21;
+    hipLaunchKernelGGL(k_dbackmap, dim3(2 * j.ntiles), dim3(256), 0, s2, j);
+    const int we = j.W - (j.xt - 1) * j.tw;                             // the edge column's width
+    for (int cls = 1; cls <= 2; cls++) {
+      const int wc = cls == 1 ? j.tw : we;
+      if (wc % 16 == 0)
+        hipLaunchKernelGGL(k_dunpred_chain<true>, dim3(ga), dim3(64), CH_SMEM, s2, j, cls);
+      else
+        hipLaunchKernelGGL(k_dunpred_chain<false>, dim3(ga), dim3(64), CH_SMEM, s2, j, cls);
+    }
+    hipLaunchKernelGGL(k_dcompose, dim3(j.ntiles, 2), dim3(256), 0, s2, j);
+    if (hipEventRecord(w.join, s2) != hipSuccess) return 3;
+  }
   hipLaunchKernelGGL(k_dunpred_fast, dim3(j.ntiles), dim3(64), (size_t)64 * ORING_PITCH + 6 * LAST_N(j.tw), s, j);
   {
     // On natural images most tiles hold copies, and a copy at a row's start that reads the end of
@@ -1985,7 +2080,7 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
     if (j.ntiles > LZ_FEW)
       hipLaunchKernelGGL(k_dunpred_lz, dim3(j.ntiles), dim3(64), (size_t)(br_many + 1) * rowb, s, j, br_many, 1);
   }
-  hipLaunchKernelGGL(k_dunpred_serial, dim3(std::min(j.ntiles, 64)), dim3(192), 0, s, j);
+  if (hipStreamWaitEvent(s, w.join, 0) != hipSuccess) return 3;   // the chain tiles are done
   ctx_mark(c, s, "dunpred", false);
   if (hipGetLastError() != hipSuccess) return 3;
   if (as) {
