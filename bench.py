@@ -587,9 +587,6 @@ def main():
         n0 = n0 if n0 is not None else int(status[K - 1, 1].item())
         sha = hashlib.sha256(s0.out[:n0].cpu().numpy().tobytes()).hexdigest()
         comp_total = n0
-    legs = {}
-    if not sharded and not args.no_legs:      # after the checks: the legs reuse the slots' buffers
-        legs = extra_legs(args, slots, W, H, D, status, torch, hoh_ans, hd)
     else:
         n_rank = int(slots[0].sizes_host.numpy().astype(np.int64).sum())
         tt = torch.tensor([el, 0.0 if lossless else 1.0, t_enc, t_dec], dtype=torch.float64, device=dev)
@@ -601,6 +598,9 @@ def main():
         comp_total = int(nn.item())          # slot 0's image (seed args.seed), all shards
     raw_total = W * H * 3
     value = raw_total * K / el / 1e6
+    legs = {}
+    if not sharded and not args.no_legs:      # after the checks: the legs reuse the slots' buffers
+        legs = extra_legs(args, slots, W, H, D, status, torch, hoh_ans, hd)
 
     if rank == 0:
         kavg = {k: v[0] / v[1] for k, v in stats.items() if v[1]}

@@ -23,6 +23,7 @@
 #include "hoh_internal.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <atomic>
 
 #define WIN 32
@@ -326,6 +327,17 @@ __global__ __launch_bounds__(64) void k_rans_gen(EncodeJob j, int nstreams, SidM
 
 static std::atomic<unsigned> g_rot{0};
 
+// LDS requested per chain workgroup (isolation: at most 160 / this many chains per CU); the
+// HOH_CHAIN_LDS_KB environment variable overrides it for measurement
+static size_t chain_lds() {
+  static const size_t v = [] {
+    const char* e = getenv("HOH_CHAIN_LDS_KB");
+    const int kb = e ? atoi(e) : 56;
+    return (size_t)(kb < 8 ? 8 : kb > 160 ? 160 : kb) * 1024;
+  }();
+  return v;
+}
+
 void launch_rans_fast(const EncodeJob& j, int nplane, hipStream_t s, SidMap a, int na, SidMap b, int kind) {
   if (nplane <= 0) return;
   // The chain is issue-bound, so two chains on one SIMD run at half speed, and a launch ends with
@@ -339,9 +351,9 @@ void launch_rans_fast(const EncodeJob& j, int nplane, hipStream_t s, SidMap a, i
   const int grid = (nblk >= 1024 || kind == 1) ? nblk : 1024;
   const int rot = grid == nblk ? 0 : (int)((g_rot.fetch_add(1) * 8u * (unsigned)((nblk + 7) / 8)) % (unsigned)grid);
   if (kind == 0)
-    hipLaunchKernelGGL(k_rans_fast<0>, dim3(grid), dim3(64), 56 * 1024, s, j, nplane, a, na, b, nblk, rot);
+    hipLaunchKernelGGL(k_rans_fast<0>, dim3(grid), dim3(64), chain_lds(), s, j, nplane, a, na, b, nblk, rot);
   else if (kind == 1)
-    hipLaunchKernelGGL(k_rans_fast<1>, dim3(grid), dim3(64), 56 * 1024, s, j, nplane, a, na, b, nblk, rot);
+    hipLaunchKernelGGL(k_rans_fast<1>, dim3(grid), dim3(64), chain_lds(), s, j, nplane, a, na, b, nblk, rot);
   else   // size-only trial encodes: no window; one chain per SIMD (40 KB), all at once
     hipLaunchKernelGGL(k_rans_fast<2>, dim3(grid), dim3(64), 40 * 1024, s, j, nplane, a, na, b, nblk, rot);
 }
