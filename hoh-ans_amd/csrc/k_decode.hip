@@ -1073,7 +1073,7 @@ __global__ void k_dstored(DecJob j, int nstreams) {
   dec_stored(j, sid, d);
 }
 
-// a tile with this many copies reading the row above is decoded as chains (k_dunpred_chain)
+// a tile with this many copies reading the row above is decoded as chains (the chain role of k_dunpred_lz)
 #define LZ_XROW 16
 // LZ streams -> matches (un_lz.hpp:150-170); one wave per tile, 64 future entries per step.
 // Serially idx += fut[i], and a non-255 entry is a match (its length and back distance are the
@@ -1140,7 +1140,7 @@ __global__ __launch_bounds__(64) void k_dlz(DecJob j) {
   if (bad) { ti.err = 1; atomicOr(j.gerr, 1u); }
   j.tiles[t] = ti;
   // copies that keep reading the row above make the wavefront serial: such tiles (and every LZ
-  // tile narrower than 64, whose copies reach two rows up) are chain tiles (k_dunpred_chain),
+  // tile narrower than 64, whose copies reach two rows up) are chain tiles (the chain role of k_dunpred_lz),
   // listed by width class; the others are k_dunpred_lz's work list
   if (bad) return;
   if (!g0) {                                 // no copies: the planes must be whole (k_dunpred_fast)
@@ -1450,12 +1450,28 @@ __device__ __forceinline__ void dunpred_lz_tile(const DecJob& j, int t, uint32_t
 // tile), `many` = 1 otherwise (a worker per tile, 32-row bands in 33 KB: four per CU, so the
 // tiles of a natural image, many of them nearly serial, run at once).
 #define LZ_FEW 256
-__global__ __launch_bounds__(64) void k_dunpred_lz(DecJob j, int br, int many) {
+template <bool FULL, int CH_R>
+__device__ void chain_tiles(const DecJob& j, int cls, uint32_t blk);
+
+// Workgroups [0, wgrid) take the wavefront tiles; the ones after them the chain tiles (ga
+// workgroups per width class, class 2 only when the edge column is narrower), so both run in
+// the same launch, concurrently, without a second stream.  No static LDS: the chain code
+// addresses the dynamic area from 0.
+template <int CH_R>
+__global__ __launch_bounds__(64) void k_dunpred_lz(DecJob j, int br, int many, int wgrid, int ga, int full1, int full2) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lz_lds[];
-  if (dec_abort(j)) return;
+  if (*(volatile const uint32_t*)j.gerr) return;                      // one load per wave: uniform
   const uint32_t cnt = *(volatile const uint32_t*)(j.gerr + 2);
   if ((cnt > LZ_FEW) != (many != 0)) return;
-  for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+  if ((int)blockIdx.x >= wgrid) {
+    const uint32_t ci = blockIdx.x - wgrid;
+    const int cls = ci < (uint32_t)ga ? 1 : 2;
+    const uint32_t blk = ci - (cls - 1) * ga;
+    if (cls == 1 ? full1 : full2) chain_tiles<true, CH_R>(j, cls, blk);
+    else chain_tiles<false, CH_R>(j, cls, blk);
+    return;
+  }
+  for (uint32_t i = blockIdx.x; i < cnt; i += wgrid) {
     dunpred_lz_tile(j, (int)j.lzt[i], lz_lds, br);
     __syncthreads();
   }
@@ -1596,7 +1612,7 @@ __device__ __forceinline__ void dunpred_lz_tile(const DecJob& j, int t, uint32_t
 // A copy at a row's start that reads the end of the row above serialises a tile's rows (the
 // reference's raster order, un_lz.hpp:150-170 + unprediction.hpp:35-89): a tile with many of
 // them has no wavefront parallelism left, only its three planes, whose MED chains (L -> value ->
-// L) are independent once the copies are known.  k_dunpred_chain gives each (tile, plane) a LANE
+// L) are independent once the copies are known.  the chain role of k_dunpred_lz gives each (tile, plane) a LANE
 // (21 tiles per wave, lanes 3q + p) and walks the tile in raster order, one pixel per step for
 // every lane at once: the wave's tiles share a width, so the pixel index, the row loop and the
 // ring addresses are wave-uniform and a row starts with L = TL = half without a per-step select.
@@ -1608,12 +1624,18 @@ __device__ __forceinline__ void dunpred_lz_tile(const DecJob& j, int t, uint32_t
 __device__ __forceinline__ uint32_t bm_pitch(uint32_t w) { return (w + 15) & ~15u; }
 
 // per-pixel back distance of the chain tiles (0: predicted pixel), rows padded to 16 bytes
+// A small grid strides over both chain lists (an image without chain tiles dispatches little).
+__device__ __forceinline__ void backmap_tile(const DecJob& j, int t);
 __global__ __launch_bounds__(256) void k_dbackmap(DecJob j) {
   if (dec_abort(j)) return;
-  const int cls = 1 + (int)(blockIdx.x >= (unsigned)j.ntiles);
-  const uint32_t e = blockIdx.x - (cls - 1) * j.ntiles;
-  if (e >= *(volatile const uint32_t*)(j.gerr + 6 + cls)) return;
-  const int t = (int)j.lzt[(size_t)cls * j.ntiles + e];
+  const uint32_t n1 = *(volatile const uint32_t*)(j.gerr + 7), n2 = *(volatile const uint32_t*)(j.gerr + 8);
+  for (uint32_t e = blockIdx.x; e < n1 + n2; e += gridDim.x) {
+    backmap_tile(j, (int)(e < n1 ? j.lzt[(size_t)j.ntiles + e] : j.lzt[(size_t)2 * j.ntiles + e - n1]));
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ void backmap_tile(const DecJob& j, int t) {
   const DecTile ti = j.tiles[t];
   const uint32_t w = ti.w, pitch = bm_pitch(w), tp = bm_pitch(j.tw);
   uint8_t* bm = j.bmap + (size_t)t * j.th * tp;
@@ -1644,28 +1666,29 @@ __device__ void lds_st4(uint32_t, uint4);
 // CH_RES_OFF + lane * CH_QS, the abort word last.  The lane strides are an odd number of dwords:
 // the lanes' rings start on different banks, so the wave's same-offset accesses (T, the ring
 // store, every step) are conflict-free (a 2 KB stride put all 63 lanes on one bank).
-#define CH_R 1024
-#define CH_VS (CH_R * 2 + 4)
+// CH_T tiles per wave (lanes 3q + p < 3 CH_T): 35 KB of LDS with R = 512, so the launch
+// co-resides with the other kernels of images in flight (21 tiles needed 137 KB, a whole CU's).
+#define CH_T 10
+#define CH_L (3 * CH_T)
 #define CH_QS 148
-#define CH_RES_OFF (64 * CH_VS)
-#define CH_SCR (CH_RES_OFF + 64 * CH_QS)
-#define CH_SMEM (CH_SCR + 16)
+__host__ __device__ constexpr uint32_t ch_vs(int R) { return (uint32_t)R * 2 + 4; }
+__host__ __device__ constexpr uint32_t ch_res_off(int R) { return CH_L * ch_vs(R); }
+__host__ __device__ constexpr uint32_t ch_scr(int R) { return ch_res_off(R) + CH_L * CH_QS; }
+__host__ __device__ constexpr uint32_t ch_smem(int R) { return ch_scr(R) + 16; }
 
 // FULL: the wave's width is a multiple of 16, so 16-pixel blocks never straddle a row, their
 // ring slots are contiguous (constant ds offsets) and every block flushes its 16 values to the
 // plane with two 16-byte stores.  Within a block the next step's LDS reads (T, the copy source,
 // both candidate residuals) are issued before the current step's arithmetic, so the chain waits
 // on its VALU operations, not on LDS round trips.
-template <bool FULL>
-__global__ __launch_bounds__(64) void k_dunpred_chain(DecJob j, int cls) {
-  extern __shared__ __attribute__((aligned(16))) uint16_t ch_lds[];
+// Workgroup `blk` of the chain tiles of width class cls (called from k_dunpred_lz, whose launch
+// has at least ch_smem(CH_R) bytes of dynamic LDS starting at address 0).
+template <bool FULL, int CH_R>
+__device__ void chain_tiles(const DecJob& j, int cls, uint32_t blk) {
   const uint32_t lane = threadIdx.x, q = lane / 3, p = lane - 3 * q;
-  uint32_t* scr = (uint32_t*)((unsigned char*)ch_lds + CH_SCR);
-  if (lane == 0) { scr[0] = *(volatile const uint32_t*)j.gerr; scr[1] = *(volatile const uint32_t*)(j.gerr + 6 + cls); }
-  __syncthreads();
-  const uint32_t base = blockIdx.x * 21, cnt = scr[1];
-  if (scr[0] || base >= cnt) return;
-  const bool act = lane < 63 && base + q < cnt;
+  const uint32_t base = blk * CH_T, cnt = *(volatile const uint32_t*)(j.gerr + 6 + cls);
+  if (base >= cnt) return;
+  const bool act = lane < CH_L && base + q < cnt;
   const int t = (int)j.lzt[(size_t)cls * j.ntiles + base + (act ? q : 0)];
   const DecTile ti = j.tiles[t];
   const uint32_t w = __builtin_amdgcn_readfirstlane(ti.w);             // one width per wave
@@ -1673,13 +1696,14 @@ __global__ __launch_bounds__(64) void k_dunpred_chain(DecJob j, int cls) {
   uint32_t hmax = h;
 #pragma unroll
   for (int o = 32; o; o >>= 1) hmax = max(hmax, (uint32_t)__shfl_xor(hmax, o));
+  if (lane >= CH_L) return;                                            // no rings for these lanes
   const uint32_t c = p ? 512u : 256u, half = c >> 1, cm = c - 1;
   const DecStream st = j.streams[t * SK_PER_TILE + 3 + p];
   const uint16_t* res = j.dsym + (size_t)(t * 3 + p) * j.plane_cap;
   uint16_t* outp = j.dplane + (size_t)(t * 3 + p) * j.npix_cap;
   const uint32_t pitch = bm_pitch(w);
   const uint8_t* bm = j.bmap + (size_t)t * j.th * bm_pitch(j.tw);
-  const uint32_t rb = lane * CH_VS, qb = CH_RES_OFF + lane * CH_QS;   // this lane's rings
+  const uint32_t rb = lane * ch_vs(CH_R), qb = ch_res_off(CH_R) + lane * CH_QS;   // this lane's rings
   for (uint32_t e = 0; e < CH_R; e += 2) lds_st32(rb + 2 * e, half | (half << 16));
   // 16 residuals (two 16-byte loads) into ring entries s0 .. s0 + 15 as dwords
   auto land16 = [&](uint32_t s0, const uint4& a, const uint4& b4) {
@@ -1798,12 +1822,15 @@ __global__ __launch_bounds__(64) void k_dunpred_chain(DecJob j, int cls) {
 }
 
 // RGB of the chain tiles from their three decoded planes (inverse subtract-green)
+__device__ __forceinline__ void compose_tile(const DecJob& j, int t);
 __global__ __launch_bounds__(256) void k_dcompose(DecJob j) {
   if (dec_abort(j)) return;
-  const int cls = 1 + (int)(blockIdx.y);
-  const uint32_t e = blockIdx.x;
-  if (e >= *(volatile const uint32_t*)(j.gerr + 6 + cls)) return;
-  const int t = (int)j.lzt[(size_t)cls * j.ntiles + e];
+  const uint32_t n1 = *(volatile const uint32_t*)(j.gerr + 7), n2 = *(volatile const uint32_t*)(j.gerr + 8);
+  for (uint32_t e = blockIdx.x; e < n1 + n2; e += gridDim.x)
+    compose_tile(j, (int)(e < n1 ? j.lzt[(size_t)j.ntiles + e] : j.lzt[(size_t)2 * j.ntiles + e - n1]));
+}
+
+__device__ __forceinline__ void compose_tile(const DecJob& j, int t) {
   const DecTile ti = j.tiles[t];
   const uint16_t* G = j.dplane + (size_t)(t * 3) * j.npix_cap;
   const uint16_t* Rp = G + j.npix_cap;
@@ -2041,30 +2068,9 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   if (!indexed) hipLaunchKernelGGL(k_dstored, dim3(S), dim3(256), 0, s, j, S);
   hipLaunchKernelGGL(k_dlz, dim3(j.ntiles), dim3(64), 0, s, j);
   ctx_mark(c, s, "dlz", false);
-  // chain tiles (the two width classes): back-distance maps, the chains, RGB -- on a second
-  // stream, concurrently with the wavefront unpredict below (disjoint tiles; both are
-  // latency-bound and leave most of the chip idle)
-  if (!w.side) {
-    if (hipStreamCreateWithFlags(&w.side, hipStreamNonBlocking) != hipSuccess) return 3;
-    if (hipEventCreateWithFlags(&w.fork, hipEventDisableTiming) != hipSuccess) return 3;
-    if (hipEventCreateWithFlags(&w.join, hipEventDisableTiming) != hipSuccess) return 3;
-  }
-  if (hipEventRecord(w.fork, s) != hipSuccess || hipStreamWaitEvent(w.side, w.fork, 0) != hipSuccess) return 3;
-  {
-    const hipStream_t s2 = w.side;
-    const int ga = (j.ntiles + 20) / 21;
-    hipLaunchKernelGGL(k_dbackmap, dim3(2 * j.ntiles), dim3(256), 0, s2, j);
-    const int we = j.W - (j.xt - 1) * j.tw;                             // the edge column's width
-    for (int cls = 1; cls <= 2; cls++) {
-      const int wc = cls == 1 ? j.tw : we;
-      if (wc % 16 == 0)
-        hipLaunchKernelGGL(k_dunpred_chain<true>, dim3(ga), dim3(64), CH_SMEM, s2, j, cls);
-      else
-        hipLaunchKernelGGL(k_dunpred_chain<false>, dim3(ga), dim3(64), CH_SMEM, s2, j, cls);
-    }
-    hipLaunchKernelGGL(k_dcompose, dim3(j.ntiles, 2), dim3(256), 0, s2, j);
-    if (hipEventRecord(w.join, s2) != hipSuccess) return 3;
-  }
+  // chain tiles: their back-distance maps (the chains themselves run inside k_dunpred_lz)
+  const int gsmall = std::min(j.ntiles, 256);
+  hipLaunchKernelGGL(k_dbackmap, dim3(gsmall), dim3(256), 0, s, j);
   hipLaunchKernelGGL(k_dunpred_fast, dim3(j.ntiles), dim3(64), (size_t)64 * ORING_PITCH + 6 * LAST_N(j.tw), s, j);
   {
     // On natural images most tiles hold copies, and a copy at a row's start that reads the end of
@@ -2075,12 +2081,21 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
     const int br_few = (int)std::min<size_t>(64, lds / rowb - 2);
     const int br_many = (int)std::min<size_t>(32, lds / rowb - 2);
     j.lzband = br_few;
-    hipLaunchKernelGGL(k_dunpred_lz, dim3(std::min(j.ntiles, LZ_FEW)), dim3(64), (size_t)(br_few + 1) * rowb, s, j,
-                       br_few, 0);
-    if (j.ntiles > LZ_FEW)
-      hipLaunchKernelGGL(k_dunpred_lz, dim3(j.ntiles), dim3(64), (size_t)(br_many + 1) * rowb, s, j, br_many, 1);
+    // + the chain tiles' workgroups (ring R >= 2w: row 0 reads T / TL from the initial half values)
+    const int we = j.W - (j.xt - 1) * j.tw;                             // the edge column's width
+    const int ga = (j.ntiles + CH_T - 1) / CH_T, gc = ga * (we != j.tw ? 2 : 1);
+    const bool r512 = 2 * j.tw <= 512;
+    const size_t cl = r512 ? ch_smem(512) : ch_smem(1024);
+    const int wf = std::min(j.ntiles, LZ_FEW), full1 = j.tw % 16 == 0, full2 = we % 16 == 0;
+    auto launch = [&](int grid, size_t band, int br, int many) {
+      const size_t l = std::max(band, cl);
+      if (r512) hipLaunchKernelGGL(k_dunpred_lz<512>, dim3(grid + gc), dim3(64), l, s, j, br, many, grid, ga, full1, full2);
+      else hipLaunchKernelGGL(k_dunpred_lz<1024>, dim3(grid + gc), dim3(64), l, s, j, br, many, grid, ga, full1, full2);
+    };
+    launch(wf, (size_t)(br_few + 1) * rowb, br_few, 0);
+    if (j.ntiles > LZ_FEW) launch(j.ntiles, (size_t)(br_many + 1) * rowb, br_many, 1);
+    hipLaunchKernelGGL(k_dcompose, dim3(gsmall), dim3(256), 0, s, j);   // the chain tiles' RGB
   }
-  if (hipStreamWaitEvent(s, w.join, 0) != hipSuccess) return 3;   // the chain tiles are done
   ctx_mark(c, s, "dunpred", false);
   if (hipGetLastError() != hipSuccess) return 3;
   if (as) {

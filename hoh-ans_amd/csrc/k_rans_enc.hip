@@ -352,8 +352,8 @@ void launch_rans_fast(const EncodeJob& j, int nplane, hipStream_t s, SidMap a, i
   const int rot = grid == nblk ? 0 : (int)((g_rot.fetch_add(1) * 8u * (unsigned)((nblk + 7) / 8)) % (unsigned)grid);
   if (kind == 0)
     hipLaunchKernelGGL(k_rans_fast<0>, dim3(grid), dim3(64), chain_lds(), s, j, nplane, a, na, b, nblk, rot);
-  else if (kind == 1)
-    hipLaunchKernelGGL(k_rans_fast<1>, dim3(grid), dim3(64), chain_lds(), s, j, nplane, a, na, b, nblk, rot);
+  else if (kind == 1)   // short or few chains (LZ / map streams, the ladder's winners): the window only
+    hipLaunchKernelGGL(k_rans_fast<1>, dim3(grid), dim3(64), WIN * 4 * 64, s, j, nplane, a, na, b, nblk, rot);
   else   // size-only trial encodes: no window; one chain per SIMD (40 KB), all at once
     hipLaunchKernelGGL(k_rans_fast<2>, dim3(grid), dim3(64), 40 * 1024, s, j, nplane, a, na, b, nblk, rot);
 }
