@@ -9,7 +9,7 @@
 //    block ahead through 32-bit offsets from one scalar base (two symbol offsets per packed
 //    16-bit shift);
 //  * the quotient floor(x/f) of the reciprocal step is computed exactly with two f64
-//    multiplications by 1/f rounded up two ulps (the high word first, then remainder*2^32 +
+//    multiplications by 1/f rounded up one ulp (the high word first, then remainder*2^32 +
 //    low word, both < 2^53: exact floors), which is mathematically identical to the Alverson
 //    reciprocal of Rans64EncPutSymbol; the new low word is x_lo + c + ql*(2^15 - f);
 //  * each step writes its speculative output word to an LDS window and adds the renorm decision
@@ -101,8 +101,9 @@ __device__ __forceinline__ void step15(Coder& c, const EncFast& e) {
   //   qh = floor(nh / f)               (nh < 2^31)
   //   rh = nh - qh*f                   (qh < 2^16, f <= 2^15: one 24-bit multiply)
   //   ql = floor((rh*2^32 + nl) / f)   (< 2^32)
-  // The quotients equal the Alverson reciprocal's: 1/f is rounded up two ulps, so m*inv >= m/f
-  // and (m/f)(1 + 2^-51) stays below floor(m/f) + 1 for m/f < 2^32 (f <= 2^15).
+  // The quotients equal the Alverson reciprocal's: inv = RN(1/f) + 1 ulp, so 1/f <= inv <=
+  // (1/f)(1 + 1.5 * 2^-52): m*inv >= m/f, and m*inv - m/f < 2^32 * 1.5 * 2^-52 < 1/f for
+  // m/f < 2^32 and f <= 2^19, so m*inv stays below floor(m/f) + 1 (m/f <= floor + 1 - 1/f).
   const double two52 = 4503599627370496.0;
   const double nhd = __builtin_bit_cast(double, ((uint64_t)0x43300000u << 32) | nh) - two52;
   const uint32_t qh = (uint32_t)__builtin_bit_cast(uint64_t, __builtin_fma(nhd, e.inv, two52));
@@ -118,8 +119,7 @@ __device__ __forceinline__ void step15(Coder& c, const EncFast& e) {
 // layer_encode.hpp:326-391, lz.hpp:100-142): the same quotients with
 // x_max = f << (63 - pb) tested as x_hi >= f << (31 - pb) (exact: f << (31 - pb) <= 2^31), the
 // low word nl + c + ql * (2^pb - f) and the high word (q * 2^pb) >> 32 = alignbit(qh, ql, 32 - pb).
-// Exactness of the f64 floors needs the numerators (< f * 2^32) times the 2.5-ulp relative error
-// of 1/f to stay below 1: f <= 2^18 (k_tables sends pb-19 streams with a larger f to k_rans_gen).
+// The f64 floors stay exact for every f <= 2^19 (step15's bound: the quotients are < 2^32).
 // Size-only encodes (SO: the ladder's trial streams) only count the emitted words.
 struct PbShape {
   uint32_t sh, M, a32;       // 31 - pb, 2^pb, 32 - pb

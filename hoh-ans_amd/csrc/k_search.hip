@@ -650,9 +650,14 @@ __global__ __launch_bounds__(64) void k_lzscan(EncodeJob j, int limit, int rp) {
       fw[c] = k <= kmax ? F[q - k * w] : 0u;
     }
     if (rp) fill_to(q >= (uint32_t)limit ? q - (uint32_t)limit : 0u, q + 260);
-    // horizontal: b = 1 .. min(limit, q), longest first, then the smallest b; stop at 259
-    uint64_t best = 0;                                                // (L << 32) | (~b)
-    for (uint32_t g0 = 1; g0 <= bm && (best >> 32) < 259; g0 += 64 * LZS_HB) {
+    // horizontal: b = 1 .. min(limit, q), longest first, then the smallest b; stop at 259.  Each
+    // lane keeps its own best key over the chunks and the wave reduces once per candidate (a
+    // reduction per chunk with hits cost ~12 cross-lane steps each: textured natural regions hit
+    // in most of the 16 chunks); a chunk in which some lane reaches 259 ends the walk, so the
+    // smallest such b wins as in the reference's short circuit (lz.hpp:47-50).
+    uint64_t mine = 0;                                                // (L << 32) | (~b)
+    bool done = false;
+    for (uint32_t g0 = 1; g0 <= bm && !done; g0 += 64 * LZS_HB) {
       if (g0 > 1) {
 #pragma unroll
         for (int c = 0; c < LZS_HB; c++) {
@@ -663,28 +668,32 @@ __global__ __launch_bounds__(64) void k_lzscan(EncodeJob j, int limit, int rp) {
       uint32_t hb = 0;                                                // lane's hits, bit c = chunk c
 #pragma unroll
       for (int c = 0; c < LZS_HB; c++) hb |= (uint32_t)(g0 + 64 * c + lane <= bm && fv[c] == f) << c;
-      for (int c = 0; c < LZS_HB; c++) {
+      for (int c = 0; c < LZS_HB && !done; c++) {
         const bool hit = (hb >> c) & 1;
-        if ((best >> 32) < 259 && __ballot(hit)) {
+        if (__ballot(hit)) {
           const uint32_t b = g0 + 64 * c + lane;
-          uint64_t key = 0;
-          if (hit) key = ((uint64_t)runl(q, b) << 32) | (uint32_t)(~b);
-          key = wmax64(key);
-          if (key > best) best = key;
+          uint32_t L = 0;
+          if (hit) {
+            L = runl(q, b);
+            const uint64_t key = ((uint64_t)L << 32) | (uint32_t)(~b);
+            if (key > mine) mine = key;
+          }
+          done = __ballot(L >= 259) != 0;
         }
       }
     }
+    uint64_t best = wmax64(mine);
     // vertical (lz.hpp:54-74): whole rows up to 65536 back, strictly longer only
     if ((best >> 32) < 259) {
-      uint64_t vb = 0;
+      uint64_t vmine = 0;
       auto vchunk = [&](uint32_t k, uint32_t fk) {
         const uint32_t b = k * w;
         const bool hit = k <= kmax && fk == f;
         if (!__ballot(hit)) return;
-        uint64_t key = 0;
-        if (hit) key = ((uint64_t)runl(q, b) << 32) | (uint32_t)(~b);
-        key = wmax64(key);
-        if (key > vb) vb = key;
+        if (hit) {
+          const uint64_t key = ((uint64_t)runl(q, b) << 32) | (uint32_t)(~b);
+          if (key > vmine) vmine = key;
+        }
       };
       uint32_t vh = 0;
 #pragma unroll
@@ -693,6 +702,7 @@ __global__ __launch_bounds__(64) void k_lzscan(EncodeJob j, int limit, int rp) {
         const uint32_t k = k0 + lane, c = (k0 - 1) / 64;
         vchunk(k, c < LZS_VB ? ((vh >> c) & 1 ? f : ~f) : (k <= kmax ? F[q - k * w] : 0u));
       }
+      const uint64_t vb = wmax64(vmine);
       if ((vb >> 32) > (best >> 32)) best = vb;
     }
     const uint32_t longest = (uint32_t)(best >> 32), bb = ~(uint32_t)best;

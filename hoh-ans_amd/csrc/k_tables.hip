@@ -180,12 +180,9 @@ __global__ __launch_bounds__(64) void k_tables(EncodeJob j, SidMap sm) {
   for (uint32_t i = lane; i < range; i += 64) fr[i] = cum[i + 1] - cum[i];
   __syncthreads();
   // ---- encoder symbol tables.  The f64-quotient chain (k_rans_fast) takes prob_bits 7..19 with
-  // range <= 512 (7: its 24-bit multiply of the high quotient; at prob_bits 19 its floors are exact
-  // only for f <= 2^18, k_rans_enc.hip stepg)
-  uint32_t fmax = 0;
-  for (uint32_t i = lane; i < range; i += 64) fmax = max(fmax, fr[i]);
-  for (int o = 32; o > 0; o >>= 1) fmax = max(fmax, (uint32_t)__shfl_xor(fmax, o));
-  const bool fast = pb >= 7 && pb <= 19 && (pb <= 18 || fmax <= (1u << 18)) && range <= HOH_FAST_RANGE && st.fast;
+  // range <= 512 (7: its 24-bit multiply of the high quotient; 19: its floors' exactness bound,
+  // k_rans_enc.hip step15)
+  const bool fast = pb >= 7 && pb <= 19 && range <= HOH_FAST_RANGE && st.fast;
   for (uint32_t i = lane; i < (fast ? (uint32_t)HOH_FAST_RANGE : range); i += 64) {
     const uint32_t f = i < range ? fr[i] : 0, c = i < range ? cum[i] : 0;
     if (fast) {
@@ -193,7 +190,7 @@ __global__ __launch_bounds__(64) void k_tables(EncodeJob j, SidMap sm) {
       if (f) {
         double inv = 1.0 / (double)f;
         unsigned long long b = __double_as_longlong(inv);
-        e.inv = __longlong_as_double((long long)(b + 2));   // round up by two ulps
+        e.inv = __longlong_as_double((long long)(b + 1));   // RN(1/f) + 1 ulp >= 1/f
       } else {
         e.inv = 1.0;
       }
