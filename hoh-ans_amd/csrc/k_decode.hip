@@ -1180,6 +1180,10 @@ __device__ __forceinline__ uint32_t as_u32d(dus2 v) { return __builtin_bit_cast(
 __device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
   return max(min(a, b), min(max(a, b), c));
 }
+// MED of plane values T, L, TL < 2^15 (prediction.hpp:21-28 computes the gradient T + L - TL in
+// uint16 arithmetic): a negative gradient wraps to >= 2^16 - 2^15 in 16 bits and to >= 2^32 - 2^15
+// in 32 bits, above max(T, L) either way, so the 32-bit wrap gives the same median without a mask
+__device__ __forceinline__ uint32_t medp(uint32_t T, uint32_t L, uint32_t TL) { return med3u(T, L, T + L - TL); }
 
 #define UP_P 8   // steps per residual group (one 16-B residual piece per lane and plane)
 // LDS row of the output column ring: two halves of 64 columns x 3 B, each followed by a 4-byte pad
@@ -1313,7 +1317,7 @@ __device__ __forceinline__ void dunpred_fast_tile(const DecJob& j, const DecTile
         // R' residual in the low half, B' in the high half: one byte permute
         const uint32_t rRB = __builtin_amdgcn_perm(qB[u >> 1], qR[u >> 1], (u & 1) ? 0x07060302u : 0x05040100u);
         const uint32_t TG = wave_shr1(cG, oGs[u]), TRB = wave_shr1(cRB, oRBs[u]);
-        const uint32_t vG = (rG + med3u(TG, cG, (TG + cG - pG) & 0xffffu) + 128u) & 255u;
+        const uint32_t vG = (rG + medp(TG, cG, pG) + 128u) & 255u;
         const dus2 t2 = as_d2(TRB), l2 = as_d2(cRB);
         const dus2 g2 = t2 + l2 - as_d2(pRB);
         const dus2 m2 = __builtin_elementwise_max(__builtin_elementwise_min(t2, l2),
@@ -1428,9 +1432,9 @@ __device__ __forceinline__ uint32_t unpred_px(uint32_t T, uint32_t L, uint32_t T
   const uint32_t tg = T & 255, lg = L & 255, ag = TL & 255;
   const uint32_t tr = (T >> 8) & 511, lr = (L >> 8) & 511, ar = (TL >> 8) & 511;
   const uint32_t tb = T >> 17, lb = L >> 17, ab = TL >> 17;
-  const uint32_t g = ((r & 255) + med3u(tg, lg, (tg + lg - ag) & 0xffffu) + 128u) & 255u;
-  const uint32_t rr = (((r >> 8) & 511) + med3u(tr, lr, (tr + lr - ar) & 0xffffu) + 256u) & 511u;
-  const uint32_t bb = ((r >> 17) + med3u(tb, lb, (tb + lb - ab) & 0xffffu) + 256u) & 511u;
+  const uint32_t g = ((r & 255) + medp(tg, lg, ag) + 128u) & 255u;
+  const uint32_t rr = (((r >> 8) & 511) + medp(tr, lr, ar) + 256u) & 511u;
+  const uint32_t bb = ((r >> 17) + medp(tb, lb, ab) + 256u) & 511u;
   return g | (rr << 8) | (bb << 17);
 }
 
@@ -1662,15 +1666,15 @@ __device__ void lds_st4(uint32_t, uint4);
 #endif
 
 // LDS map (byte addresses; no static LDS): value rings of CH_R u16 at lane * CH_VS, residual
-// rings of 64 entries + the mirror of entry 0 (entries k and k + 1 always adjacent) at
-// CH_RES_OFF + lane * CH_QS, the abort word last.  The lane strides are an odd number of dwords:
+// rings of 64 entries + a mirror of entries 0..15 (a block's 16 entries k.. are always
+// contiguous) at CH_RES_OFF + lane * CH_QS, the abort word last.  The lane strides are an odd number of dwords:
 // the lanes' rings start on different banks, so the wave's same-offset accesses (T, the ring
 // store, every step) are conflict-free (a 2 KB stride put all 63 lanes on one bank).
 // CH_T tiles per wave (lanes 3q + p < 3 CH_T): 35 KB of LDS with R = 512, so the launch
 // co-resides with the other kernels of images in flight (21 tiles needed 137 KB, a whole CU's).
 #define CH_T 10
 #define CH_L (3 * CH_T)
-#define CH_QS 148
+#define CH_QS 164
 __host__ __device__ constexpr uint32_t ch_vs(int R) { return (uint32_t)R * 2 + 4; }
 __host__ __device__ constexpr uint32_t ch_res_off(int R) { return CH_L * ch_vs(R); }
 __host__ __device__ constexpr uint32_t ch_scr(int R) { return ch_res_off(R) + CH_L * CH_QS; }
@@ -1710,7 +1714,10 @@ __device__ void chain_tiles(const DecJob& j, int cls, uint32_t blk) {
     const uint32_t v[8] = {a.x, a.y, a.z, a.w, b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
     for (int e = 0; e < 8; e++) lds_st32(qb + 2 * s0 + 4 * e, v[e]);
-    if (s0 == 0) lds_st16(qb + 128, a.x);                              // mirror of entry 0
+    if (s0 == 0) {                                                     // the mirror (entries 64..79)
+#pragma unroll
+      for (int e = 0; e < 8; e++) lds_st32(qb + 128 + 4 * e, v[e]);
+    }
   };
   // residual ring: entries [k, kfill) resident, the next 16 in flight (pend) when hp
   uint32_t k = 0, kfill = 32;
@@ -1748,44 +1755,44 @@ __device__ void chain_tiles(const DecJob& j, int cls, uint32_t blk) {
         const uint32_t pos0 = i0 & (CH_R - 1);
         const uint32_t tA = rb + 2 * ((pos0 - w) & (CH_R - 1));        // T of step u at tA + 2u
         const uint32_t wA = rb + 2 * pos0;                             // this block's slots
-        // the 16 steps, specialised on whether a copy source can wrap around the ring (b <= 255)
+        // the 16 steps, specialised on whether a copy source can wrap around the ring (b <= 255).
+        // The block's residuals are ring entries k .. k + 15, contiguous thanks to the mirror: the
+        // next step's entry is known from the byte map alone (d counts this block's non-copy
+        // steps), so every read of step u + 1 is issued before step u's arithmetic.  A copy with
+        // b <= 1 reads a harmless slot of its own ring (b = 0 uses the MED value, b = 1 uses L).
         auto block = [&](auto nowrap_c) {
           constexpr bool NOWRAP = decltype(nowrap_c)::value;
           auto srcA = [&](int u, uint32_t b) -> uint32_t {
             return NOWRAP ? wA + 2 * u - 2 * b : rb + 2 * ((pos0 + (uint32_t)u - b) & (CH_R - 1));
           };
+          const uint32_t qk = qb + 2 * (k & 63);
+          uint32_t d = 0;
           // step 0 reads its copy source after every earlier write, so even b = 1 comes from the
           // ring (at a row's start that is the end of the row above, not L = half)
           uint32_t b = bw[0] & 255u;
-          uint32_t T = lds_u16(tA), vC = lds_u16(srcA(0, b ? b : 1));
-          uint32_t ra = lds_u16(qb + 2 * (k & 63)), rbv = lds_u16(qb + 2 * (k & 63) + 2);
-          bool pcopy = true;                                           // r = ra for step 0 (k is current)
+          uint32_t T = lds_u16(tA), vC = lds_u16(srcA(0, b ? b : 1)), r = lds_u16(qk);
 #pragma unroll
           for (int u = 0; u < 16; u++) {
-            // the next step's reads first (its copy source, when it is not this step's pixel, was
-            // written by an earlier step; its residual is entry k or k + 1)
-            uint32_t bn = 0, Tn = 0, vCn = 0, ran = 0, rbn = 0;
+            const uint32_t dn = d + (b == 0 ? 1u : 0u);
+            uint32_t bn = 0, Tn = 0, vCn = 0, rn = 0;
             if (u < 15) {
               bn = (bw[(u + 1) >> 2] >> (8 * ((u + 1) & 3))) & 255u;
               Tn = lds_u16(tA + 2 * (u + 1));
-              vCn = lds_u16(srcA(u + 1, bn < 2 ? 2 : bn));
-              ran = lds_u16(qb + 2 * (k & 63));
-              rbn = lds_u16(qb + 2 * (k & 63) + 2);
+              vCn = lds_u16(srcA(u + 1, bn));
+              rn = lds_u16(qk + 2 * dn);
             }
-            const uint32_t r = pcopy ? ra : rbv;
-            const uint32_t pr = med3u(T, L, (T + L - Tp) & 0xffffu);
+            const uint32_t pr = medp(T, L, Tp);
             uint32_t vm = (r + pr + half) & cm, vc = (u > 0 && b == 1) ? L : vC;
             // both values, then a select: left to itself the compiler branches around the MED
             // (exec-mask juggling on every step of a divergent wave)
             asm volatile("" : "+v"(vm), "+v"(vc));
             const uint32_t v = b ? vc : vm;
-            k += b ? 0u : 1u;
-            pcopy = b != 0;
             lds_st16(wA + 2 * u, v);
             Tp = T;
             L = v;
-            b = bn; T = Tn; vC = vCn; ra = ran; rbv = rbn;
+            b = bn; T = Tn; vC = vCn; r = rn; d = dn;
           }
+          k += d;
         };
         if (pos0 >= 256) block(std::true_type{});                       // i - b >= 1 for every b <= 255
         else block(std::false_type{});
@@ -1805,7 +1812,7 @@ __device__ void chain_tiles(const DecJob& j, int cls, uint32_t blk) {
             const uint32_t vC = lds_u16(rb + 2 * ((i - b) & (CH_R - 1)));
             const uint32_t T = lds_u16(rb + 2 * ((i - w) & (CH_R - 1)));
             const uint32_t r = lds_u16(qb + 2 * (k & 63));
-            const uint32_t pr = med3u(T, L, (T + L - Tp) & 0xffffu);
+            const uint32_t pr = medp(T, L, Tp);
             const uint32_t vm = (r + pr + half) & cm;
             const uint32_t v = b ? vC : vm;
             k += b ? 0u : 1u;
@@ -1836,6 +1843,44 @@ __device__ __forceinline__ void compose_tile(const DecJob& j, int t) {
   const uint16_t* Rp = G + j.npix_cap;
   const uint16_t* Bp = Rp + j.npix_cap;
   const uint32_t w = ti.w, npix = w * ti.h;
+  if ((w & 15) == 0 && (j.W & 15) == 0 && (ti.x0 & 15) == 0 && ((uintptr_t)j.rgb & 15) == 0) {
+    // 16 pixels per thread: 32 B of each plane in, 48 B of RGB out as three 16-B stores (the
+    // plane offsets are multiples of 64 values, the RGB rows and groups 16-B aligned)
+    for (uint32_t i0 = threadIdx.x * 16; i0 < npix; i0 += 256 * 16) {
+      const uint32_t yy = i0 / w, xx = i0 - yy * w;
+      const uint4* g4 = (const uint4*)(G + i0);
+      const uint4* r4 = (const uint4*)(Rp + i0);
+      const uint4* b4 = (const uint4*)(Bp + i0);
+      const uint4 ga = g4[0], gb = g4[1], ra = r4[0], rb = r4[1], ba = b4[0], bb = b4[1];
+      const uint32_t gw[8] = {ga.x, ga.y, ga.z, ga.w, gb.x, gb.y, gb.z, gb.w};
+      const uint32_t rw[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
+      const uint32_t bw[8] = {ba.x, ba.y, ba.z, ba.w, bb.x, bb.y, bb.z, bb.w};
+      uint32_t px[16];                                  // 0x00BBGGRR
+#pragma unroll
+      for (int m = 0; m < 16; m++) {
+        const uint32_t sh = 16 * (m & 1);
+        const uint32_t g = (gw[m >> 1] >> sh) & 0xffffu;
+        const uint32_t r = ((rw[m >> 1] >> sh) + g) & 255u, b = ((bw[m >> 1] >> sh) + g) & 255u;   // -256: mod 256
+        px[m] = r | (g << 8) | (b << 16);
+      }
+      uint32_t o[12];
+#pragma unroll
+      for (int k = 0; k < 12; k++) {
+        uint32_t d = 0;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+          const int mb = 4 * k + c;
+          d |= ((px[mb / 3] >> (8 * (mb % 3))) & 255u) << (8 * c);
+        }
+        o[k] = d;
+      }
+      uint4* out = (uint4*)(j.rgb + ((size_t)(ti.y0 + yy) * j.W + ti.x0 + xx) * 3);
+      out[0] = make_uint4(o[0], o[1], o[2], o[3]);
+      out[1] = make_uint4(o[4], o[5], o[6], o[7]);
+      out[2] = make_uint4(o[8], o[9], o[10], o[11]);
+    }
+    return;
+  }
   for (uint32_t i = threadIdx.x; i < npix; i += 256) {
     const uint32_t yy = i / w, xx = i - yy * w;
     uint8_t* o = j.rgb + ((size_t)(ti.y0 + yy) * j.W + ti.x0 + xx) * 3;

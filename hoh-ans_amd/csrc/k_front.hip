@@ -462,34 +462,39 @@ __device__ __forceinline__ uint32_t wshr1(uint32_t v, uint32_t old) {   // lane 
 }
 __device__ __forceinline__ uint32_t lane_of(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
-// lookup of key k in a (read-only) table: true if present
-__device__ __forceinline__ bool wt_find(const uint32_t* key, uint32_t k) {
+// slot of key k in a (read-only) table, F2_TAB if absent
+__device__ __forceinline__ uint32_t wt_find(const uint32_t* key, uint32_t k) {
   uint32_t sl = (k >> 1) & (F2_TAB - 1);
   for (int probe = 0; probe < F2_TAB; probe++) {
     const uint32_t o = key[sl];
-    if (o == k) return true;
-    if (o == 0u) return false;
-    sl = (sl + 1) & (F2_TAB - 1);
-  }
-  return false;
-}
-
-// insert into a chunk table (open addressing); returns the slot (F2_TAB if none); a key met a
-// second time sets the slot's duplicate bit
-__device__ __forceinline__ uint32_t wt_put(uint32_t* key, uint32_t* dup, uint32_t k) {
-  uint32_t sl = (k >> 1) & (F2_TAB - 1);
-  for (int probe = 0; probe < F2_TAB; probe++) {
-    const uint32_t old = atomicCAS(&key[sl], 0u, k);
-    if (old == 0u) return sl;
-    if (old == k) { atomicOr(&dup[sl >> 5], 1u << (sl & 31)); return sl; }
+    if (o == k) return sl;
+    if (o == 0u) return F2_TAB;
     sl = (sl + 1) & (F2_TAB - 1);
   }
   return F2_TAB;
 }
 
+// insert into a chunk table (open addressing, one slot per distinct key); returns the slot
+// (F2_TAB if none)
+__device__ __forceinline__ uint32_t wt_put(uint32_t* key, uint32_t k) {
+  uint32_t sl = (k >> 1) & (F2_TAB - 1);
+  for (int probe = 0; probe < F2_TAB; probe++) {
+    const uint32_t old = atomicCAS(&key[sl], 0u, k);
+    if (old == 0u || old == k) return sl;
+    sl = (sl + 1) & (F2_TAB - 1);
+  }
+  return F2_TAB;
+}
+
+// the lanes that hold a slot's key: {max lane, 63 - min lane}, both by LDS max (cleared to 0)
+__device__ __forceinline__ void wt_lanes(uint32_t* pos, uint32_t sl, uint32_t lane) {
+  __hip_atomic_fetch_max(&pos[2 * sl], lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __hip_atomic_fetch_max(&pos[2 * sl + 1], 63u - lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 __global__ __launch_bounds__(NT) void k_front256(EncodeJob j) {
   __shared__ uint32_t tab[4][2][F2_TAB + 1];        // per wave: two alternating chunk tables
-  __shared__ uint32_t tdup[4][2][F2_TAB / 32];
+  __shared__ __attribute__((aligned(8))) uint32_t tpos[4][2][2 * (F2_TAB + 1)];   // wt_lanes per slot
   __shared__ uint32_t pring[4][F2_RING];
   __shared__ uint32_t hist[3 * 512 - 256];
   __shared__ int s_notgrey, s_ncand;
@@ -499,7 +504,7 @@ __global__ __launch_bounds__(NT) void k_front256(EncodeJob j) {
   const uint32_t npix = 256u * 256u;
   for (int i = tid; i < 3 * 512 - 256; i += NT) hist[i] = 0;
   for (int i = lane; i < 2 * (F2_TAB + 1); i += 64) tab[wv][i / (F2_TAB + 1)][i % (F2_TAB + 1)] = 0;
-  if (lane < 2 * (F2_TAB / 32)) tdup[wv][lane / (F2_TAB / 32)][lane % (F2_TAB / 32)] = 0;
+  for (int i = lane; i < 4 * (F2_TAB + 1); i += 64) tpos[wv][i / (2 * (F2_TAB + 1))][i % (2 * (F2_TAB + 1))] = 0;
   if (tid == 0) { s_notgrey = 0; s_ncand = 0; }
   uint16_t* res0 = j.sym + med_plane_off(j, t, 0);
   uint16_t* res1 = j.sym + med_plane_off(j, t, 1);
@@ -542,7 +547,8 @@ __global__ __launch_bounds__(NT) void k_front256(EncodeJob j) {
       const uint32_t a2 = wshl1(a1, lane_of(cur[0], 1));
       const uint32_t a3 = wshl1(a2, lane_of(cur[0], 2));
       const uint32_t k = fp32(pv, a1, a2, a3);
-      slot_prev = wt_put(tab[wv][1], tdup[wv][1], k);
+      slot_prev = wt_put(tab[wv][1], k);
+      if (slot_prev < F2_TAB) wt_lanes(tpos[wv][1], slot_prev, lane);
       ring[(uint32_t)(ya * 256 - 64 + lane) & (F2_RING - 1)] = pv;
     }
     ring[(uint32_t)(ya * 256 + lane) & (F2_RING - 1)] = cur[0];
@@ -587,22 +593,38 @@ __global__ __launch_bounds__(NT) void k_front256(EncodeJob j) {
       const bool win = q + 3 < npix;
       const uint32_t hq = win ? fp32(v, v1, v2, v3) : 0u;
       uint32_t* tc = tab[wv][cb];
-      uint32_t* dc = tdup[wv][cb];
+      uint32_t* pc = tpos[wv][cb];
       const uint32_t* tp = tab[wv][cb ^ 1];
-      const bool inprev = hq && wt_find(tp, hq);
-      const uint32_t sq = hq ? wt_put(tc, dc, hq) : F2_TAB;
-      const bool hit = inprev || (sq < F2_TAB && ((dc[sq >> 5] >> (sq & 31)) & 1));
-      const uint64_t flag = __ballot(hit);
+      const uint32_t* pp = tpos[wv][cb ^ 1];
+      const uint32_t sq = hq ? wt_put(tc, hq) : F2_TAB;
+      if (sq < F2_TAB) wt_lanes(pc, sq, lane);
+      const uint32_t sp = hq ? wt_find(tp, hq) : F2_TAB;
+      // Equal windows have equal fingerprints, so the windows before q equal to q's can only be
+      // at the positions holding hq: in this chunk at lanes min..lane-1 (the earliest is checked),
+      // in the previous chunk at lanes >= lane (distance <= 64; the latest, i.e. nearest, is
+      // checked).  When a checked window differs (a fingerprint collision) the lane falls back
+      // to the full test over b = 1..64 (lz.hpp:37-42 with offset < 4).
+      const uint32_t fcur = sq < F2_TAB ? 63u - pc[2 * sq + 1] : 64u;
+      const uint32_t lprev = sp < F2_TAB ? pp[2 * sp] : 0u;
+      const bool ccur = fcur < (uint32_t)lane, cprev = sp < F2_TAB && lprev >= (uint32_t)lane;
+      const uint64_t flag = __ballot(ccur || cprev);
       uint64_t word = 0;
       if (flag) {
-        // exact check (lz.hpp:37-42 with offset < 4), first back distance that matches
-        bool c = false;
-        if (hit) {
-          const uint32_t bmax = q < 64 ? q : 64;
-          for (uint32_t b = 1; b <= bmax && !c; b++) {
-            const uint32_t p = q - b;
-            c = ring[p & (F2_RING - 1)] == v && ring[(p + 1) & (F2_RING - 1)] == v1 &&
-                ring[(p + 2) & (F2_RING - 1)] == v2 && ring[(p + 3) & (F2_RING - 1)] == v3;
+        auto same = [&](uint32_t p) {
+          return ring[p & (F2_RING - 1)] == v && ring[(p + 1) & (F2_RING - 1)] == v1 &&
+                 ring[(p + 2) & (F2_RING - 1)] == v2 && ring[(p + 3) & (F2_RING - 1)] == v3;
+        };
+        const uint32_t q0 = q - lane;
+        bool c = false, full = false;
+        if (ccur || cprev) {
+          c = same(ccur ? q0 + fcur : q0 - 64u + lprev);
+          if (!c && ccur && cprev) c = same(q0 - 64u + lprev);
+          full = !c;
+        }
+        if (__ballot(full)) {
+          if (full) {
+            const uint32_t bmax = q < 64 ? q : 64;
+            for (uint32_t b = 1; b <= bmax && !c; b++) c = same(q - b);
           }
         }
         word = __ballot(c);
@@ -612,7 +634,7 @@ __global__ __launch_bounds__(NT) void k_front256(EncodeJob j) {
       // empty the previous chunk's table for the next chunk (wave-ordered: every lookup is done)
       uint32_t* tpw = tab[wv][cb ^ 1];
       tpw[slot_prev] = 0;                             // slot F2_TAB is a spare: no branch
-      if (lane < F2_TAB / 32) tdup[wv][cb ^ 1][lane] = 0;
+      *(uint2*)&tpos[wv][cb ^ 1][2 * slot_prev] = make_uint2(0u, 0u);
       slot_prev = sq;
       cb ^= 1;
     }

@@ -24,7 +24,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIBPATH = os.path.join(os.path.dirname(HERE), "lib", "libhohgpu.so")
+LIBPATH = os.environ.get("HOH_LIB") or os.path.join(os.path.dirname(HERE), "lib", "libhohgpu.so")  # HOH_LIB: A/B builds
 
 HOH_OK = 0
 ERRNAMES = {1: "E_ARG", 2: "E_CAP", 3: "E_HIP", 4: "E_RANGE", 5: "E_UNREPRODUCIBLE", 6: "E_UNSUPPORTED",
