@@ -65,7 +65,7 @@ struct hoh_ctx {
   Buf idx8, fpb, pinfo, lg;     // -s>=1 workspaces
   uint32_t lg_key[4] = {0, 0, 0, 0};
   uint64_t lg_off[4] = {0, 0, 0, 0};
-  Buf sym, hist, candbits, matches, pal, streams, tiles, hdr, tab_fast, tab_gen, slabs, ckpt, misc, tsizes;
+  Buf sym, hist, candbits, matches, lzspec, pal, streams, tiles, hdr, tab_fast, tab_gen, slabs, ckpt, misc, tsizes;
   DecWork dec;                  // decoder workspaces (k_decode.hip)
   uint64_t* pinned = nullptr;   // small host staging (status words, sizes)
   int profiling = 0;
@@ -166,7 +166,7 @@ static void freebuf(Buf& b) { if (b.p) (void)hipFree(b.p); b.p = nullptr; b.n = 
 void hoh_ctx_destroy(hoh_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  Buf* all[] = {&c->idx8, &c->fpb, &c->pinfo, &c->lg, &c->sym, &c->hist, &c->candbits, &c->matches, &c->pal, &c->streams, &c->tiles, &c->hdr,
+  Buf* all[] = {&c->idx8, &c->fpb, &c->pinfo, &c->lg, &c->sym, &c->hist, &c->candbits, &c->matches, &c->lzspec, &c->pal, &c->streams, &c->tiles, &c->hdr,
                 &c->tab_fast, &c->tab_gen, &c->slabs, &c->ckpt, &c->misc, &c->tsizes};
   for (Buf* b : all) freebuf(*b);
   for (Buf& b : c->scr.chunks) freebuf(b);
@@ -202,6 +202,15 @@ int hoh_get_kernel_stats(hoh_ctx* c, const char** names, double* total_ms, uint6
     if (count) count[k] = c->scount[k];
   }
   return k;
+}
+
+// measurement only (not in include/): copy a workspace of the last encode to the host
+// (0: the LZ match lists, 1: k_lz's segment walks)
+extern "C" int hoh_debug_read(hoh_ctx* c, int which, void* dst, size_t bytes) {
+  if (!c || !dst) return HOH_E_ARG;
+  const Buf& b = which == 0 ? c->matches : c->lzspec;
+  if (bytes > b.n || !b.p) return HOH_E_ARG;
+  return hipMemcpy(dst, b.p, bytes, hipMemcpyDeviceToHost) == hipSuccess ? HOH_OK : HOH_E_HIP;
 }
 
 void hoh_reset_kernel_stats(hoh_ctx* c) {
@@ -361,6 +370,7 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   if ((e = ensure(c->hist, S * 512 * 4))) return e;
   if ((e = ensure(c->candbits, (size_t)ntiles * (j.npix_cap / 64) * 8))) return e;
   if ((e = ensure(c->matches, (size_t)ntiles * 3 * (j.lz_cap + 1) * 4))) return e;
+  if (!speed && (e = ensure(c->lzspec, (size_t)ntiles * j.lz_cap * 4))) return e;
   if ((e = ensure(c->pal, (size_t)ntiles * 257 * 4))) return e;   // palettes, then colour counts
   if ((e = ensure(c->streams, S * sizeof(StreamInfo)))) return e;
   if ((e = ensure(c->tiles, (size_t)ntiles * sizeof(TileInfo)))) return e;
@@ -373,6 +383,7 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   j.hist = (uint32_t*)c->hist.p;
   j.candbits = (uint64_t*)c->candbits.p;
   j.matches = (uint32_t*)c->matches.p;
+  j.lzspec = (uint32_t*)c->lzspec.p;
   j.palette = (uint32_t*)c->pal.p;
   j.ncol = (int32_t*)c->pal.p + (size_t)ntiles * 256;
   j.streams = (StreamInfo*)c->streams.p;

@@ -115,6 +115,22 @@ struct EncGen {           // generic encoder symbol: rans64.hpp Rans64EncSymbol 
   uint32_t freq, bias, cmpl, shift;
 };
 
+#ifdef __HIPCC__
+// maximum over the 64 lanes (every lane active), in registers: DPP within rows of 16 (xor 1,
+// xor 2, half mirror, mirror), then the four row maxima by readlane (a __shfl_xor tree is 6
+// dependent LDS permute round trips per call; the scan calls this once per candidate)
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xf, 0xf, false));
+  const uint32_t a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
+  const uint32_t c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
+  return max(max(a, b), max(c, d));
+}
+
+#endif
+
 __host__ __device__ inline uint32_t hoh_varint_len(uint64_t v) {
   return v < (1u << 7) ? 1u : v < (1u << 14) ? 2u : v < (1u << 21) ? 3u : 0u;   // varint.hpp:29-45 (Q2)
 }
@@ -156,6 +172,7 @@ struct EncodeJob {
   uint32_t* hist;         // [stream][512]
   uint64_t* candbits;     // [tile][npix_cap/64] LZ candidate bitmap
   uint32_t* matches;      // [tile][lz_cap] packed (pos, len, back) triples (3 words each)
+  uint32_t* lzspec;       // [tile][lz_cap] k_lz's segment walks: pos | (len - 4) << 16 | (back - 1) << 24
   uint32_t* palette;      // [tile][256] colours in first-occurrence order (palette tiles)
   int32_t* ncol;          // [tile] distinct colours (<= 256) or -1 (k_colours)
   uint8_t* idx8;          // -s>=1: [tile][npix_cap] palette indices (the indexed plane's data)

@@ -14,21 +14,34 @@ __device__ __forceinline__ uint32_t img_px(const EncodeJob& j, int x0, int y0, i
   return p[0] | (p[1] << 8) | (p[2] << 16);
 }
 
-__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
-  for (int o = 32; o > 0; o >>= 1) {
-    uint64_t u = __shfl_xor(v, o);
-    v = u > v ? u : v;
-  }
-  return v;
-}
-
-#define LZR 2048          // pixel ring of k_lz (positions p & (LZR - 1))
+#ifndef LZ_SEG
+#define LZ_SEG 4          // waves per tile (segments scanned speculatively, section below)
+#endif
+#ifndef LZ_FILL
+#define LZ_FILL 4         // 64-position chunks per batch of ring loads
+#endif
+#define LZR (LZ_FILL >= 4 ? 1024 : 512)   // pixel ring of a k_lz wave: [q - 64, q + 260 + 64 LZ_FILL)
 
 #define LZ_BITS_MAX 1024   // candidate words kept in LDS (tiles up to 65,536 pixels)
-__global__ __launch_bounds__(64) void k_lz(EncodeJob j) {
-  __shared__ uint32_t ring[LZR];
+// The greedy walk is serial (the next decision is at the first candidate after the last match),
+// but the walk from any position is a function of that position alone, so a tile is cut into
+// LZ_SEG segments of whole 64-position words walked at once, each from its own first position
+// (one wave each, matches packed into lzspec), every visited candidate marked in an LDS bitmap.
+// Wave 0 then stitches: segment s's true walk enters at the exit of s - 1's; from there it is
+// re-walked until it reaches a candidate segment s's own walk visited (from then on the two
+// coincide: that walk's matches from this candidate on, and its exit, are the true ones) or
+// leaves the segment.  Matches are decided exactly as before, so the list is the serial one.
+__global__ __launch_bounds__(64 * LZ_SEG) void k_lz(EncodeJob j) {
+  __shared__ uint32_t ring[LZ_SEG][LZR];
   __shared__ uint64_t cbits[LZ_BITS_MAX];
-  const int t = blockIdx.x, lane = threadIdx.x;
+  __shared__ uint32_t vis[2 * LZ_BITS_MAX];          // visited candidates (segmented walks only)
+  __shared__ uint32_t s_cnt[LZ_SEG], s_exit[LZ_SEG];
+#ifdef LZ_DBG
+  __shared__ uint32_t s_dbg[LZ_SEG][3];
+  const uint64_t dbg_t0 = __builtin_amdgcn_s_memrealtime();
+  uint32_t dbg_vis = 0, dbg_fix = 0, dbg_rounds = 0;
+#endif
+  const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   TileInfo ti = j.tiles[t];
   const uint32_t npix = (uint32_t)ti.w * ti.h;
   const uint32_t nwords = (npix + 63) / 64;
@@ -42,81 +55,194 @@ __global__ __launch_bounds__(64) void k_lz(EncodeJob j) {
     else if (ti.colours <= 32) bonus = 2;
   }
   const uint32_t thr = 4 + bonus;
-  uint32_t nm = 0, pos = 0;
-  bool overflow = false;
-  // The run lengths compare pixels q + k with q + k - b (b <= 64, k < 259): they come from an LDS
-  // ring holding the tile positions [wlo, wend) (wend - wlo <= LZR), loaded 64 at a time as the
-  // scan moves and only around candidates (each pixel read from memory at most once per tile;
-  // natural tiles hold thousands of copies and per-step global reads made this kernel ~16 ms
-  // per image)
+  // the candidate bitmap in LDS: the scan searches it once per step (natural tiles: thousands)
+  const bool lds_bits = nwords <= LZ_BITS_MAX;
+  // segmented walks need the LDS bitmaps and 16-bit positions (lzspec entries)
+  const uint32_t nseg = (lds_bits && nwords >= 4 * LZ_SEG) ? LZ_SEG : 1;
+  const uint32_t segcap = j.lz_cap / LZ_SEG;
+  uint32_t* spec = j.lzspec + (size_t)t * j.lz_cap;
+  auto seg_lo = [&](uint32_t s) { return s >= nseg ? npix : (nwords * s / nseg) * 64; };
+  if (ti.ncand) {
+    for (uint32_t i = tid; i < nwords; i += 64 * LZ_SEG) cbits[i] = lds_bits ? bits[i] : 0;
+    if (nseg > 1)
+      for (uint32_t i = tid; i < 2 * nwords; i += 64 * LZ_SEG) vis[i] = 0;
+  }
+  __syncthreads();
+  // The run lengths compare pixels q + k with q + k - b (b <= 64, k < 259): they come from the
+  // wave's LDS ring holding the tile positions [wlo, wend) (wend - wlo <= LZR), loaded 256 at a
+  // time as the scan moves and only around candidates (natural tiles hold thousands of copies and
+  // per-step global reads made this kernel ~16 ms per image)
+  uint32_t* rg = ring[wv];
+  const int x0 = ti.x0, y0 = ti.y0, tw = ti.w;
   uint32_t wend = 0;
   auto fill_to = [&](uint32_t lo, uint32_t need) {
     if (lo > wend) wend = lo & ~63u;                  // nothing needed in between
-    while (wend < need) {
-      const uint32_t p = wend + (uint32_t)lane;
-      ring[p & (LZR - 1)] = p < npix ? img_px(j, ti.x0, ti.y0, ti.w, p) : 0xff000000u;
-      wend += 64;
+    while (wend < need) {                             // 64 LZ_FILL positions per batch of loads
+      // unconditional loads (positions past the tile read its last pixel and are replaced after):
+      // a load under a lane condition is awaited inside its branch, one round trip per chunk
+      uint32_t v[LZ_FILL];
+#pragma unroll
+      for (int u = 0; u < LZ_FILL; u++) v[u] = img_px(j, x0, y0, tw, min(wend + 64u * u + (uint32_t)lane, npix - 1));
+#pragma unroll
+      for (int u = 0; u < LZ_FILL; u++) {
+        const uint32_t p = wend + 64u * u + (uint32_t)lane;
+        rg[p & (LZR - 1)] = p < npix ? v[u] : 0xff000000u;
+      }
+      wend += 64 * LZ_FILL;
     }
-    __syncthreads();
+    // the wave's own ring: its LDS accesses are ordered without a barrier
   };
-  // the candidate bitmap in LDS: the scan searches it once per step (natural tiles: thousands)
-  const bool lds_bits = nwords <= LZ_BITS_MAX;
-  if (ti.ncand && lds_bits) {
-    for (uint32_t i = lane; i < nwords; i += 64) cbits[i] = bits[i];
-    __syncthreads();
-  }
-  if (ti.ncand) {
-    while (pos < npix) {
-      // next candidate q >= pos
-      uint32_t q = 0xffffffffu;
-      for (uint32_t wi = pos >> 6; wi < nwords; wi += 64) {
-        uint64_t wv = (wi + lane < nwords) ? (lds_bits ? cbits[wi + lane] : bits[wi + lane]) : 0;
-        if (wi + lane == (pos >> 6)) wv &= ~0ull << (pos & 63);
-        uint64_t bal = __ballot(wv != 0);
-        if (bal) {
-          int l = __ffsll((unsigned long long)bal) - 1;
-          uint64_t word = __shfl(wv, l);
-          q = (wi + l) * 64 + (__ffsll((unsigned long long)word) - 1);
-          break;
-        }
+  uint32_t cwi = 0xffffffffu;                         // the bitmap word last read, kept in registers
+  uint64_t cw = 0;
+  // first candidate q >= pos (0xffffffff: none)
+  auto next_cand = [&](uint32_t pos) -> uint32_t {
+    if (pos >= npix) return 0xffffffffu;
+    if (lds_bits) {                                   // usually in pos's own word
+      if ((pos >> 6) != cwi) { cwi = pos >> 6; cw = cbits[cwi]; }
+      const uint64_t wv2 = cw & (~0ull << (pos & 63));
+      if (wv2) return (pos & ~63u) + (uint32_t)(__ffsll((unsigned long long)wv2) - 1);
+    }
+    for (uint32_t wi = pos >> 6; wi < nwords; wi += 64) {
+      uint64_t w2 = (wi + lane < nwords) ? (lds_bits ? cbits[wi + lane] : bits[wi + lane]) : 0;
+      if (wi + lane == (pos >> 6)) w2 &= ~0ull << (pos & 63);
+      const uint64_t bal = __ballot(w2 != 0);
+      if (bal) {
+        const int l = __ffsll((unsigned long long)bal) - 1;
+        const uint64_t word = __shfl(w2, l);
+        return (wi + l) * 64 + (__ffsll((unsigned long long)word) - 1);
       }
-      if (q == 0xffffffffu) break;
-      fill_to(q >= 64 ? q - 64 : 0, q + 260);
-      const uint32_t b = lane + 1;
-      uint32_t L = 0;
-      if (b <= q) {
-        // eight positions per LDS round trip (a flat region's copies run to the 259 cap)
-        const uint32_t lim = min(259u, npix - q);
-        bool go = true;
-        while (go && L < lim) {
-          uint32_t a[8], c[8];
+    }
+    return 0xffffffffu;
+  };
+  // (longest, smallest back) at candidate q, lz.hpp:35-53: lane = back - 1
+  auto measure = [&](uint32_t q) -> uint32_t {
+    fill_to(q >= 64 ? q - 64 : 0, q + 260);
+    const uint32_t b = lane + 1;
+    uint32_t L = 0;
+    if (b <= q) {
+      // sixteen positions per LDS round trip (a flat region's copies run to the 259 cap), the
+      // equal positions as a bit mask whose trailing ones are the run
+      const uint32_t lim = min(259u, npix - q);
+      for (;;) {
+        uint32_t a[16], c[16];
 #pragma unroll
-          for (int u = 0; u < 8; u++) {
-            a[u] = ring[(q + L + u) & (LZR - 1)];
-            c[u] = ring[(q + L + u - b) & (LZR - 1)];
-          }
-#pragma unroll
-          for (int u = 0; u < 8; u++) {
-            if (go && L < lim && a[u] == c[u]) L++;
-            else go = false;
-          }
+        for (int u = 0; u < 16; u++) {
+          a[u] = rg[(q + L + u) & (LZR - 1)];
+          c[u] = rg[(q + L + u - b) & (LZR - 1)];
         }
+        uint32_t m = 0;                               // bits 16.. of ~m stop the count at 16
+#pragma unroll
+        for (int u = 0; u < 16; u++) m |= (uint32_t)(a[u] == c[u]) << u;
+        const uint32_t run = (uint32_t)__builtin_ctz(~m);
+        L = min(L + run, lim);
+#ifdef LZ_DBG
+        if (lane == 0) dbg_rounds++;
+#endif
+        if (run < 16 || L >= lim) break;
       }
-      uint64_t key = ((uint64_t)L << 8) | (255u - b);
-      key = wave_max_u64(key);
-      const uint32_t longest = (uint32_t)(key >> 8), best = 255u - (uint32_t)(key & 255);
+    }
+    return wave_max_u32((L << 8) | (255u - b));
+  };
+  uint32_t nm = 0;
+  bool overflow = false;
+  auto emit = [&](uint32_t q, uint32_t longest, uint32_t best) {
+    if (nm < j.lz_cap) {
+      if (lane == 0) { mt[3 * nm] = q; mt[3 * nm + 1] = longest; mt[3 * nm + 2] = best; }
+    } else {
+      overflow = true;
+    }
+    nm++;
+  };
+  // ---- phase 1: every segment's own walk (nseg == 1: the serial walk, straight into mt)
+  if (ti.ncand && (uint32_t)wv < nseg) {
+    const uint32_t lo = seg_lo(wv), hi = seg_lo(wv + 1);
+    uint32_t pos = lo, cnt = 0;
+    while (pos < hi) {
+      const uint32_t q = next_cand(pos);
+      if (q >= hi) break;
+      if (nseg > 1 && lane == 0) atomicOr(&vis[q >> 5], 1u << (q & 31));   // no round trip
+#ifdef LZ_DBG
+      dbg_vis++;
+#endif
+      const uint32_t key = measure(q);
+      const uint32_t longest = key >> 8, best = 255u - (key & 255);
       if (longest >= thr) {
-        if (nm < j.lz_cap) {
-          if (lane == 0) { mt[3 * nm] = q; mt[3 * nm + 1] = longest; mt[3 * nm + 2] = best; }
-        } else {
-          overflow = true;
-        }
-        nm++;
+        if (nseg == 1) emit(q, longest, best);
+        else if (cnt < segcap && lane == 0) spec[wv * segcap + cnt] = q | ((longest - 4) << 16) | ((best - 1) << 24);
+        cnt++;
         pos = q + longest;
       } else {
         pos = q + 1;
       }
     }
+    if (lane == 0) { s_cnt[wv] = cnt; s_exit[wv] = max(pos, hi); }
+  }
+#ifdef LZ_DBG
+  if (lane == 0) {
+    s_dbg[wv][0] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - dbg_t0);
+    s_dbg[wv][1] = dbg_vis;
+    s_dbg[wv][2] = dbg_rounds;
+  }
+#endif
+  if (nseg > 1) {
+    __syncthreads();
+    if (wv) return;
+    // ---- phase 2 (wave 0): stitch the segments
+    uint32_t pos = 0;
+    for (uint32_t s = 0; s < (ti.ncand ? nseg : 0u); s++) {
+      const uint32_t hi = seg_lo(s + 1), cnt = s_cnt[s];
+      if (cnt > segcap) { overflow = true; nm += cnt; continue; }     // cannot happen: lz_cap >= npix / 4 + 16
+      uint32_t from = 0;                                              // first valid entry of s's walk
+      bool conv = s == 0;
+      if (s > 0) {
+        while (pos < hi) {
+          const uint32_t q = next_cand(pos);
+          if (q >= hi) { pos = hi; break; }
+          if ((vis[q >> 5] >> (q & 31)) & 1) { conv = true; pos = q; break; }
+#ifdef LZ_DBG
+          dbg_fix++;
+#endif
+          const uint32_t key = measure(q);
+          const uint32_t longest = key >> 8, best = 255u - (key & 255);
+          if (longest >= thr) { emit(q, longest, best); pos = q + longest; }
+          else pos = q + 1;
+        }
+        if (conv) {                                                   // first entry at or after pos
+          from = cnt;
+          for (uint32_t i0 = 0; i0 < cnt; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            const uint64_t m = __ballot(i < cnt && (spec[s * segcap + i] & 0xffffu) >= pos);
+            if (m) { from = i0 + (uint32_t)(__ffsll((unsigned long long)m) - 1); break; }
+          }
+        }
+      }
+      if (conv) {
+        for (uint32_t i0 = from; i0 < cnt; i0 += 256) {               // four loads in flight
+          uint32_t e[4];
+#pragma unroll
+          for (int u = 0; u < 4; u++) e[u] = spec[s * segcap + min(i0 + 64u * u + lane, cnt - 1)];
+#pragma unroll
+          for (int u = 0; u < 4; u++) {
+            const uint32_t i = i0 + 64u * u + lane, k = nm + (i - from);
+            if (i < cnt && k < j.lz_cap) { mt[3 * k] = e[u] & 0xffffu; mt[3 * k + 1] = ((e[u] >> 16) & 255u) + 4; mt[3 * k + 2] = (e[u] >> 24) + 1; }
+          }
+        }
+        nm += cnt - from;
+        if (nm > j.lz_cap) overflow = true;
+        pos = s_exit[s];
+      }
+    }
+#ifdef LZ_DBG
+    if (lane == 0) {
+      uint32_t w = 0;
+      for (uint32_t k = 1; k < nseg; k++) if (s_dbg[k][0] > s_dbg[w][0]) w = k;
+      mt[3 * j.lz_cap] = s_dbg[w][0];
+      mt[3 * j.lz_cap + 1] = s_dbg[w][1] | (dbg_fix << 16);
+      mt[3 * j.lz_cap + 2] = s_dbg[w][2];
+    }
+#endif
+  } else if (wv) {
+    return;
   }
   // --- LZ symbol streams (lz.hpp:75-95): future (gaps, 255-chunked), length-4, back%256
   uint16_t* lz0 = j.sym + (size_t)j.ntiles * 3 * j.npix_cap + (size_t)(t * 3) * j.lz_cap;
@@ -311,7 +437,7 @@ __device__ __forceinline__ void nuke_tile(const EncodeJob& j, int t, uint32_t* n
 }
 
 void launch_lz(const EncodeJob& j, hipStream_t s) {
-  hipLaunchKernelGGL(k_lz, dim3(j.ntiles), dim3(64), 0, s, j);
+  hipLaunchKernelGGL(k_lz, dim3(j.ntiles), dim3(64 * LZ_SEG), 0, s, j);
 }
 
 void launch_nuke(const EncodeJob& j, hipStream_t s) {

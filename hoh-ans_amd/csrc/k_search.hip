@@ -542,15 +542,7 @@ __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring)
   if (lane == 0 && ncand) atomicAdd(&j.tiles[t].ncand, ncand);
 }
 
-__device__ __forceinline__ uint64_t wmax64(uint64_t v) {
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint64_t u = __shfl_xor(v, o);
-    v = u > v ? u : v;
-  }
-  return v;
-}
-
-
+#define LZS_KB 0x1ffffu      // k_lzscan keys: (L << 17) | (LZS_KB - b)
 #define LZS_HB 16        // horizontal back-distance chunks of 64 whose fingerprints load at once
 #define LZS_VB 4         // vertical chunks (k * w <= 65536: 256 rows of a 256-wide tile)
 #define LZS_BITS 1024    // candidate words in LDS (tiles up to 65,536 pixels)
@@ -564,6 +556,7 @@ __device__ __forceinline__ uint64_t wmax64(uint64_t v) {
 __global__ __launch_bounds__(64) void k_lzscan(EncodeJob j, int limit, int rp) {
   extern __shared__ uint32_t pring[];
   __shared__ uint64_t cb[LZS_BITS];
+  __shared__ uint32_t hl[LZS_HB * 64];                                 // a batch's hit list
   const int t = blockIdx.x, lane = threadIdx.x;
   TileInfo ti = j.tiles[t];
   const uint32_t npix = (uint32_t)ti.w * ti.h, nwords = (npix + 63) / 64, w = ti.w;
@@ -589,29 +582,31 @@ __global__ __launch_bounds__(64) void k_lzscan(EncodeJob j, int limit, int rp) {
     if (lo > wend) wend = lo & ~63u;
     while (wend < need) {
       const uint32_t p = wend + (uint32_t)lane;
-      pring[p & rmask] = p < npix ? tile_px(j, ti, p) : 0xff000000u;
+      const uint32_t v = tile_px(j, ti, min(p, npix - 1));          // unconditional load
+      pring[p & rmask] = p < npix ? v : 0xff000000u;
       wend += 64;
     }
-    __syncthreads();
+    // one-wave workgroup: its LDS accesses are ordered without a barrier
   };
   // run length of q against q - b (lz.hpp:37-45), at most 259
   auto runl = [&](uint32_t q, uint32_t b) -> uint32_t {
     const uint32_t lim = min(259u, npix - q);
     uint32_t L = 0;
     if (rp && b <= (uint32_t)limit) {
-      bool go = true;
-      while (go && L < lim) {
-        uint32_t a[8], c[8];
+      // sixteen positions per LDS round trip, the equal ones as a mask (trailing ones = the run)
+      for (;;) {
+        uint32_t a[16], c[16];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
+        for (int u = 0; u < 16; u++) {
           a[u] = pring[(q + L + u) & rmask];
           c[u] = pring[(q + L + u - b) & rmask];
         }
+        uint32_t m = 0;                               // bits 16.. of ~m stop the count at 16
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-          if (go && L < lim && a[u] == c[u]) L++;
-          else go = false;
-        }
+        for (int u = 0; u < 16; u++) m |= (uint32_t)(a[u] == c[u]) << u;
+        const uint32_t run = (uint32_t)__builtin_ctz(~m);
+        L = min(L + run, lim);
+        if (run < 16 || L >= lim) break;
       }
     } else {
       while (L < lim && (rp ? pring[(q + L) & rmask] : tile_px(j, ti, q + L)) == tile_px(j, ti, q + L - b)) L++;
@@ -622,6 +617,11 @@ __global__ __launch_bounds__(64) void k_lzscan(EncodeJob j, int limit, int rp) {
   bool overflow = false;
   while (ti.ncand && pos < npix) {
     uint32_t q = 0xffffffffu;
+    if (lds_bits && (pos >> 6) < nwords) {              // usually in pos's own word
+      const uint64_t wv = cb[pos >> 6] & (~0ull << (pos & 63));
+      if (wv) q = (pos & ~63u) + (uint32_t)(__ffsll((unsigned long long)wv) - 1);
+    }
+    if (q == 0xffffffffu)
     for (uint32_t wi = pos >> 6; wi < nwords; wi += 64) {
       uint64_t wv = (wi + lane < nwords) ? (lds_bits ? cb[wi + lane] : bits[wi + lane]) : 0;
       if (wi + lane == (pos >> 6)) wv &= ~0ull << (pos & 63);
@@ -655,7 +655,8 @@ __global__ __launch_bounds__(64) void k_lzscan(EncodeJob j, int limit, int rp) {
     // reduction per chunk with hits cost ~12 cross-lane steps each: textured natural regions hit
     // in most of the 16 chunks); a chunk in which some lane reaches 259 ends the walk, so the
     // smallest such b wins as in the reference's short circuit (lz.hpp:47-50).
-    uint64_t mine = 0;                                                // (L << 32) | (~b)
+    // keys (L << 17) | (LZS_KB - b): L <= 259, b <= 65536 < LZS_KB
+    uint32_t mine = 0;
     bool done = false;
     for (uint32_t g0 = 1; g0 <= bm && !done; g0 += 64 * LZS_HB) {
       if (g0 > 1) {
@@ -665,33 +666,40 @@ __global__ __launch_bounds__(64) void k_lzscan(EncodeJob j, int limit, int rp) {
           fv[c] = b <= bm ? F[q - b] : 0u;
         }
       }
-      uint32_t hb = 0;                                                // lane's hits, bit c = chunk c
+      // the batch's hits (equal fingerprints) listed in LDS, then measured 64 at a time: a
+      // textured region hits a few lanes in most chunks, and a chunk at a time left most lanes
+      // idle through a run-length loop per chunk.  Every hit is measured (no stop at the first
+      // 259): the maximum key is the same, the smallest b of length 259 winning as in the
+      // reference's short circuit (lz.hpp:47-50).
+      uint32_t tot = 0;
 #pragma unroll
-      for (int c = 0; c < LZS_HB; c++) hb |= (uint32_t)(g0 + 64 * c + lane <= bm && fv[c] == f) << c;
-      for (int c = 0; c < LZS_HB && !done; c++) {
-        const bool hit = (hb >> c) & 1;
-        if (__ballot(hit)) {
-          const uint32_t b = g0 + 64 * c + lane;
-          uint32_t L = 0;
-          if (hit) {
-            L = runl(q, b);
-            const uint64_t key = ((uint64_t)L << 32) | (uint32_t)(~b);
-            if (key > mine) mine = key;
-          }
-          done = __ballot(L >= 259) != 0;
-        }
+      for (int c = 0; c < LZS_HB; c++) {
+        const bool hit = g0 + 64 * c + lane <= bm && fv[c] == f;
+        const uint64_t m = __ballot(hit);
+        if (hit)
+          hl[tot + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+              g0 + 64 * c + lane;
+        tot += (uint32_t)__popcll(m);
       }
+      bool top = false;
+      for (uint32_t i = lane; i < tot; i += 64) {
+        const uint32_t b = hl[i], L = runl(q, b);
+        const uint32_t key = (L << 17) | (LZS_KB - b);
+        if (key > mine) mine = key;
+        top = top || L >= 259;
+      }
+      done = __ballot(top) != 0;
     }
-    uint64_t best = wmax64(mine);
+    uint32_t best = wave_max_u32(mine);
     // vertical (lz.hpp:54-74): whole rows up to 65536 back, strictly longer only
-    if ((best >> 32) < 259) {
-      uint64_t vmine = 0;
+    if ((best >> 17) < 259) {
+      uint32_t vmine = 0;
       auto vchunk = [&](uint32_t k, uint32_t fk) {
         const uint32_t b = k * w;
         const bool hit = k <= kmax && fk == f;
         if (!__ballot(hit)) return;
         if (hit) {
-          const uint64_t key = ((uint64_t)runl(q, b) << 32) | (uint32_t)(~b);
+          const uint32_t key = (runl(q, b) << 17) | (LZS_KB - b);
           if (key > vmine) vmine = key;
         }
       };
@@ -702,10 +710,10 @@ __global__ __launch_bounds__(64) void k_lzscan(EncodeJob j, int limit, int rp) {
         const uint32_t k = k0 + lane, c = (k0 - 1) / 64;
         vchunk(k, c < LZS_VB ? ((vh >> c) & 1 ? f : ~f) : (k <= kmax ? F[q - k * w] : 0u));
       }
-      const uint64_t vb = wmax64(vmine);
-      if ((vb >> 32) > (best >> 32)) best = vb;
+      const uint32_t vb = wave_max_u32(vmine);
+      if ((vb >> 17) > (best >> 17)) best = vb;
     }
-    const uint32_t longest = (uint32_t)(best >> 32), bb = ~(uint32_t)best;
+    const uint32_t longest = best >> 17, bb = LZS_KB - (best & LZS_KB);
     if (longest >= thr) {
       if (nm < j.lz_cap) {
         if (lane == 0) { mt[3 * nm] = q; mt[3 * nm + 1] = longest; mt[3 * nm + 2] = bb; }
