@@ -32,7 +32,7 @@ __device__ __forceinline__ uint32_t img_px(const EncodeJob& j, int x0, int y0, i
 // coincide: that walk's matches from this candidate on, and its exit, are the true ones) or
 // leaves the segment.  Matches are decided exactly as before, so the list is the serial one.
 __global__ __launch_bounds__(64 * LZ_SEG) void k_lz(EncodeJob j) {
-  __shared__ uint32_t ring[LZ_SEG][LZR];
+  __shared__ uint32_t ring[LZ_SEG][LZR + 16];        // + a mirror of entries 0..15
   __shared__ uint64_t cbits[LZ_BITS_MAX];
   __shared__ uint32_t vis[2 * LZ_BITS_MAX];          // visited candidates (segmented walks only)
   __shared__ uint32_t s_cnt[LZ_SEG], s_exit[LZ_SEG];
@@ -85,8 +85,10 @@ __global__ __launch_bounds__(64 * LZ_SEG) void k_lz(EncodeJob j) {
       for (int u = 0; u < LZ_FILL; u++) v[u] = img_px(j, x0, y0, tw, min(wend + 64u * u + (uint32_t)lane, npix - 1));
 #pragma unroll
       for (int u = 0; u < LZ_FILL; u++) {
-        const uint32_t p = wend + 64u * u + (uint32_t)lane;
-        rg[p & (LZR - 1)] = p < npix ? v[u] : 0xff000000u;
+        const uint32_t p = wend + 64u * u + (uint32_t)lane, e = p & (LZR - 1);
+        const uint32_t x = p < npix ? v[u] : 0xff000000u;
+        rg[e] = x;
+        if (e < 16) rg[e + LZR] = x;                  // the mirror: 16 entries read from any base
       }
       wend += 64 * LZ_FILL;
     }
@@ -98,6 +100,7 @@ __global__ __launch_bounds__(64 * LZ_SEG) void k_lz(EncodeJob j) {
   auto next_cand = [&](uint32_t pos) -> uint32_t {
     if (pos >= npix) return 0xffffffffu;
     if (lds_bits) {                                   // usually in pos's own word
+      // (kept in VGPRs: readfirstlane on the word or on q measured 1.7x / 1.05x slower)
       if ((pos >> 6) != cwi) { cwi = pos >> 6; cw = cbits[cwi]; }
       const uint64_t wv2 = cw & (~0ull << (pos & 63));
       if (wv2) return (pos & ~63u) + (uint32_t)(__ffsll((unsigned long long)wv2) - 1);
@@ -120,20 +123,22 @@ __global__ __launch_bounds__(64 * LZ_SEG) void k_lz(EncodeJob j) {
     const uint32_t b = lane + 1;
     uint32_t L = 0;
     if (b <= q) {
-      // sixteen positions per LDS round trip (a flat region's copies run to the 259 cap), the
-      // equal positions as a bit mask whose trailing ones are the run
+      // sixteen positions per LDS round trip from two bases (the mirror spares every read its
+      // wrap), the first unequal one by a select chain
       const uint32_t lim = min(259u, npix - q);
       for (;;) {
+        const uint32_t* pa = rg + ((q + L) & (LZR - 1));
+        const uint32_t* pc = rg + ((q + L - b) & (LZR - 1));
         uint32_t a[16], c[16];
 #pragma unroll
-        for (int u = 0; u < 16; u++) {
-          a[u] = rg[(q + L + u) & (LZR - 1)];
-          c[u] = rg[(q + L + u - b) & (LZR - 1)];
-        }
-        uint32_t m = 0;                               // bits 16.. of ~m stop the count at 16
+        for (int u = 0; u < 16; u++) { a[u] = pa[u]; c[u] = pc[u]; }
+        uint32_t r0 = 8, r1 = 16;                     // two chains: no compare-to-select stalls
 #pragma unroll
-        for (int u = 0; u < 16; u++) m |= (uint32_t)(a[u] == c[u]) << u;
-        const uint32_t run = (uint32_t)__builtin_ctz(~m);
+        for (int u = 7; u >= 0; u--) {
+          r1 = a[u + 8] != c[u + 8] ? (uint32_t)u + 8 : r1;
+          r0 = a[u] != c[u] ? (uint32_t)u : r0;
+        }
+        const uint32_t run = r0 < 8 ? r0 : r1;
         L = min(L + run, lim);
 #ifdef LZ_DBG
         if (lane == 0) dbg_rounds++;

@@ -582,8 +582,10 @@ __global__ __launch_bounds__(64) void k_lzscan(EncodeJob j, int limit, int rp) {
     if (lo > wend) wend = lo & ~63u;
     while (wend < need) {
       const uint32_t p = wend + (uint32_t)lane;
-      const uint32_t v = tile_px(j, ti, min(p, npix - 1));          // unconditional load
-      pring[p & rmask] = p < npix ? v : 0xff000000u;
+      const uint32_t v = tile_px(j, ti, min(p, npix - 1)), e = p & rmask;   // unconditional load
+      const uint32_t x = p < npix ? v : 0xff000000u;
+      pring[e] = x;
+      if (e < 16) pring[e + rp] = x;                                 // the mirror of entries 0..15
       wend += 64;
     }
     // one-wave workgroup: its LDS accesses are ordered without a barrier
@@ -595,16 +597,19 @@ __global__ __launch_bounds__(64) void k_lzscan(EncodeJob j, int limit, int rp) {
     if (rp && b <= (uint32_t)limit) {
       // sixteen positions per LDS round trip, the equal ones as a mask (trailing ones = the run)
       for (;;) {
+        // two bases (the mirror spares every read its wrap), the first unequal one by two chains
+        const uint32_t* pa = pring + ((q + L) & rmask);
+        const uint32_t* pc = pring + ((q + L - b) & rmask);
         uint32_t a[16], c[16];
 #pragma unroll
-        for (int u = 0; u < 16; u++) {
-          a[u] = pring[(q + L + u) & rmask];
-          c[u] = pring[(q + L + u - b) & rmask];
-        }
-        uint32_t m = 0;                               // bits 16.. of ~m stop the count at 16
+        for (int u = 0; u < 16; u++) { a[u] = pa[u]; c[u] = pc[u]; }
+        uint32_t r0 = 8, r1 = 16;
 #pragma unroll
-        for (int u = 0; u < 16; u++) m |= (uint32_t)(a[u] == c[u]) << u;
-        const uint32_t run = (uint32_t)__builtin_ctz(~m);
+        for (int u = 7; u >= 0; u--) {
+          r1 = a[u + 8] != c[u + 8] ? (uint32_t)u + 8 : r1;
+          r0 = a[u] != c[u] ? (uint32_t)u : r0;
+        }
+        const uint32_t run = r0 < 8 ? r0 : r1;
         L = min(L + run, lim);
         if (run < 16 || L >= lim) break;
       }
@@ -1051,7 +1056,7 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, void (*mark)(void*, const
   int rp = 1;
   while (rp < limit + 324) rp <<= 1;
   if (rp > 8192) rp = 0;                                              // -s4: pixels from the image
-  hipLaunchKernelGGL(k_lzscan, dim3(j.ntiles), dim3(64), (size_t)(rp ? rp : 1) * 4, s, j, limit, rp);
+  hipLaunchKernelGGL(k_lzscan, dim3(j.ntiles), dim3(64), (size_t)(rp ? rp + 16 : 1) * 4, s, j, limit, rp);
   launch_nuke(j, s);
   mark(mc, "lz");
   hipLaunchKernelGGL(k_setup_s, dim3(j.ntiles), dim3(128), 0, s, j);
