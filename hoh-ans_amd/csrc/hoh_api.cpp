@@ -208,6 +208,11 @@ int hoh_get_kernel_stats(hoh_ctx* c, const char** names, double* total_ms, uint6
 // (0: the LZ match lists, 1: k_lz's segment walks)
 extern "C" int hoh_debug_read(hoh_ctx* c, int which, void* dst, size_t bytes) {
   if (!c || !dst) return HOH_E_ARG;
+  if (which == 2) {                    // the tail of the decoder's back-distance map buffer
+    if (!c->dec.bufs[15] || bytes > c->dec.sizes[15]) return HOH_E_ARG;
+    return hipMemcpy(dst, (const uint8_t*)c->dec.bufs[15] + c->dec.sizes[15] - bytes, bytes, hipMemcpyDeviceToHost) == hipSuccess
+               ? HOH_OK : HOH_E_HIP;
+  }
   const Buf& b = which == 0 ? c->matches : c->lzspec;
   if (bytes > b.n || !b.p) return HOH_E_ARG;
   return hipMemcpy(dst, b.p, bytes, hipMemcpyDeviceToHost) == hipSuccess ? HOH_OK : HOH_E_HIP;

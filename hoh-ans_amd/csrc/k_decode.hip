@@ -1467,18 +1467,33 @@ __global__ __launch_bounds__(64) void k_dunpred_lz(DecJob j, int br, int many, i
   if (*(volatile const uint32_t*)j.gerr) return;                      // one load per wave: uniform
   const uint32_t cnt = *(volatile const uint32_t*)(j.gerr + 2);
   if ((cnt > LZ_FEW) != (many != 0)) return;
-  if ((int)blockIdx.x >= wgrid) {
-    const uint32_t ci = blockIdx.x - wgrid;
+  // the chain workgroups come first in the grid: they are the launch's long pole (a serial walk
+  // per tile plane), and behind ~1000 wavefront workgroups they waited for free CUs
+  const uint32_t nch = gridDim.x - (uint32_t)wgrid;
+#ifdef DEC_DBG
+  // per workgroup {start, end} (s_memrealtime, 100 MHz) at the tail of the bmap buffer
+  uint32_t* dbg = (uint32_t*)(j.bmap + (size_t)j.ntiles * j.th * ((j.tw + 15) & ~15) + 16) + (many ? 8192 : 0);
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  if (blockIdx.x < nch) {
+    __builtin_amdgcn_s_setprio(3);                                     // issue ahead of the wavefront waves
+    const uint32_t ci = blockIdx.x;
     const int cls = ci < (uint32_t)ga ? 1 : 2;
     const uint32_t blk = ci - (cls - 1) * ga;
     if (cls == 1 ? full1 : full2) chain_tiles<true, CH_R>(j, cls, blk);
     else chain_tiles<false, CH_R>(j, cls, blk);
+#ifdef DEC_DBG
+    if (threadIdx.x == 0 && blockIdx.x < 4096) { dbg[2 * blockIdx.x] = (uint32_t)t0; dbg[2 * blockIdx.x + 1] = (uint32_t)__builtin_amdgcn_s_memrealtime(); }
+#endif
     return;
   }
-  for (uint32_t i = blockIdx.x; i < cnt; i += wgrid) {
+  for (uint32_t i = blockIdx.x - nch; i < cnt; i += wgrid) {
     dunpred_lz_tile(j, (int)j.lzt[i], lz_lds, br);
     __syncthreads();
   }
+#ifdef DEC_DBG
+  if (threadIdx.x == 0 && blockIdx.x < 4096) { dbg[2 * blockIdx.x] = (uint32_t)t0; dbg[2 * blockIdx.x + 1] = (uint32_t)__builtin_amdgcn_s_memrealtime(); }
+#endif
 }
 
 
@@ -2078,7 +2093,11 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   if ((e = dbuf(w, 6, 64, &q))) return e; j.gerr = (uint32_t*)q;
   if ((e = dbuf(w, 7, (size_t)j.ntiles * 3 * j.npix_cap * 2, &q))) return e; j.dplane = (uint16_t*)q;
   if ((e = dbuf(w, 14, (size_t)j.ntiles * 3 * 4, &q))) return e; j.lzt = (uint32_t*)q;
+#ifdef DEC_DBG
+  if ((e = dbuf(w, 15, (size_t)j.ntiles * j.th * ((j.tw + 15) & ~15) + 16 + (1 << 16), &q))) return e; j.bmap = (uint8_t*)q;
+#else
   if ((e = dbuf(w, 15, (size_t)j.ntiles * j.th * ((j.tw + 15) & ~15) + 16, &q))) return e; j.bmap = (uint8_t*)q;
+#endif
   j.lz_xrow = lz_xrow();
   j.ix = index_streams(idx);
   j.ck = index_ckpts(idx);
