@@ -1456,6 +1456,8 @@ __device__ __forceinline__ void dunpred_lz_tile(const DecJob& j, int t, uint32_t
 #define LZ_FEW 256
 template <bool FULL, int CH_R>
 __device__ void chain_tiles(const DecJob& j, int cls, uint32_t blk);
+template <int CH_R>
+__device__ void chain_full(const DecJob& j, int cls, uint32_t blk);
 
 // Workgroups [0, wgrid) take the wavefront tiles; the ones after them the chain tiles (ga
 // workgroups per width class, class 2 only when the edge column is narrower), so both run in
@@ -1480,7 +1482,7 @@ __global__ __launch_bounds__(64) void k_dunpred_lz(DecJob j, int br, int many, i
     const uint32_t ci = blockIdx.x;
     const int cls = ci < (uint32_t)ga ? 1 : 2;
     const uint32_t blk = ci - (cls - 1) * ga;
-    if (cls == 1 ? full1 : full2) chain_tiles<true, CH_R>(j, cls, blk);
+    if (cls == 1 ? full1 : full2) chain_full<CH_R>(j, cls, blk);
     else chain_tiles<false, CH_R>(j, cls, blk);
 #ifdef DEC_DBG
     if (threadIdx.x == 0 && blockIdx.x < 4096) { dbg[2 * blockIdx.x] = (uint32_t)t0; dbg[2 * blockIdx.x + 1] = (uint32_t)__builtin_amdgcn_s_memrealtime(); }
@@ -1694,6 +1696,165 @@ __host__ __device__ constexpr uint32_t ch_vs(int R) { return (uint32_t)R * 2 + 4
 __host__ __device__ constexpr uint32_t ch_res_off(int R) { return CH_L * ch_vs(R); }
 __host__ __device__ constexpr uint32_t ch_scr(int R) { return ch_res_off(R) + CH_L * CH_QS; }
 __host__ __device__ constexpr uint32_t ch_smem(int R) { return ch_scr(R) + 16; }
+
+// Chain tiles whose width is a multiple of 16 (every 256-wide tile): k_dexpand has already
+// put each pixel's residual + half into the output plane itself (copies: anything), so a step
+// takes its residual from the block's 32 bytes in registers (one SDWA add) instead of a
+// residual ring indexed by a running symbol count, and the block's values overwrite the
+// residuals it consumed.  16-pixel blocks never straddle a row; their ring slots are contiguous
+// (constant ds offsets); the next step's LDS reads (T, the copy source) are issued before the
+// current step's arithmetic.
+template <int CH_R>
+__device__ void chain_full(const DecJob& j, int cls, uint32_t blk) {
+  const uint32_t lane = threadIdx.x, q = lane / 3, p = lane - 3 * q;
+  const uint32_t base = blk * CH_T, cnt = *(volatile const uint32_t*)(j.gerr + 6 + cls);
+  if (base >= cnt) return;
+  const bool act = lane < CH_L && base + q < cnt;
+  const int t = (int)j.lzt[(size_t)cls * j.ntiles + base + (act ? q : 0)];
+  const DecTile ti = j.tiles[t];
+  const uint32_t w = __builtin_amdgcn_readfirstlane(ti.w);             // one width per wave
+  const uint32_t h = act ? (uint32_t)ti.h : 0u;
+  uint32_t hmax = h;
+#pragma unroll
+  for (int o = 32; o; o >>= 1) hmax = max(hmax, (uint32_t)__shfl_xor(hmax, o));
+  if (lane >= CH_L) return;                                            // no rings for these lanes
+  const uint32_t c = p ? 512u : 256u, half = c >> 1, cm = c - 1;
+  uint16_t* outp = j.dplane + (size_t)(t * 3 + p) * j.npix_cap;
+  const uint4* e4 = (const uint4*)outp;
+  const uint32_t pitch = bm_pitch(w), npix = w * (h ? h : 1u);
+  const uint8_t* bm = j.bmap + (size_t)t * j.th * bm_pitch(j.tw);
+  const uint32_t rb = lane * ch_vs(CH_R);                              // this lane's value ring
+  for (uint32_t e = 0; e < CH_R; e += 2) lds_st32(rb + 2 * e, half | (half << 16));
+  uint4 bnext = *(const uint4*)bm;                                     // row 0, columns 0..15
+  uint4 en0 = e4[0], en1 = e4[1];                                      // block 0's residuals
+  for (uint32_t y = 0; y < hmax; y++) {
+    uint32_t L = half, Tp = half;                                      // row start: L = TL = half
+    const bool live = y < h;
+    for (uint32_t x0 = 0; x0 < w; x0 += 16) {
+      const uint32_t i0 = y * w + x0;
+      const uint4 bcur = bnext, ec0 = en0, ec1 = en1;
+      {
+        const uint32_t ny = x0 + 16 < w ? y : y + 1, nx = x0 + 16 < w ? x0 + 16 : 0;
+        const bool more = live && ny < h;
+        bnext = more ? *(const uint4*)(bm + (size_t)ny * pitch + nx) : make_uint4(0, 0, 0, 0);
+        const uint32_t nb = more ? (i0 + 16) / 8 : 0u;                 // (block i0 + 16 < npix)
+        en0 = e4[nb]; en1 = e4[nb + 1];
+      }
+      if (!live) continue;
+      const uint32_t bw[4] = {bcur.x, bcur.y, bcur.z, bcur.w};
+      const uint32_t rw[8] = {ec0.x, ec0.y, ec0.z, ec0.w, ec1.x, ec1.y, ec1.z, ec1.w};
+      const uint32_t pos0 = i0 & (CH_R - 1);
+      const uint32_t tA = rb + 2 * ((pos0 - w) & (CH_R - 1));          // T of step u at tA + 2u
+      const uint32_t wA = rb + 2 * pos0;                               // this block's slots
+      auto block = [&](auto nowrap_c) {
+        constexpr bool NOWRAP = decltype(nowrap_c)::value;
+        auto srcA = [&](int u, uint32_t b) -> uint32_t {
+          return NOWRAP ? wA + 2 * u - 2 * b : rb + 2 * ((pos0 + (uint32_t)u - b) & (CH_R - 1));
+        };
+        // step 0 reads its copy source after every earlier write, so even b = 1 comes from the
+        // ring (at a row's start that is the end of the row above, not L = half)
+        uint32_t b = bw[0] & 255u;
+        uint32_t T = lds_u16(tA), vC = lds_u16(srcA(0, b ? b : 1));
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+          uint32_t bn = 0, Tn = 0, vCn = 0;
+          if (u < 15) {
+            bn = (bw[(u + 1) >> 2] >> (8 * ((u + 1) & 3))) & 255u;
+            Tn = lds_u16(tA + 2 * (u + 1));
+            vCn = lds_u16(srcA(u + 1, bn));
+          }
+          const uint32_t r = (rw[u >> 1] >> (16 * (u & 1))) & 0xffffu;   // residual + half
+          uint32_t vm = (r + medp(T, L, Tp)) & cm, vc = (u > 0 && b == 1) ? L : vC;
+          // both values, then a select: left to itself the compiler branches around the MED
+          asm volatile("" : "+v"(vm), "+v"(vc));
+          const uint32_t v = b ? vc : vm;
+          lds_st16(wA + 2 * u, v);
+          Tp = T;
+          L = v;
+          b = bn; T = Tn; vC = vCn;
+        }
+      };
+      if (pos0 >= 256) block(std::true_type{});                         // i - b >= 1 for every b <= 255
+      else block(std::false_type{});
+      // the block's 16 values over its residuals (two 16-byte stores)
+      uint32_t d[8];
+#pragma unroll
+      for (int e = 0; e < 8; e++) d[e] = lds_u32(wA + 4 * e);
+      uint4* o4 = (uint4*)(outp + i0);
+      o4[0] = make_uint4(d[0], d[1], d[2], d[3]);
+      o4[1] = make_uint4(d[4], d[5], d[6], d[7]);
+    }
+  }
+  (void)npix;
+}
+
+// k_dexpand: each FULL chain tile's three residual streams spread to their pixels (+ half) in the
+// output planes, copies skipped (bmap != 0); the streams' lengths are checked against the count
+// of non-copy pixels.  One workgroup per tile, 1024 pixels per pass: four per thread (a row never
+// splits a thread's four: w % 16 == 0), wave prefix counts by ballots, the waves' totals in LDS.
+__global__ __launch_bounds__(256) void k_dexpand(DecJob j, int full1, int full2) {
+  if (dec_abort(j)) return;
+  __shared__ uint32_t wtot[4];
+  const uint32_t n1 = *(volatile const uint32_t*)(j.gerr + 7), n2 = *(volatile const uint32_t*)(j.gerr + 8);
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (uint32_t e = blockIdx.x; e < n1 + n2; e += gridDim.x) {
+    const bool c1 = e < n1;
+    if (!(c1 ? full1 : full2)) continue;
+    const int t = (int)(c1 ? j.lzt[(size_t)j.ntiles + e] : j.lzt[(size_t)2 * j.ntiles + e - n1]);
+    const DecTile ti = j.tiles[t];
+    const uint32_t w = ti.w, npix = w * ti.h, pitch = bm_pitch(w);
+    const uint8_t* bm = j.bmap + (size_t)t * j.th * bm_pitch(j.tw);
+    const uint16_t* r0 = j.dsym + (size_t)(t * 3) * j.plane_cap;
+    const uint16_t* r1 = r0 + j.plane_cap;
+    const uint16_t* r2 = r1 + j.plane_cap;
+    uint16_t* o0 = j.dplane + (size_t)(t * 3) * j.npix_cap;
+    uint16_t* o1 = o0 + j.npix_cap;
+    uint16_t* o2 = o1 + j.npix_cap;
+    uint32_t kb = 0;
+    for (uint32_t i0 = 0; i0 < npix; i0 += 1024) {
+      const uint32_t i = i0 + 4 * tid;
+      uint32_t f = 0;
+      if (i < npix) {
+        const uint32_t y = i / w, x = i - y * w;
+        const uint32_t m = *(const uint32_t*)(bm + (size_t)y * pitch + x);
+#pragma unroll
+        for (int u = 0; u < 4; u++) f |= (((m >> (8 * u)) & 255u) == 0 ? 1u : 0u) << u;
+      }
+      const uint32_t n = __popc(f);
+      // exclusive prefix of n over the wave (three bit planes of n by ballot), then over the waves
+      uint32_t ex = 0;
+#pragma unroll
+      for (int bit = 0; bit < 3; bit++) {
+        const uint64_t bl = __ballot((n >> bit) & 1);
+        ex += __builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u)) << bit;
+      }
+      uint32_t wt = 0;
+#pragma unroll
+      for (int bit = 0; bit < 3; bit++) wt += (uint32_t)__popcll(__ballot((n >> bit) & 1)) << bit;
+      if (lane == 0) wtot[wv] = wt;
+      __syncthreads();
+      uint32_t k = kb + ex, tot = 0;
+#pragma unroll
+      for (int v = 0; v < 4; v++) { const uint32_t x = wtot[v]; if ((uint32_t)v < wv) k += x; tot += x; }
+      __syncthreads();
+      if (i < npix) {
+        uint32_t a0 = 0, a1 = 0, a2 = 0, b0 = 0, b1 = 0, b2 = 0;      // four u16 per plane
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          uint32_t g = 0, rr = 0, bb = 0;
+          if ((f >> u) & 1) { g = r0[k] + 128u; rr = r1[k] + 256u; bb = r2[k] + 256u; k++; }
+          if (u < 2) { a0 |= g << (16 * u); a1 |= rr << (16 * u); a2 |= bb << (16 * u); }
+          else { b0 |= g << (16 * (u - 2)); b1 |= rr << (16 * (u - 2)); b2 |= bb << (16 * (u - 2)); }
+        }
+        *(uint2*)(o0 + i) = make_uint2(a0, b0);
+        *(uint2*)(o1 + i) = make_uint2(a1, b1);
+        *(uint2*)(o2 + i) = make_uint2(a2, b2);
+      }
+      kb += tot;
+    }
+    if (tid < 3 && kb != j.streams[t * SK_PER_TILE + 3 + tid].n) atomicOr(j.gerr, 1u);
+  }
+}
 
 // FULL: the wave's width is a multiple of 16, so 16-pixel blocks never straddle a row, their
 // ring slots are contiguous (constant ds offsets) and every block flushes its 16 values to the
@@ -2135,6 +2296,10 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   // chain tiles: their back-distance maps (the chains themselves run inside k_dunpred_lz)
   const int gsmall = std::min(j.ntiles, 256);
   hipLaunchKernelGGL(k_dbackmap, dim3(gsmall), dim3(256), 0, s, j);
+  {
+    const int we = j.W - (j.xt - 1) * j.tw;
+    hipLaunchKernelGGL(k_dexpand, dim3(gsmall), dim3(256), 0, s, j, j.tw % 16 == 0 ? 1 : 0, we % 16 == 0 ? 1 : 0);
+  }
   hipLaunchKernelGGL(k_dunpred_fast, dim3(j.ntiles), dim3(64), (size_t)64 * ORING_PITCH + 6 * LAST_N(j.tw), s, j);
   {
     // On natural images most tiles hold copies, and a copy at a row's start that reads the end of
