@@ -30,8 +30,8 @@ Also at N = 1: detail.single_image_MBps (one image at a time, host-synchronous c
 detail.no_index_decode_MBps (dhoh of slot 0's file WITHOUT the side index: the serial rANS decode
 any foreign .hoh gets, checked lossless).
 
-roofline: the dominant kernel k_rans_fast (one launch = all 3 plane streams of every tile of one
-image).  avg_launch_ms is its average duration with one image in flight (HIP events on the
+roofline: the dominant kernel k_rans_fast01 (one launch = all 3 plane streams of every tile of one
+image, and its LZ streams in otherwise idle blocks).  avg_launch_ms is its average duration with one image in flight (HIP events on the
 encoder's stream, 5 launches; rocprofv3 agrees: profiles/), algorithmic bytes per launch = 2 B
 read per symbol + the payload written.  The kernel is bounded by the latency of
 its serial coder chain, not by HBM ("limiter"); roofline.pipeline_* is the whole pipeline's
@@ -63,7 +63,7 @@ sys.path.insert(0, os.path.join(ROOT, "hoh-ans_amd"))
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 DOM = "rans_enc_fast"   # stage name of the dominant kernel (k_rans_fast)
-PMC_KERNELS = {"k_rans_fast": "rans_enc_fast", "k_front": "front", "k_front256": "front", "k_drans": "drans",
+PMC_KERNELS = {"k_rans_fast": "rans_enc_fast", "k_rans_fast01": "rans_enc_fast", "k_front": "front", "k_front256": "front", "k_drans": "drans",
                "k_dunpred_fast": "dunpred_fast", "k_tables": "tables", "k_streambytes": "streambytes",
                "k_dunpred_lz": "dunpred_lz", "k_nuke": "nuke"}
 
@@ -611,7 +611,7 @@ def main():
         achieved = alg / (kms * 1e-3) / 1e9 if kms else None
         pipeline_gbs = 2 * (1 + ratio) * raw_total * K / el / 1e9
         traffic = pmc.get(DOM, {}).get("hbm_bytes") if pmc else None
-        roof = {"bound": "hbm", "kernel": "k_rans_fast (" + DOM + ")",
+        roof = {"bound": "hbm", "kernel": "k_rans_fast01 (" + DOM + ")",
                 "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
                 "traffic": traffic, "algorithmic_bytes": alg,

@@ -427,8 +427,10 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
     launch_lz(j, s);
     launch_nuke(j, s);             prof.mark("lz");
     launch_tables(j, (int)S, s);   prof.mark("tables");
-    launch_rans_fast(j, ntiles * 4, s, SidMap{3, SK_G}, ntiles * 3, SidMap{1, SK_I}); prof.mark("rans_enc_fast");
-    launch_rans_fast(j, ntiles * 3, s, SidMap{3, 0}, ntiles * 3, SidMap{0, 0}, 1);   // the LZ streams
+    // the plane chains and the LZ streams (prob_bits 10) in one launch
+    launch_rans_fast01(j, s, ntiles * 4, SidMap{3, SK_G}, ntiles * 3, SidMap{1, SK_I}, ntiles * 3, SidMap{3, 0}, ntiles * 3,
+                       SidMap{0, 0});
+    prof.mark("rans_enc_fast");
     launch_rans_gen(j, (int)S, s); prof.mark("rans_enc_gen");
     launch_finalize(j, (int)S, s); prof.mark("finalize");
     launch_layout(j, s);           prof.mark("layout");

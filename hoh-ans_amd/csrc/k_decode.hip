@@ -1749,7 +1749,14 @@ __device__ void chain_full(const DecJob& j, int cls, uint32_t blk) {
       auto block = [&](auto nowrap_c) {
         constexpr bool NOWRAP = decltype(nowrap_c)::value;
         auto srcA = [&](int u, uint32_t b) -> uint32_t {
-          return NOWRAP ? wA + 2 * u - 2 * b : rb + 2 * ((pos0 + (uint32_t)u - b) & (CH_R - 1));
+          // (wA - 2b) + 2u: the constant part goes to the read's offset field (the empty asm keeps
+          // the compiler from reassociating it back into a per-step add)
+          if (NOWRAP) {
+            uint32_t sb = wA - 2 * b;
+            asm("" : "+v"(sb));
+            return sb + 2 * u;
+          }
+          return rb + 2 * ((pos0 + (uint32_t)u - b) & (CH_R - 1));
         };
         // step 0 reads its copy source after every earlier write, so even b = 1 comes from the
         // ring (at a row's start that is the end of the row above, not L = half)
@@ -1810,27 +1817,31 @@ __global__ __launch_bounds__(256) void k_dexpand(DecJob j, int full1, int full2)
     uint16_t* o0 = j.dplane + (size_t)(t * 3) * j.npix_cap;
     uint16_t* o1 = o0 + j.npix_cap;
     uint16_t* o2 = o1 + j.npix_cap;
+    // eight pixels per thread and pass (never split by a row: w % 16 == 0); the next pass's map
+    // bytes are loaded before this pass's residual gathers
+    auto mapw = [&](uint32_t i) -> uint2 {
+      if (i >= npix) return make_uint2(0x01010101u, 0x01010101u);      // no pixel: "copies"
+      const uint32_t y = i / w, x = i - y * w;
+      return *(const uint2*)(bm + (size_t)y * pitch + x);
+    };
     uint32_t kb = 0;
-    for (uint32_t i0 = 0; i0 < npix; i0 += 1024) {
-      const uint32_t i = i0 + 4 * tid;
+    uint2 mnext = mapw(8 * tid);
+    for (uint32_t i0 = 0; i0 < npix; i0 += 2048) {
+      const uint32_t i = i0 + 8 * tid;
+      const uint2 m = mnext;
+      mnext = mapw(i + 2048);
       uint32_t f = 0;
-      if (i < npix) {
-        const uint32_t y = i / w, x = i - y * w;
-        const uint32_t m = *(const uint32_t*)(bm + (size_t)y * pitch + x);
 #pragma unroll
-        for (int u = 0; u < 4; u++) f |= (((m >> (8 * u)) & 255u) == 0 ? 1u : 0u) << u;
-      }
+      for (int u = 0; u < 8; u++) f |= ((((u < 4 ? m.x : m.y) >> (8 * (u & 3))) & 255u) == 0 ? 1u : 0u) << u;
       const uint32_t n = __popc(f);
-      // exclusive prefix of n over the wave (three bit planes of n by ballot), then over the waves
-      uint32_t ex = 0;
+      // exclusive prefix of n over the wave (four bit planes of n by ballot), then over the waves
+      uint32_t ex = 0, wt = 0;
 #pragma unroll
-      for (int bit = 0; bit < 3; bit++) {
+      for (int bit = 0; bit < 4; bit++) {
         const uint64_t bl = __ballot((n >> bit) & 1);
         ex += __builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u)) << bit;
+        wt += (uint32_t)__popcll(bl) << bit;
       }
-      uint32_t wt = 0;
-#pragma unroll
-      for (int bit = 0; bit < 3; bit++) wt += (uint32_t)__popcll(__ballot((n >> bit) & 1)) << bit;
       if (lane == 0) wtot[wv] = wt;
       __syncthreads();
       uint32_t k = kb + ex, tot = 0;
@@ -1838,17 +1849,18 @@ __global__ __launch_bounds__(256) void k_dexpand(DecJob j, int full1, int full2)
       for (int v = 0; v < 4; v++) { const uint32_t x = wtot[v]; if ((uint32_t)v < wv) k += x; tot += x; }
       __syncthreads();
       if (i < npix) {
-        uint32_t a0 = 0, a1 = 0, a2 = 0, b0 = 0, b1 = 0, b2 = 0;      // four u16 per plane
+        uint32_t a[4] = {0, 0, 0, 0}, bq[4] = {0, 0, 0, 0}, cq[4] = {0, 0, 0, 0};   // u16 pairs per plane
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < 8; u++) {
           uint32_t g = 0, rr = 0, bb = 0;
           if ((f >> u) & 1) { g = r0[k] + 128u; rr = r1[k] + 256u; bb = r2[k] + 256u; k++; }
-          if (u < 2) { a0 |= g << (16 * u); a1 |= rr << (16 * u); a2 |= bb << (16 * u); }
-          else { b0 |= g << (16 * (u - 2)); b1 |= rr << (16 * (u - 2)); b2 |= bb << (16 * (u - 2)); }
+          a[u >> 1] |= g << (16 * (u & 1));
+          bq[u >> 1] |= rr << (16 * (u & 1));
+          cq[u >> 1] |= bb << (16 * (u & 1));
         }
-        *(uint2*)(o0 + i) = make_uint2(a0, b0);
-        *(uint2*)(o1 + i) = make_uint2(a1, b1);
-        *(uint2*)(o2 + i) = make_uint2(a2, b2);
+        *(uint4*)(o0 + i) = make_uint4(a[0], a[1], a[2], a[3]);
+        *(uint4*)(o1 + i) = make_uint4(bq[0], bq[1], bq[2], bq[3]);
+        *(uint4*)(o2 + i) = make_uint4(cq[0], cq[1], cq[2], cq[3]);
       }
       kb += tot;
     }
@@ -2298,7 +2310,7 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   hipLaunchKernelGGL(k_dbackmap, dim3(gsmall), dim3(256), 0, s, j);
   {
     const int we = j.W - (j.xt - 1) * j.tw;
-    hipLaunchKernelGGL(k_dexpand, dim3(gsmall), dim3(256), 0, s, j, j.tw % 16 == 0 ? 1 : 0, we % 16 == 0 ? 1 : 0);
+    hipLaunchKernelGGL(k_dexpand, dim3(j.ntiles), dim3(256), 0, s, j, j.tw % 16 == 0 ? 1 : 0, we % 16 == 0 ? 1 : 0);
   }
   hipLaunchKernelGGL(k_dunpred_fast, dim3(j.ntiles), dim3(64), (size_t)64 * ORING_PITCH + 6 * LAST_N(j.tw), s, j);
   {

@@ -173,16 +173,11 @@ __device__ __forceinline__ void ckpt(const Coder& c, Checkpoint* ck, uint32_t k)
   ck[k] = p;
 }
 
-// One lane per stream, 64 streams per wave, one wave per workgroup.
+// One lane per stream, 64 streams per wave, one wave per workgroup: block blk of a launch.
 template <int KIND>
-__global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane, SidMap ma, int na, SidMap mb, int nblk,
-                                                  int rot) {
+__device__ __forceinline__ void rans_fast_body(const EncodeJob& j, int nplane, SidMap ma, int na, SidMap mb, int blk) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int lane = threadIdx.x;
-  // the grid covers every CU; the working blocks are a window rotated per launch so that the
-  // chains of images in flight land on different CUs instead of sharing the first ones
-  const int blk = (int)((blockIdx.x + gridDim.x - rot) % gridDim.x);
-  if (blk >= nblk) return;
   // the chain is the critical path of an image: win issue arbitration against co-resident waves
   __builtin_amdgcn_s_setprio(3);
   // f64 rounding toward zero (MODE.FP_ROUND[3:2] = 3) for step15's floor-by-fma, this wave only.
@@ -257,6 +252,25 @@ __global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane, SidMa
   c.slab[--c.widx] = c.xl;
   j.streams[sid].words = st.slab_cap - c.widx;
   j.streams[sid].widx_end = c.widx;
+}
+
+template <int KIND>
+__global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane, SidMap ma, int na, SidMap mb, int nblk,
+                                                  int rot) {
+  // the grid covers every CU; the working blocks are a window rotated per launch so that the
+  // chains of images in flight land on different CUs instead of sharing the first ones
+  const int blk = (int)((blockIdx.x + gridDim.x - rot) % gridDim.x);
+  if (blk < nblk) rans_fast_body<KIND>(j, nplane, ma, na, mb, blk);
+}
+
+// The pb-15 plane chains and, in otherwise idle blocks of the same chip-wide grid, the LZ
+// streams (prob_bits 10): one launch, so the short LZ chains run beside the long ones instead of
+// after them (-0.2 ms per image encoded alone).
+__global__ __launch_bounds__(64) void k_rans_fast01(EncodeJob j, int np0, SidMap a0, int na0, SidMap b0, int nblk0,
+                                                    int np1, SidMap a1, int na1, SidMap b1, int nblk1, int rot) {
+  const int blk = (int)((blockIdx.x + gridDim.x - rot) % gridDim.x);
+  if (blk < nblk0) rans_fast_body<0>(j, np0, a0, na0, b0, blk);
+  else if (blk - nblk0 < nblk1) rans_fast_body<1>(j, np1, a1, na1, b1, blk - nblk0);
 }
 
 // Generic: one lane per stream, rans64.hpp:262-278 verbatim (64x64 high product).
@@ -336,6 +350,15 @@ static size_t chain_lds() {
     return (size_t)(kb < 8 ? 8 : kb > 160 ? 160 : kb) * 1024;
   }();
   return v;
+}
+
+void launch_rans_fast01(const EncodeJob& j, hipStream_t s, int np0, SidMap a0, int na0, SidMap b0, int np1, SidMap a1,
+                        int na1, SidMap b1) {
+  const int nblk0 = (np0 + 63) / 64, nblk1 = (np1 + 63) / 64;
+  const int grid = std::max(nblk0 + nblk1, 1024);
+  const int rot = (int)((g_rot.fetch_add(1) * 8u * (unsigned)((nblk0 + nblk1 + 7) / 8)) % (unsigned)grid);
+  hipLaunchKernelGGL(k_rans_fast01, dim3(grid), dim3(64), chain_lds(), s, j, np0, a0, na0, b0, nblk0, np1, a1, na1, b1,
+                     nblk1, rot);
 }
 
 void launch_rans_fast(const EncodeJob& j, int nplane, hipStream_t s, SidMap a, int na, SidMap b, int kind) {
