@@ -315,20 +315,38 @@ __global__ __launch_bounds__(NT) void k_colours(EncodeJob j) {
   uint32_t x = tid, y = 0;
   while (x >= (uint32_t)w) { x -= w; y++; }
   __syncthreads();
-  for (uint32_t q = tid; q - tid < npix; q += NT) {
-    if (q < npix) {
-      const uint8_t* p = img + (size_t)y * pitch + (size_t)x * 3;
-      const uint32_t v = p[0] | (p[1] << 8) | (p[2] << 16);
-      uint32_t hsh = (v * 2654435761u) >> 23;
-      for (int probe = 0; probe < CSET; probe++) {
-        const uint32_t old = atomicCAS(&hset[hsh], 0xffffffffu, v);
-        if (old == 0xffffffffu) { atomicAdd(&s_ncol, 1); atomicMin(&hpos[hsh], q); break; }
-        if (old == v) { atomicMin(&hpos[hsh], q); break; }
-        hsh = (hsh + 1) & (CSET - 1);
+  const int lane = tid & 63;
+  // four 256-pixel blocks per barrier (their loads together); a pixel whose colour equals the
+  // previous lane's (the previous raster position, or its block's) skips the insert: that lane
+  // holds the smaller first position (flat tiles no longer send 256 CAS to one LDS word)
+  for (uint32_t q0 = 0; q0 < npix; q0 += 4 * NT) {
+    uint32_t v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint32_t q = q0 + (uint32_t)u * NT + tid;
+      v[u] = 0xffffffffu;
+      if (q < npix) {
+        const uint8_t* p = img + (size_t)y * pitch + (size_t)x * 3;
+        v[u] = p[0] | (p[1] << 8) | (p[2] << 16);
+      }
+      x += NT;
+      while (x >= (uint32_t)w) { x -= w; y++; }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint32_t q = q0 + (uint32_t)u * NT + tid;
+      const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp((int)v[u], (int)v[u], 0x138, 0xf, 0xf, false);
+      // (past 256 colours the tile is decided: stop filling the 512-slot set)
+      if (q < npix && (lane == 0 || v[u] != prev) && *(volatile int*)&s_ncol <= 256) {
+        uint32_t hsh = (v[u] * 2654435761u) >> 23;
+        for (int probe = 0; probe < CSET; probe++) {
+          const uint32_t old = atomicCAS(&hset[hsh], 0xffffffffu, v[u]);
+          if (old == 0xffffffffu) { atomicAdd(&s_ncol, 1); atomicMin(&hpos[hsh], q); break; }
+          if (old == v[u]) { atomicMin(&hpos[hsh], q); break; }
+          hsh = (hsh + 1) & (CSET - 1);
+        }
       }
     }
-    x += NT;
-    while (x >= (uint32_t)w) { x -= w; y++; }
     __syncthreads();
     if (s_ncol > 256) break;                         // block-uniform after the barrier
   }
