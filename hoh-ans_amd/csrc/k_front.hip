@@ -504,15 +504,16 @@ __device__ __forceinline__ uint32_t wt_put(uint32_t* key, uint32_t k) {
   return F2_TAB;
 }
 
-// the lanes that hold a slot's key: {max lane, 63 - min lane}, both by LDS max (cleared to 0)
-__device__ __forceinline__ void wt_lanes(uint32_t* pos, uint32_t sl, uint32_t lane) {
-  __hip_atomic_fetch_max(&pos[2 * sl], lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  __hip_atomic_fetch_max(&pos[2 * sl + 1], 63u - lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+// LDS max over the lanes that hold a slot's key (of `lane` or of 63 - lane; the word is cleared to 0)
+__device__ __forceinline__ void wt_max(uint32_t* pos, uint32_t sl, uint32_t v) {
+  __hip_atomic_fetch_max(&pos[sl], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 __global__ __launch_bounds__(NT) void k_front256(EncodeJob j) {
   __shared__ uint32_t tab[4][2][F2_TAB + 1];        // per wave: two alternating chunk tables
-  __shared__ __attribute__((aligned(8))) uint32_t tpos[4][2][2 * (F2_TAB + 1)];   // wt_lanes per slot
+  // per slot, one word: while its table is the current chunk's, 63 - the key's smallest lane; then
+  // (rewritten after the chunk's checks) the largest lane, for the next chunk's lookups
+  __shared__ uint32_t tpos[4][2][F2_TAB + 1];
   __shared__ uint32_t pring[4][F2_RING];
   __shared__ uint32_t hist[3 * 512 - 256];
   __shared__ int s_notgrey, s_ncand;
@@ -522,7 +523,7 @@ __global__ __launch_bounds__(NT) void k_front256(EncodeJob j) {
   const uint32_t npix = 256u * 256u;
   for (int i = tid; i < 3 * 512 - 256; i += NT) hist[i] = 0;
   for (int i = lane; i < 2 * (F2_TAB + 1); i += 64) tab[wv][i / (F2_TAB + 1)][i % (F2_TAB + 1)] = 0;
-  for (int i = lane; i < 4 * (F2_TAB + 1); i += 64) tpos[wv][i / (2 * (F2_TAB + 1))][i % (2 * (F2_TAB + 1))] = 0;
+  for (int i = lane; i < 2 * (F2_TAB + 1); i += 64) tpos[wv][i / (F2_TAB + 1)][i % (F2_TAB + 1)] = 0;
   if (tid == 0) { s_notgrey = 0; s_ncand = 0; }
   uint16_t* res0 = j.sym + med_plane_off(j, t, 0);
   uint16_t* res1 = j.sym + med_plane_off(j, t, 1);
@@ -566,7 +567,7 @@ __global__ __launch_bounds__(NT) void k_front256(EncodeJob j) {
       const uint32_t a3 = wshl1(a2, lane_of(cur[0], 2));
       const uint32_t k = fp32(pv, a1, a2, a3);
       slot_prev = wt_put(tab[wv][1], k);
-      if (slot_prev < F2_TAB) wt_lanes(tpos[wv][1], slot_prev, lane);
+      if (slot_prev < F2_TAB) wt_max(tpos[wv][1], slot_prev, lane);
       ring[(uint32_t)(ya * 256 - 64 + lane) & (F2_RING - 1)] = pv;
     }
     ring[(uint32_t)(ya * 256 + lane) & (F2_RING - 1)] = cur[0];
@@ -615,15 +616,15 @@ __global__ __launch_bounds__(NT) void k_front256(EncodeJob j) {
       const uint32_t* tp = tab[wv][cb ^ 1];
       const uint32_t* pp = tpos[wv][cb ^ 1];
       const uint32_t sq = hq ? wt_put(tc, hq) : F2_TAB;
-      if (sq < F2_TAB) wt_lanes(pc, sq, lane);
+      if (sq < F2_TAB) wt_max(pc, sq, 63u - lane);
       const uint32_t sp = hq ? wt_find(tp, hq) : F2_TAB;
       // Equal windows have equal fingerprints, so the windows before q equal to q's can only be
       // at the positions holding hq: in this chunk at lanes min..lane-1 (the earliest is checked),
       // in the previous chunk at lanes >= lane (distance <= 64; the latest, i.e. nearest, is
       // checked).  When a checked window differs (a fingerprint collision) the lane falls back
       // to the full test over b = 1..64 (lz.hpp:37-42 with offset < 4).
-      const uint32_t fcur = sq < F2_TAB ? 63u - pc[2 * sq + 1] : 64u;
-      const uint32_t lprev = sp < F2_TAB ? pp[2 * sp] : 0u;
+      const uint32_t fcur = sq < F2_TAB ? 63u - pc[sq] : 64u;
+      const uint32_t lprev = sp < F2_TAB ? pp[sp] : 0u;
       const bool ccur = fcur < (uint32_t)lane, cprev = sp < F2_TAB && lprev >= (uint32_t)lane;
       const uint64_t flag = __ballot(ccur || cprev);
       uint64_t word = 0;
@@ -647,12 +648,15 @@ __global__ __launch_bounds__(NT) void k_front256(EncodeJob j) {
         }
         word = __ballot(c);
       }
+      // this chunk's words turn into the largest lane for the next chunk's lookups (program order
+      // on one address: the fcur reads above come first)
+      if (sq < F2_TAB) { pc[sq] = 0; wt_max(pc, sq, lane); }
       if (lane == 0) cand[q >> 6] = word;
       ncand += lane == 0 ? __popcll(word) : 0;
       // empty the previous chunk's table for the next chunk (wave-ordered: every lookup is done)
       uint32_t* tpw = tab[wv][cb ^ 1];
       tpw[slot_prev] = 0;                             // slot F2_TAB is a spare: no branch
-      *(uint2*)&tpos[wv][cb ^ 1][2 * slot_prev] = make_uint2(0u, 0u);
+      tpos[wv][cb ^ 1][slot_prev] = 0;
       slot_prev = sq;
       cb ^= 1;
     }
