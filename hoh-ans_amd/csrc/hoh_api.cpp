@@ -375,7 +375,7 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   if ((e = ensure(c->hist, S * 512 * 4))) return e;
   if ((e = ensure(c->candbits, (size_t)ntiles * (j.npix_cap / 64) * 8))) return e;
   if ((e = ensure(c->matches, (size_t)ntiles * 3 * (j.lz_cap + 1) * 4))) return e;
-  if (!speed && (e = ensure(c->lzspec, (size_t)ntiles * j.lz_cap * 4))) return e;
+  if ((e = ensure(c->lzspec, (size_t)ntiles * j.lz_cap * (speed ? 8 : 4)))) return e;   // k_lz / k_lzscan segments
   if ((e = ensure(c->pal, (size_t)ntiles * 257 * 4))) return e;   // palettes, then colour counts
   if ((e = ensure(c->streams, S * sizeof(StreamInfo)))) return e;
   if ((e = ensure(c->tiles, (size_t)ntiles * sizeof(TileInfo)))) return e;

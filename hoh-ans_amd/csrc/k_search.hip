@@ -546,18 +546,24 @@ __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring)
 #define LZS_HB 16        // horizontal back-distance chunks of 64 whose fingerprints load at once
 #define LZS_VB 4         // vertical chunks (k * w <= 65536: 256 rows of a 256-wide tile)
 #define LZS_BITS 1024    // candidate words in LDS (tiles up to 65,536 pixels)
-// greedy scan (lz.hpp:32-95) over the candidates, one wave per tile, + the four LZ streams.
+#define LZS_SEG 4        // waves per tile at -s1 (segment walks stitched as in k_lz)
+// greedy scan (lz.hpp:32-95) over the candidates + the four LZ streams.
 // Per candidate one batch of global loads (its fingerprint, 16 chunks of 64 horizontal back
 // distances and the vertical ones) and then LDS only: the candidate bitmap is staged in LDS and
 // the run lengths compare pixels from an LDS ring of the positions [q - limit, q + 260) (filled
-// 64 positions at a time as the scan moves: each pixel read once per tile), eight positions per
+// 64 positions at a time as the scan moves: each pixel read once per tile), sixteen positions per
 // LDS round trip; vertical backs beyond the ring read the image.  rp = ring size (0: -s4, whose
 // 16384-position window does not fit next to the other workgroups; pixels from the image).
-__global__ __launch_bounds__(64) void k_lzscan(EncodeJob j, int limit, int rp) {
-  extern __shared__ uint32_t pring[];
+// nseg waves per tile (-s1: LZS_SEG; the larger rings of -s2..-s4 leave one): the tile's walk
+// is cut into segments walked at once and stitched by wave 0, exactly as k_lz does at -s0
+// (segment matches packed into lzspec as two words: pos | (len - 4) << 16, back).
+__global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit, int rp, int nseg_req) {
+  extern __shared__ uint32_t pring_all[];                              // nseg rings of rp + 16
   __shared__ uint64_t cb[LZS_BITS];
-  __shared__ uint32_t hl[LZS_HB * 64];                                 // a batch's hit list
-  const int t = blockIdx.x, lane = threadIdx.x;
+  __shared__ uint32_t vis[2 * LZS_BITS];                               // visited candidates
+  __shared__ uint16_t hl_all[LZS_SEG][LZS_HB * 64];                    // a batch's hit list per wave
+  __shared__ uint32_t s_cnt[LZS_SEG], s_exit[LZS_SEG];
+  const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   TileInfo ti = j.tiles[t];
   const uint32_t npix = (uint32_t)ti.w * ti.h, nwords = (npix + 63) / 64, w = ti.w;
   const uint64_t* bits = j.candbits + (size_t)t * (j.npix_cap / 64);
@@ -572,10 +578,18 @@ __global__ __launch_bounds__(64) void k_lzscan(EncodeJob j, int limit, int rp) {
   }
   const uint32_t thr = 4 + bonus;
   const bool lds_bits = nwords <= LZS_BITS;
-  if (ti.ncand && lds_bits) {
-    for (uint32_t i = lane; i < nwords; i += 64) cb[i] = bits[i];
-    __syncthreads();
+  const uint32_t nseg = (lds_bits && rp && nwords >= 4 * LZS_SEG && nseg_req > 1) ? (uint32_t)nseg_req : 1u;
+  const uint32_t segcap = j.lz_cap / LZS_SEG;
+  uint32_t* spec = j.lzspec + (size_t)t * 2 * j.lz_cap;
+  auto seg_lo = [&](uint32_t s) { return s >= nseg ? npix : (nwords * s / nseg) * 64; };
+  if (ti.ncand) {
+    for (uint32_t i = tid; i < nwords; i += 64 * LZS_SEG) cb[i] = lds_bits ? bits[i] : 0;
+    if (nseg > 1)
+      for (uint32_t i = tid; i < 2 * nwords; i += 64 * LZS_SEG) vis[i] = 0;
   }
+  __syncthreads();
+  uint32_t* pring = pring_all + (size_t)(wv < (int)nseg ? wv : 0) * (uint32_t)(rp + 16);
+  uint16_t* hl = hl_all[wv];
   const uint32_t rmask = (uint32_t)rp - 1;
   uint32_t wend = 0;
   auto fill_to = [&](uint32_t lo, uint32_t need) {
@@ -588,16 +602,16 @@ __global__ __launch_bounds__(64) void k_lzscan(EncodeJob j, int limit, int rp) {
       if (e < 16) pring[e + rp] = x;                                 // the mirror of entries 0..15
       wend += 64;
     }
-    // one-wave workgroup: its LDS accesses are ordered without a barrier
+    // the wave's own ring: its LDS accesses are ordered without a barrier
   };
   // run length of q against q - b (lz.hpp:37-45), at most 259
   auto runl = [&](uint32_t q, uint32_t b) -> uint32_t {
     const uint32_t lim = min(259u, npix - q);
     uint32_t L = 0;
     if (rp && b <= (uint32_t)limit) {
-      // sixteen positions per LDS round trip, the equal ones as a mask (trailing ones = the run)
       for (;;) {
-        // two bases (the mirror spares every read its wrap), the first unequal one by two chains
+        // sixteen positions per LDS round trip from two bases (the mirror spares every read its
+        // wrap), the first unequal one by two select chains
         const uint32_t* pa = pring + ((q + L) & rmask);
         const uint32_t* pc = pring + ((q + L - b) & rmask);
         uint32_t a[16], c[16];
@@ -618,27 +632,27 @@ __global__ __launch_bounds__(64) void k_lzscan(EncodeJob j, int limit, int rp) {
     }
     return L;
   };
-  uint32_t nm = 0, pos = 0;
-  bool overflow = false;
-  while (ti.ncand && pos < npix) {
-    uint32_t q = 0xffffffffu;
-    if (lds_bits && (pos >> 6) < nwords) {              // usually in pos's own word
-      const uint64_t wv = cb[pos >> 6] & (~0ull << (pos & 63));
-      if (wv) q = (pos & ~63u) + (uint32_t)(__ffsll((unsigned long long)wv) - 1);
+  // first candidate q >= pos (0xffffffff: none)
+  auto next_cand = [&](uint32_t pos) -> uint32_t {
+    if (pos >= npix) return 0xffffffffu;
+    if (lds_bits) {                                   // usually in pos's own word
+      const uint64_t wv2 = cb[pos >> 6] & (~0ull << (pos & 63));
+      if (wv2) return (pos & ~63u) + (uint32_t)(__ffsll((unsigned long long)wv2) - 1);
     }
-    if (q == 0xffffffffu)
     for (uint32_t wi = pos >> 6; wi < nwords; wi += 64) {
-      uint64_t wv = (wi + lane < nwords) ? (lds_bits ? cb[wi + lane] : bits[wi + lane]) : 0;
-      if (wi + lane == (pos >> 6)) wv &= ~0ull << (pos & 63);
-      const uint64_t bal = __ballot(wv != 0);
+      uint64_t w2 = (wi + lane < nwords) ? (lds_bits ? cb[wi + lane] : bits[wi + lane]) : 0;
+      if (wi + lane == (pos >> 6)) w2 &= ~0ull << (pos & 63);
+      const uint64_t bal = __ballot(w2 != 0);
       if (bal) {
         const int l = __ffsll((unsigned long long)bal) - 1;
-        const uint64_t word = __shfl(wv, l);
-        q = (wi + l) * 64 + (__ffsll((unsigned long long)word) - 1);
-        break;
+        const uint64_t word = __shfl(w2, l);
+        return (wi + l) * 64 + (__ffsll((unsigned long long)word) - 1);
       }
     }
-    if (q == 0xffffffffu) break;
+    return 0xffffffffu;
+  };
+  // (longest, back) at candidate q as the key (L << 17) | (LZS_KB - b)
+  auto measure = [&](uint32_t q) -> uint32_t {
     const uint32_t bm = q < (uint32_t)limit ? q : (uint32_t)limit;
     const uint32_t kmax = min(65536u, q) / w;                         // vertical: k * w <= min(65536, q)
     // one batch: f, the first 16 horizontal chunks, the vertical chunks
@@ -655,12 +669,11 @@ __global__ __launch_bounds__(64) void k_lzscan(EncodeJob j, int limit, int rp) {
       fw[c] = k <= kmax ? F[q - k * w] : 0u;
     }
     if (rp) fill_to(q >= (uint32_t)limit ? q - (uint32_t)limit : 0u, q + 260);
-    // horizontal: b = 1 .. min(limit, q), longest first, then the smallest b; stop at 259.  Each
-    // lane keeps its own best key over the chunks and the wave reduces once per candidate (a
-    // reduction per chunk with hits cost ~12 cross-lane steps each: textured natural regions hit
-    // in most of the 16 chunks); a chunk in which some lane reaches 259 ends the walk, so the
-    // smallest such b wins as in the reference's short circuit (lz.hpp:47-50).
-    // keys (L << 17) | (LZS_KB - b): L <= 259, b <= 65536 < LZS_KB
+    // horizontal: b = 1 .. min(limit, q), longest first, then the smallest b.  Each batch's hits
+    // (equal fingerprints) are listed in LDS and measured 64 at a time; every hit is measured
+    // (no stop at the first 259): the maximum key is the same, the smallest b of length 259
+    // winning as in the reference's short circuit (lz.hpp:47-50).  A batch with a 259 ends the
+    // walk.  Keys (L << 17) | (LZS_KB - b): L <= 259, b <= 65536 < LZS_KB.
     uint32_t mine = 0;
     bool done = false;
     for (uint32_t g0 = 1; g0 <= bm && !done; g0 += 64 * LZS_HB) {
@@ -671,11 +684,6 @@ __global__ __launch_bounds__(64) void k_lzscan(EncodeJob j, int limit, int rp) {
           fv[c] = b <= bm ? F[q - b] : 0u;
         }
       }
-      // the batch's hits (equal fingerprints) listed in LDS, then measured 64 at a time: a
-      // textured region hits a few lanes in most chunks, and a chunk at a time left most lanes
-      // idle through a run-length loop per chunk.  Every hit is measured (no stop at the first
-      // 259): the maximum key is the same, the smallest b of length 259 winning as in the
-      // reference's short circuit (lz.hpp:47-50).
       uint32_t tot = 0;
 #pragma unroll
       for (int c = 0; c < LZS_HB; c++) {
@@ -683,7 +691,7 @@ __global__ __launch_bounds__(64) void k_lzscan(EncodeJob j, int limit, int rp) {
         const uint64_t m = __ballot(hit);
         if (hit)
           hl[tot + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
-              g0 + 64 * c + lane;
+              (uint16_t)(g0 + 64 * c + lane);                          // b <= limit <= 16384
         tot += (uint32_t)__popcll(m);
       }
       bool top = false;
@@ -718,18 +726,83 @@ __global__ __launch_bounds__(64) void k_lzscan(EncodeJob j, int limit, int rp) {
       const uint32_t vb = wave_max_u32(vmine);
       if ((vb >> 17) > (best >> 17)) best = vb;
     }
-    const uint32_t longest = best >> 17, bb = LZS_KB - (best & LZS_KB);
-    if (longest >= thr) {
-      if (nm < j.lz_cap) {
-        if (lane == 0) { mt[3 * nm] = q; mt[3 * nm + 1] = longest; mt[3 * nm + 2] = bb; }
-      } else {
-        overflow = true;
-      }
-      nm++;
-      pos = q + longest;
+    return best;
+  };
+  uint32_t nm = 0;
+  bool overflow = false;
+  auto emit = [&](uint32_t q, uint32_t longest, uint32_t bb) {
+    if (nm < j.lz_cap) {
+      if (lane == 0) { mt[3 * nm] = q; mt[3 * nm + 1] = longest; mt[3 * nm + 2] = bb; }
     } else {
-      pos = q + 1;
+      overflow = true;
     }
+    nm++;
+  };
+  // ---- phase 1: every segment's own walk (nseg == 1: the serial walk, straight into mt)
+  if (ti.ncand && (uint32_t)wv < nseg) {
+    const uint32_t lo = seg_lo(wv), hi = seg_lo(wv + 1);
+    uint32_t pos = lo, cnt = 0;
+    while (pos < hi) {
+      const uint32_t q = next_cand(pos);
+      if (q >= hi) break;
+      if (nseg > 1 && lane == 0) atomicOr(&vis[q >> 5], 1u << (q & 31));
+      const uint32_t best = measure(q);
+      const uint32_t longest = best >> 17, bb = LZS_KB - (best & LZS_KB);
+      if (longest >= thr) {
+        if (nseg == 1) emit(q, longest, bb);
+        else if (cnt < segcap && lane == 0) {
+          spec[2 * (wv * segcap + cnt)] = q | ((longest - 4) << 16);
+          spec[2 * (wv * segcap + cnt) + 1] = bb;
+        }
+        cnt++;
+        pos = q + longest;
+      } else {
+        pos = q + 1;
+      }
+    }
+    if (lane == 0) { s_cnt[wv] = cnt; s_exit[wv] = max(pos, hi); }
+  }
+  if (nseg > 1) {
+    __syncthreads();
+    if (wv) return;
+    // ---- phase 2 (wave 0): stitch the segments (k_lz)
+    uint32_t pos = 0;
+    for (uint32_t s = 0; s < (ti.ncand ? nseg : 0u); s++) {
+      const uint32_t hi = seg_lo(s + 1), cnt = s_cnt[s];
+      if (cnt > segcap) { overflow = true; nm += cnt; continue; }     // cannot happen: lz_cap >= npix / 4 + 16
+      uint32_t from = 0;
+      bool conv = s == 0;
+      if (s > 0) {
+        while (pos < hi) {
+          const uint32_t q = next_cand(pos);
+          if (q >= hi) { pos = hi; break; }
+          if ((vis[q >> 5] >> (q & 31)) & 1) { conv = true; pos = q; break; }
+          const uint32_t best = measure(q);
+          const uint32_t longest = best >> 17, bb = LZS_KB - (best & LZS_KB);
+          if (longest >= thr) { emit(q, longest, bb); pos = q + longest; }
+          else pos = q + 1;
+        }
+        if (conv) {                                                   // first entry at or after pos
+          from = cnt;
+          for (uint32_t i0 = 0; i0 < cnt; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            const uint64_t m = __ballot(i < cnt && (spec[2 * (s * segcap + i)] & 0xffffu) >= pos);
+            if (m) { from = i0 + (uint32_t)(__ffsll((unsigned long long)m) - 1); break; }
+          }
+        }
+      }
+      if (conv) {
+        for (uint32_t i = from + lane; i < cnt; i += 64) {
+          const uint32_t e0 = spec[2 * (s * segcap + i)], e1 = spec[2 * (s * segcap + i) + 1], k = nm + (i - from);
+          if (k < j.lz_cap) { mt[3 * k] = e0 & 0xffffu; mt[3 * k + 1] = (e0 >> 16) + 4; mt[3 * k + 2] = e1; }
+        }
+        nm += cnt - from;
+        if (nm > j.lz_cap) overflow = true;
+        pos = s_exit[s];
+      }
+    }
+  } else if (wv) {
+    return;
   }
   // streams (lz.hpp:75-95): future, length - 4, back % 256, back / 256 (as u8)
   uint16_t* lz0 = j.sym + lz_sym_off_s(j, t, 0);
@@ -1056,7 +1129,11 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, void (*mark)(void*, const
   int rp = 1;
   while (rp < limit + 324) rp <<= 1;
   if (rp > 8192) rp = 0;                                              // -s4: pixels from the image
-  hipLaunchKernelGGL(k_lzscan, dim3(j.ntiles), dim3(64), (size_t)(rp ? rp + 16 : 1) * 4, s, j, limit, rp);
+  // -s1 (ring 2048): four segment walks per tile (four rings: two workgroups per CU); the larger
+  // rings of -s2..-s4 keep one walk per tile
+  const int nseg = rp && rp <= 2048 ? LZS_SEG : 1;
+  hipLaunchKernelGGL(k_lzscan, dim3(j.ntiles), dim3(64 * LZS_SEG), (size_t)nseg * (rp ? rp + 16 : 1) * 4, s, j, limit, rp,
+                     nseg);
   launch_nuke(j, s);
   mark(mc, "lz");
   hipLaunchKernelGGL(k_setup_s, dim3(j.ntiles), dim3(128), 0, s, j);
