@@ -501,30 +501,88 @@ __global__ __launch_bounds__(NT) void k_lzfp(EncodeJob j) {
 // q - b for some b <= min(limit, q), or at q - k*w with k*w <= 65536 (lz.hpp:35, :55); equal
 // windows have equal fingerprints, so the screen never misses one.  Chunks of 256 positions in
 // order, the last `limit` fingerprints in an LDS ring.
+// The horizontal test is answered from LDS hash tables before any ring walk:
+//  - three window tables (2048 slots each, three hashes of f): the latest position p < base whose
+//    fingerprint hashed to the slot, (p + 1) << 8 | tag(f), by LDS atomic max (positions in the
+//    high 24 bits, so the max is the latest; tiles hold < 2^24 pixels).  An occurrence of f in the
+//    window updated all three slots, so one slot whose latest position is older than q - bm is an
+//    exact no; a slot holding f's tag is a yes (an 8-bit tag collision only adds a candidate,
+//    which k_lzscan measures and drops);
+//  - two chunk tables (1024 slots each): the first position of the chunk per slot (atomic min);
+//    a first position equal to q is an exact no for the chunk, an earlier one holding f a yes.
+// Only a lane whose every slot is held by other fingerprints is walked: the wave walks each such
+// lane's window together.  40 KB of LDS at -s1 (ring 8 KB, tables 24 + 8 KB): four tiles per CU.
+#define LZC_W 2048
+#define LZC_C 1024
+__device__ __forceinline__ uint32_t lzc_h(uint32_t f, int k) {
+  return k == 0 ? (f >> 1) & (LZC_W - 1) : k == 1 ? (f >> 12) & (LZC_W - 1) : (f * 0x9E3779B1u) >> 21;
+}
 __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring) {
   extern __shared__ uint32_t fr[];
+  uint32_t* ht = fr + ring;                                            // window tables
+  uint32_t* ct = ht + 3 * LZC_W;                                       // chunk tables
   const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const TileInfo ti = j.tiles[t];
   const uint32_t npix = (uint32_t)ti.w * ti.h, w = ti.w;
   const uint32_t* F = j.fpb + (size_t)t * j.npix_cap;
   uint64_t* cand = j.candbits + (size_t)t * (j.npix_cap / 64);
+  for (uint32_t e = tid; e < 3 * LZC_W; e += NT) ht[e] = 0u;
+  for (uint32_t e = tid; e < 2 * LZC_C; e += NT) ct[e] = 0xffffffffu;
+  __syncthreads();
   uint32_t ncand = 0;
   for (uint32_t base = 0; base < npix; base += NT) {
     const uint32_t q = base + tid;
     const uint32_t f = q < npix ? F[q] : 0u;
+    const uint32_t tag = f >> 24;
+    const uint32_t hs0 = lzc_h(f, 0), hs1 = LZC_W + lzc_h(f, 1), hs2 = 2 * LZC_W + lzc_h(f, 2);
+    const uint32_t cs0 = (f >> 1) & (LZC_C - 1), cs1 = LZC_C + ((f >> 12) & (LZC_C - 1));
     fr[q & (ring - 1)] = f;
-    __syncthreads();
-    bool c = false;
     if (f) {
-      // eight ring entries per LDS round trip, sixteen rows per batch of global loads
-      const uint32_t bm = q < (uint32_t)limit ? q : (uint32_t)limit;
-      for (uint32_t b0 = 1; b0 <= bm && !c; b0 += 8) {
-        uint32_t v[8];
+      atomicMin(&ct[cs0], tid);
+      atomicMin(&ct[cs1], tid);
+    }
+    __syncthreads();
+    bool c = false, walk = false;
+    const uint32_t bm = q < (uint32_t)limit ? q : (uint32_t)limit;
+    if (f) {
+      // earlier in the chunk
+      const uint32_t m0 = ct[cs0], m1 = ct[cs1];
+      const bool first = m0 == (uint32_t)tid || m1 == (uint32_t)tid;
+      c = (m0 < (uint32_t)tid && fr[(base + m0) & (ring - 1)] == f) ||
+          (m1 < (uint32_t)tid && fr[(base + m1) & (ring - 1)] == f);
+      walk = !first && !c;
+      if (!c) {
+        // in the window before the chunk
+        bool none = false, yes = false;
+        const uint32_t hw[3] = {ht[hs0], ht[hs1], ht[hs2]};
 #pragma unroll
-        for (int u = 0; u < 8; u++) v[u] = fr[(q - b0 - u) & (ring - 1)];
-#pragma unroll
-        for (int u = 0; u < 8; u++) c |= b0 + u <= bm && v[u] == f;
+        for (int k = 0; k < 3; k++) {
+          const uint32_t p1 = hw[k] >> 8;
+          const bool recent = p1 && q - (p1 - 1) <= bm;
+          none |= !recent;
+          yes |= recent && (hw[k] & 0xffu) == tag;
+        }
+        c = yes && !none;
+        walk = walk || (!none && !yes);
       }
+    }
+    // the uncertain lanes, one at a time by the whole wave: 64 window entries per LDS read
+    // (consecutive addresses), a ballot per read, out at the first equal fingerprint
+    for (uint64_t um = __ballot(walk && !c); um; um &= um - 1) {
+      const int l = __ffsll((unsigned long long)um) - 1;
+      const uint32_t fl = __shfl(f, l), ql = __shfl(q, l), bl = __shfl(bm, l);
+      bool hit = false;
+      for (uint32_t b0 = 1; b0 <= bl && !hit; b0 += 64) {
+        const uint32_t b = b0 + lane;
+        hit = __ballot(b <= bl && fr[(ql - b) & (ring - 1)] == fl) != 0;
+      }
+      if (lane == l) c = hit;
+    }
+    if (f && !c) {
+#ifdef HOH_LZC_NOV                                                     // measurement knob (invalid files)
+      (void)w;
+#else
+      // vertical backs beyond the window: sixteen rows per batch of (coalesced) global loads
       const uint32_t vlim = min(65536u, q);
       for (uint32_t b0 = (bm / w + 1) * w; b0 <= vlim && !c; b0 += 16 * w) {
         uint32_t v[16];
@@ -533,10 +591,20 @@ __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring)
 #pragma unroll
         for (int u = 0; u < 16; u++) c |= v[u] == f;
       }
+#endif
     }
     const uint64_t word = __ballot(c);
     if (lane == 0 && q < npix) cand[q >> 6] = word;
     ncand += lane == 0 ? (uint32_t)__popcll(word) : 0u;
+    __syncthreads();                                                   // every check has read the tables
+    if (f) {
+      ct[cs0] = 0xffffffffu;
+      ct[cs1] = 0xffffffffu;
+      const uint32_t e = ((q + 1) << 8) | tag;
+      atomicMax(&ht[hs0], e);
+      atomicMax(&ht[hs1], e);
+      atomicMax(&ht[hs2], e);
+    }
     __syncthreads();
   }
   if (lane == 0 && ncand) atomicAdd(&j.tiles[t].ncand, ncand);
@@ -1125,7 +1193,7 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, void (*mark)(void*, const
   hipLaunchKernelGGL(k_search, dim3(j.ntiles * HOH_NPLANE_S), dim3(NT), sizeof(SearchLds), s, j);
   mark(mc, "search");
   hipLaunchKernelGGL(k_lzfp, dim3(16, j.ntiles), dim3(NT), 0, s, j);
-  hipLaunchKernelGGL(k_lzcand, dim3(j.ntiles), dim3(NT), (size_t)ring * 4, s, j, limit, ring);
+  hipLaunchKernelGGL(k_lzcand, dim3(j.ntiles), dim3(NT), (size_t)(ring + 3 * LZC_W + 2 * LZC_C) * 4, s, j, limit, ring);
   int rp = 1;
   while (rp < limit + 324) rp <<= 1;
   if (rp > 8192) rp = 0;                                              // -s4: pixels from the image
