@@ -256,6 +256,8 @@ void launch_lz(const EncodeJob& j, hipStream_t s);
 void launch_tables(const EncodeJob& j, int nstreams, hipStream_t s, SidMap m = SidMap{0, 0});
 // kind 0: prob_bits-15 streams; 1: any prob_bits 7..19; 2: the same, size-only trial encodes
 void launch_rans_fast(const EncodeJob& j, int nplane, hipStream_t s, SidMap a, int na, SidMap b, int kind = 0);
+void launch_rans_fast_s(const EncodeJob& j, hipStream_t s, int np0, SidMap a0, int na0, SidMap b0, int np2, SidMap a2,
+                        int na2, int np1, SidMap a1, int na1);
 void launch_rans_fast01(const EncodeJob& j, hipStream_t s, int np0, SidMap a0, int na0, SidMap b0, int np1, SidMap a1,
                         int na1, SidMap b1);
 void launch_rans_gen(const EncodeJob& j, int nstreams, hipStream_t s, SidMap m = SidMap{0, 0});

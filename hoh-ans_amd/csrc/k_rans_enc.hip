@@ -273,6 +273,19 @@ __global__ __launch_bounds__(64) void k_rans_fast01(EncodeJob j, int np0, SidMap
   else if (blk - nblk0 < nblk1) rans_fast_body<1>(j, np1, a1, na1, b1, blk - nblk0);
 }
 
+// -s>=1: the real pb-15 encodes (KIND 0), every size-only trial of the prob_bits ladder (KIND 2)
+// and the other real encodes (KIND 1: LZ / predictor-map streams) are independent, so they share
+// one launch: an image waits for one chain length instead of three.  One chain per SIMD (a 40 KB
+// request per one-wave workgroup: four per CU), the long chains first in the grid.
+__global__ __launch_bounds__(64) void k_rans_fast_s(EncodeJob j, int np0, SidMap a0, int na0, SidMap b0, int nblk0,
+                                                    int np2, SidMap a2, int na2, int nblk2,
+                                                    int np1, SidMap a1, int na1, int nblk1) {
+  const int blk = (int)blockIdx.x;
+  if (blk < nblk0) rans_fast_body<0>(j, np0, a0, na0, b0, blk);
+  else if (blk - nblk0 < nblk2) rans_fast_body<2>(j, np2, a2, na2, SidMap{0, 0}, blk - nblk0);
+  else if (blk - nblk0 - nblk2 < nblk1) rans_fast_body<1>(j, np1, a1, na1, SidMap{0, 0}, blk - nblk0 - nblk2);
+}
+
 // Generic: one lane per stream, rans64.hpp:262-278 verbatim (64x64 high product).
 __global__ __launch_bounds__(64) void k_rans_gen(EncodeJob j, int nstreams, SidMap sm) {
   const int i = blockIdx.x * 64 + threadIdx.x;
@@ -379,6 +392,15 @@ void launch_rans_fast(const EncodeJob& j, int nplane, hipStream_t s, SidMap a, i
     hipLaunchKernelGGL(k_rans_fast<1>, dim3(grid), dim3(64), WIN * 4 * 64, s, j, nplane, a, na, b, nblk, rot);
   else   // size-only trial encodes: no window; one chain per SIMD (40 KB), all at once
     hipLaunchKernelGGL(k_rans_fast<2>, dim3(grid), dim3(64), 40 * 1024, s, j, nplane, a, na, b, nblk, rot);
+}
+
+void launch_rans_fast_s(const EncodeJob& j, hipStream_t s, int np0, SidMap a0, int na0, SidMap b0, int np2, SidMap a2,
+                        int na2, int np1, SidMap a1, int na1) {
+  const int nblk0 = (np0 + 63) / 64, nblk2 = (np2 + 63) / 64, nblk1 = (np1 + 63) / 64;
+  if (nblk0 + nblk2 + nblk1 == 0) return;
+  static_assert(WIN * 4 * 64 <= 40 * 1024, "the window fits the 40 KB request");
+  hipLaunchKernelGGL(k_rans_fast_s, dim3(nblk0 + nblk2 + nblk1), dim3(64), 40 * 1024, s, j, np0, a0, na0, b0, nblk0,
+                     np2, a2, na2, nblk2, np1, a1, na1, nblk1);
 }
 
 void launch_rans_gen(const EncodeJob& j, int nstreams, hipStream_t s, SidMap m) {

@@ -142,8 +142,11 @@ struct SearchLds {
   double ent[512];
   double cost[HOH_MAPCAP * 14];
   uint32_t hist[512];
+#ifdef HOH_SEARCH_LDSWALK  // the cell walk's state in LDS (measurement variant of cell_cost_reg)
   uint16_t top[NT][42];   // rows of 21 / 11 dwords (odd): the lanes' same-column accesses hit
   uint8_t bp[NT][44];     // distinct banks (40 / 40 gave 4- / 2-way conflicts)
+#endif
+  uint8_t brow[2][1024];  // the final pass's best predictors of two rows
   uint16_t plist[HOH_MAPCAP];
   uint8_t pidx[HOH_MAPCAP];
 };
@@ -188,6 +191,111 @@ __device__ double cell_cost(const uint16_t* D, int w, int h, int depth, int xt, 
       top[xm] = (uint16_t)v;
       L = v;
       bp[xm] = (uint8_t)best_pred(v, p, mask, c);
+    }
+  }
+  return cost;
+}
+
+// cell_cost for a one-predictor mask {k}, k in {0, 1, 4, 5} (kMasks[0..3]): best_pred then always
+// returns k (|v - p| < c < 2c), so bp[] is 4 where it still holds its initial value (row 0 of the
+// cell; bp[tw - 1] also when the cell is cut by the plane edge, vw < tw) and k elsewhere, and a step
+// needs only L, T, TL: predictors 0 (L), 1 (T), 4 (MED) and 5 (midp(L, T)).  Same pixels, same
+// f64 additions in the same order as cell_cost.
+#define CELL_MAX 40     // tw = ceil(w / ceil(w / 40)) <= 40, likewise th
+__device__ double cell_cost_one(const uint16_t* D, int w, int h, int depth, int xt, int yt, int cx, int cy,
+                                uint32_t k, const double* ent) {
+  const int c = 1 << depth, half = c >> 1;
+  const int tw = (w + xt - 1) / xt, th = (h + yt - 1) / yt;
+  const int x0 = cx * tw, y0 = cy * th;
+  const int vw = min(tw, w - x0);
+  // the row above and the current row in registers (the walk has no other state: every value
+  // is an original), each row's loads issued together instead of one pixel ahead
+  uint32_t up[CELL_MAX], cur[CELL_MAX];
+#pragma unroll
+  for (int i = 0; i < CELL_MAX; i++) up[i] = (i < tw && cy) ? D[(long)y0 * w + x0 + i - w] : (uint32_t)half;
+  double cost = 0.0;
+  for (int ym = 0; ym < th && y0 + ym < h; ym++) {
+    uint32_t L, TL;
+    if (cx) {
+      L = D[(long)(y0 + ym) * w + x0 - 1];
+      TL = (ym || cy) ? D[(long)(y0 + ym - 1) * w + x0 - 1] : (uint32_t)half;
+    } else {
+      L = TL = half;
+    }
+    const uint16_t* row = D + (long)(y0 + ym) * w + x0;
+#pragma unroll
+    for (int i = 0; i < CELL_MAX; i++) cur[i] = i < vw ? row[i] : 0u;
+    const bool a4 = ym == 0, b4first = !(ym > 0 && vw == tw);
+#pragma unroll
+    for (int xm = 0; xm < CELL_MAX; xm++) {
+      if (xm < vw) {
+        const uint32_t v = cur[xm], T = up[xm];
+        const uint32_t med = med16s(T, L, (T + L - TL) & 0xffffu);
+        const uint32_t pk = k == 0 ? L : k == 1 ? T : k == 4 ? med : midp(L, T);
+        const uint32_t pa = a4 ? med : pk, pb = (xm == 0 && b4first) ? med : pk;
+        const uint32_t pr = midp(pa, pb);
+        const uint32_t r = ((uint32_t)((int)v - (int)pr + half + c)) & (uint32_t)(c - 1);
+        cost += ent[r];
+        TL = T;
+        up[xm] = v;
+        L = v;
+      }
+    }
+  }
+  return cost;
+}
+
+// cell_cost with the cell's state in registers: the row above (T, and TR up to the cell's last
+// column, whose TR is this row's first value: top[0] is already overwritten there), this row,
+// and the row above's best predictors as nibbles (bp[]: 4 until written).  Every value of the
+// walk is an original, so the only serial part is the f64 sum, kept in raster order.
+__device__ double cell_cost_reg(const uint16_t* D, int w, int h, int depth, int xt, int yt, int cx, int cy,
+                                uint32_t mask, const double* ent) {
+  const int c = 1 << depth, half = c >> 1;
+  const int tw = (w + xt - 1) / xt, th = (h + yt - 1) / yt;
+  const int x0 = cx * tw, y0 = cy * th;
+  const int vw = min(tw, w - x0);
+  uint32_t up[CELL_MAX], cur[CELL_MAX], bpk[CELL_MAX / 8];
+#pragma unroll
+  for (int i = 0; i < CELL_MAX; i++) up[i] = (i < tw && cy) ? D[(long)y0 * w + x0 + i - w] : (uint32_t)half;
+#pragma unroll
+  for (int i = 0; i < CELL_MAX / 8; i++) bpk[i] = 0x44444444u;
+  double cost = 0.0;
+  for (int ym = 0; ym < th && y0 + ym < h; ym++) {
+    uint32_t L, TL;
+    if (cx) {
+      L = D[(long)(y0 + ym) * w + x0 - 1];
+      TL = (ym || cy) ? D[(long)(y0 + ym - 1) * w + x0 - 1] : (uint32_t)half;
+    } else {
+      L = TL = half;
+    }
+    const uint16_t* row = D + (long)(y0 + ym) * w + x0;
+#pragma unroll
+    for (int i = 0; i < CELL_MAX; i++) cur[i] = i < vw ? row[i] : 0u;
+    // bp[tw - 1] of the row above (the left neighbour's predictor at xm = 0)
+    uint32_t wl = bpk[0];
+#pragma unroll
+    for (int i = 1; i < CELL_MAX / 8; i++) wl = (tw - 1) / 8 == i ? bpk[i] : wl;
+    const uint32_t bl0 = (wl >> (4 * ((tw - 1) & 7))) & 15u;
+    uint32_t bB = bl0;
+#pragma unroll
+    for (int xm = 0; xm < CELL_MAX; xm++) {
+      if (xm < vw) {
+        const uint32_t v = cur[xm], T = up[xm];
+        const uint32_t TR = (xm + 1 == tw || xm + 1 == CELL_MAX) ? cur[0] : up[xm + 1 < CELL_MAX ? xm + 1 : 0];
+        Preds p;
+        preds16(L, T, TL, TR, false, p);
+        const uint32_t bA = (bpk[xm / 8] >> (4 * (xm & 7))) & 15u;
+        const uint32_t pr = midp(pick(p, bA), pick(p, bB));
+        const uint32_t r = ((uint32_t)((int)v - (int)pr + half + c)) & (uint32_t)(c - 1);
+        cost += ent[r];
+        TL = T;
+        up[xm] = v;
+        L = v;
+        const uint32_t nb = best_pred(v, p, mask, c);
+        bpk[xm / 8] = (bpk[xm / 8] & ~(15u << (4 * (xm & 7)))) | (nb << (4 * (xm & 7)));
+        bB = nb;
+      }
     }
   }
   return cost;
@@ -282,10 +390,22 @@ __global__ __launch_bounds__(NT) void k_search(EncodeJob j) {
       for (int i = tid; i < c; i += NT) S.ent[i] = lg[1 + S.hist[i]];
       __syncthreads();
     }
+    // mask-major task order: a wave's lanes share one or two masks, so the one-predictor masks
+    // (kMasks[0..3], ~7x fewer instructions per pixel) take whole waves off the full walk
+#ifdef HOH_SEARCH_NOCOST                                              // measurement knob (invalid files)
+    for (int k = tid; k < ncell * npred; k += NT) S.cost[(k % ncell) * 14 + k / ncell] = 0.0;
+    if (0)
+#endif
     for (int k = tid; k < ncell * npred; k += NT) {
-      const int cell = k / npred, m = k % npred;
-      S.cost[cell * 14 + m] = cell_cost(D, w, h, depth, xt, yt, cell % xt, cell / xt, kMasks[m], S.ent,
-                                        S.top[tid], S.bp[tid]);
+      const int m = k / ncell, cell = k % ncell;
+      const uint32_t mk = kMasks[m];
+      S.cost[cell * 14 + m] =
+          m < 4 ? cell_cost_one(D, w, h, depth, xt, yt, cell % xt, cell / xt, (uint32_t)__builtin_ctz(mk), S.ent)
+#ifdef HOH_SEARCH_LDSWALK
+                : cell_cost(D, w, h, depth, xt, yt, cell % xt, cell / xt, mk, S.ent, S.top[tid], S.bp[tid]);
+#else
+                : cell_cost_reg(D, w, h, depth, xt, yt, cell % xt, cell / xt, mk, S.ent);
+#endif
     }
     __syncthreads();
     for (int cell = tid; cell < ncell; cell += NT) {
@@ -302,12 +422,31 @@ __global__ __launch_bounds__(NT) void k_search(EncodeJob j) {
   }
   // final channelpredict_all residuals, in place over the staged data: rows from the last up,
   // each row read completely before it is overwritten (reads reach rows y-2..y only)
+  // Each row's best predictors are computed once: bnext holds row y's (from the previous
+  // iteration; the last row's are 0, :214-216), bcur gets row y - 1's, so a pixel costs one
+  // bp_all and one predictor set instead of resid_all's two and three.  w <= 1024 (hoh_api).
+  uint8_t* bnext = S.brow[0];
+  uint8_t* bcur = S.brow[1];
+  for (int i = tid; i < w; i += NT) bnext[i] = 0;
   for (int i = tid; i < 512; i += NT) S.hist[i] = 0;
   __syncthreads();
+#ifdef HOH_SEARCH_NOFINAL                                             // measurement knob (invalid files)
+  if (0)
+#endif
   for (int y = h - 1; y >= 0; y--) {
+    if (y > 0)
+      for (int x = tid; x < w; x += NT) bcur[x] = (uint8_t)bp_all(a, x, y - 1);
+    __syncthreads();
     uint32_t rv[4];
     int n = 0;
-    for (int x = tid; x < w && n < 4; x += NT) rv[n++] = resid_all(a, x, y);   // w < 512
+    for (int x = tid; x < w && n < 4; x += NT) {                      // resid_all(a, x, y)
+      const uint32_t bA = y ? bcur[x] : 4u;
+      const uint32_t bB = x ? bnext[x - 1] : (y ? bcur[w - 1] : 4u);
+      Preds p;
+      preds_all_at(a, x, y, p);
+      const uint32_t pr = midp(pick(p, bA), pick(p, bB));
+      rv[n++] = ((uint32_t)((int)D[(long)y * w + x] - (int)pr + half + c)) & (uint32_t)(c - 1);
+    }
     __syncthreads();
     n = 0;
     for (int x = tid; x < w && n < 4; x += NT) {
@@ -316,6 +455,9 @@ __global__ __launch_bounds__(NT) void k_search(EncodeJob j) {
       n++;
     }
     __syncthreads();
+    uint8_t* const b = bnext;                                           // row y - 1 is next
+    bnext = bcur;
+    bcur = b;
   }
   for (int i = tid; i < 512; i += NT) fh[i] = S.hist[i];
   // predictor map: used masks and their order (:279-307)
@@ -1208,11 +1350,11 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, void (*mark)(void*, const
   const int S = j.ntiles * SPT_S;
   launch_tables(j, S, s);
   mark(mc, "tables");
-  launch_rans_fast(j, j.ntiles * 6, s, SidMap{3, KS_MED}, j.ntiles * 3, SidMap{3, KS_MED + 3});
-  // the prob_bits ladder's trial encodes (size only) on the f64-quotient chain as well
-  launch_rans_fast(j, j.ntiles * HOH_NPLANE_S * 8, s, SidMap{HOH_NPLANE_S * 8, KS_VAR}, j.ntiles * HOH_NPLANE_S * 8,
-                   SidMap{0, 0}, 2);
-  launch_rans_fast(j, S, s, SidMap{0, 0}, S, SidMap{0, 0}, 1);        // LZ and predictor-map streams
+  // the MED planes' pb-15 encodes, the prob_bits ladder's trial encodes (size only) and the LZ /
+  // predictor-map streams, all on the f64-quotient chain in one launch
+  launch_rans_fast_s(j, s, j.ntiles * 6, SidMap{3, KS_MED}, j.ntiles * 3, SidMap{3, KS_MED + 3},
+                     j.ntiles * HOH_NPLANE_S * 8, SidMap{HOH_NPLANE_S * 8, KS_VAR}, j.ntiles * HOH_NPLANE_S * 8, S,
+                     SidMap{0, 0}, S);
   launch_rans_gen(j, S, s);
   launch_finalize(j, S, s);
   mark(mc, "rans_enc");
