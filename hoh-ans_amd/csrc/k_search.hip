@@ -138,18 +138,19 @@ __global__ __launch_bounds__(NT) void k_rawmed(EncodeJob j) {
 
 // ---------------------------------------------------------------- predictor search
 
-struct SearchLds {
-  double ent[512];
-  double cost[HOH_MAPCAP * 14];
+struct SearchLds {         // the pick / refine / final phases of k_search
   uint32_t hist[512];
-#ifdef HOH_SEARCH_LDSWALK  // the cell walk's state in LDS (measurement variant of cell_cost_reg)
-  uint16_t top[NT][42];   // rows of 21 / 11 dwords (odd): the lanes' same-column accesses hit
-  uint8_t bp[NT][44];     // distinct banks (40 / 40 gave 4- / 2-way conflicts)
-#endif
   uint8_t brow[2][1024];  // the final pass's best predictors of two rows
   uint16_t plist[HOH_MAPCAP];
   uint8_t pidx[HOH_MAPCAP];
 };
+
+// Search scratch per plane slot pl = t * HOH_NPLANE_S + p, in the tab_gen buffer (written only by
+// k_tables, after the search): the 512 entropy weights ent[] and the cells' mask costs [cell][14].
+#define SCR_STRIDE (512 + HOH_MAPCAP * 14)
+__device__ __forceinline__ double* search_scr(const EncodeJob& j, int pl) {
+  return (double*)j.tab_gen + (size_t)pl * SCR_STRIDE;
+}
 
 // cost of mask m on cell (cx, cy): prediction.hpp:46-151 walked in the cell's raster order with
 // the reference's cell-local top row / best_pred state, sum of ent[] in f64 (layer_encode.hpp:192-195)
@@ -245,62 +246,6 @@ __device__ double cell_cost_one(const uint16_t* D, int w, int h, int depth, int 
   return cost;
 }
 
-// cell_cost with the cell's state in registers: the row above (T, and TR up to the cell's last
-// column, whose TR is this row's first value: top[0] is already overwritten there), this row,
-// and the row above's best predictors as nibbles (bp[]: 4 until written).  Every value of the
-// walk is an original, so the only serial part is the f64 sum, kept in raster order.
-__device__ double cell_cost_reg(const uint16_t* D, int w, int h, int depth, int xt, int yt, int cx, int cy,
-                                uint32_t mask, const double* ent) {
-  const int c = 1 << depth, half = c >> 1;
-  const int tw = (w + xt - 1) / xt, th = (h + yt - 1) / yt;
-  const int x0 = cx * tw, y0 = cy * th;
-  const int vw = min(tw, w - x0);
-  uint32_t up[CELL_MAX], cur[CELL_MAX], bpk[CELL_MAX / 8];
-#pragma unroll
-  for (int i = 0; i < CELL_MAX; i++) up[i] = (i < tw && cy) ? D[(long)y0 * w + x0 + i - w] : (uint32_t)half;
-#pragma unroll
-  for (int i = 0; i < CELL_MAX / 8; i++) bpk[i] = 0x44444444u;
-  double cost = 0.0;
-  for (int ym = 0; ym < th && y0 + ym < h; ym++) {
-    uint32_t L, TL;
-    if (cx) {
-      L = D[(long)(y0 + ym) * w + x0 - 1];
-      TL = (ym || cy) ? D[(long)(y0 + ym - 1) * w + x0 - 1] : (uint32_t)half;
-    } else {
-      L = TL = half;
-    }
-    const uint16_t* row = D + (long)(y0 + ym) * w + x0;
-#pragma unroll
-    for (int i = 0; i < CELL_MAX; i++) cur[i] = i < vw ? row[i] : 0u;
-    // bp[tw - 1] of the row above (the left neighbour's predictor at xm = 0)
-    uint32_t wl = bpk[0];
-#pragma unroll
-    for (int i = 1; i < CELL_MAX / 8; i++) wl = (tw - 1) / 8 == i ? bpk[i] : wl;
-    const uint32_t bl0 = (wl >> (4 * ((tw - 1) & 7))) & 15u;
-    uint32_t bB = bl0;
-#pragma unroll
-    for (int xm = 0; xm < CELL_MAX; xm++) {
-      if (xm < vw) {
-        const uint32_t v = cur[xm], T = up[xm];
-        const uint32_t TR = (xm + 1 == tw || xm + 1 == CELL_MAX) ? cur[0] : up[xm + 1 < CELL_MAX ? xm + 1 : 0];
-        Preds p;
-        preds16(L, T, TL, TR, false, p);
-        const uint32_t bA = (bpk[xm / 8] >> (4 * (xm & 7))) & 15u;
-        const uint32_t pr = midp(pick(p, bA), pick(p, bB));
-        const uint32_t r = ((uint32_t)((int)v - (int)pr + half + c)) & (uint32_t)(c - 1);
-        cost += ent[r];
-        TL = T;
-        up[xm] = v;
-        L = v;
-        const uint32_t nb = best_pred(v, p, mask, c);
-        bpk[xm / 8] = (bpk[xm / 8] & ~(15u << (4 * (xm & 7)))) | (nb << (4 * (xm & 7)));
-        bB = nb;
-      }
-    }
-  }
-  return cost;
-}
-
 // channelpredict_all (prediction.hpp:153-229) at one pixel, fully parallel: the best predictors
 // it needs (row above, left neighbour / end of the row above) are recomputed from the originals
 struct AllCtx {
@@ -337,15 +282,47 @@ __device__ __forceinline__ uint32_t resid_all(const AllCtx& a, int x, int y) {
   return ((uint32_t)((int)a.D[(long)y * a.w + x] - (int)pr + a.half + a.c)) & (uint32_t)(a.c - 1);   // > 0: % c
 }
 
-// one workgroup per (tile, plane)
-__global__ __launch_bounds__(NT) void k_search(EncodeJob j) {
+// The mask costs of every searched plane: a lane per (mask, plane, cell) task, mask-major, so a
+// wave's lanes share a mask (the one-predictor masks kMasks[0..3] walk without the predictor set)
+// and all planes' walks run at once across the chip instead of one workgroup's tasks behind its
+// slowest wave.  The full walk keeps the cell's top row and best predictors in LDS (8 KB per
+// wave: ~120 VGPRs, four waves per SIMD).  ncmax: cells of the largest plane (host, from the tile
+// size).
+__global__ __launch_bounds__(64) void k_search_walk(EncodeJob j, int npred, int ncmax) {
+  __shared__ uint16_t top[64][42];
+  __shared__ uint8_t bp[64][44];
+  const int lane = threadIdx.x;
+  const uint32_t npl = (uint32_t)j.ntiles * HOH_NPLANE_S;
+  const uint64_t g = (uint64_t)blockIdx.x * 64 + lane;
+  const uint32_t m = (uint32_t)(g / ((uint64_t)npl * ncmax));
+  if (m >= (uint32_t)npred) return;
+  const uint32_t rem = (uint32_t)(g % ((uint64_t)npl * ncmax)), pl = rem / ncmax, cell = rem % ncmax;
+  const int t = (int)(pl / HOH_NPLANE_S), p = (int)(pl % HOH_NPLANE_S);
+  const TileInfo ti = j.tiles[t];
+  if (!plane_present(j, ti, p)) return;
+  const int w = ti.w, h = ti.h, depth = plane_depth(p);
+  const int xt = (w + 39) / 40, yt = (h + 39) / 40;
+  if (!(xt > 1 || yt > 1) || (int)cell >= xt * yt) return;
+  const uint16_t* D = j.sym + fin_plane_off(j, t, p);
+  double* ent = search_scr(j, (int)pl);
+  const uint32_t mk = kMasks[m];
+  ent[512 + cell * 14 + m] =
+      m < 4 ? cell_cost_one(D, w, h, depth, xt, yt, (int)cell % xt, (int)cell / xt, (uint32_t)__builtin_ctz(mk), ent)
+            : cell_cost(D, w, h, depth, xt, yt, (int)cell % xt, (int)cell / xt, mk, ent, top[lane], bp[lane]);
+}
+
+// One workgroup per (tile, plane).  phase 0: the plane's data staged, the MED residuals'
+// entropy weights to the scratch; then k_search_walk fills the mask costs; phase 1: the masks
+// picked; pass 0 of -s>=3 then refines the weights and returns for a second walk, otherwise the
+// final residuals and the predictor map follow.
+__global__ __launch_bounds__(NT) void k_search(EncodeJob j, int phase, int pass) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sl_raw[];
   SearchLds& S = *(SearchLds*)sl_raw;
   const int t = blockIdx.x / HOH_NPLANE_S, p = blockIdx.x % HOH_NPLANE_S, tid = threadIdx.x;
   const TileInfo ti = j.tiles[t];
   PlaneInfo* pi = j.pinfo + (size_t)t * HOH_NPLANE_S + p;
   if (!plane_present(j, ti, p)) {
-    if (tid == 0) { PlaneInfo z; memset(&z, 0, sizeof(z)); *pi = z; }
+    if (tid == 0 && phase == 0) { PlaneInfo z; memset(&z, 0, sizeof(z)); *pi = z; }
     return;
   }
   const int w = ti.w, h = ti.h, depth = plane_depth(p), c = 1 << depth, half = c >> 1;
@@ -355,70 +332,57 @@ __global__ __launch_bounds__(NT) void k_search(EncodeJob j) {
   const uint32_t* mh = j.hist + (size_t)(t * j.spt + KS_MED + p) * 512;
   const int xt = (w + 39) / 40, yt = (h + 39) / 40;               // layer_encode.hpp:124-132, :150-151
   const bool grid = xt > 1 || yt > 1;
-  if (!grid) {
-    // no search: the layer keeps the MED residuals (00 00 00 10 header)
-    const uint16_t* M = j.sym + med_plane_off(j, t, p);
-    for (uint32_t q = tid; q < npix; q += NT) D[q] = M[q];
-    for (int i = tid; i < 512; i += NT) fh[i] = mh[i];
-    if (tid == 0) {
-      PlaneInfo z; memset(&z, 0, sizeof(z));
-      z.present = 1; z.depth = depth; z.fixed_len = 5;
-      *pi = z;
-    }
-    return;
-  }
-  // the plane's data values, staged in the searched-residual slot (overwritten at the end)
-  for (uint32_t q = tid; q < npix; q += NT) D[q] = (uint16_t)plane_value(j, ti, t, p, q);
-  // entropy of the MED residuals over all pixels, freq = 1 + count (layer_encode.hpp:133-144)
+  double* ent = search_scr(j, t * HOH_NPLANE_S + p);
+  const double* cost = ent + 512;
   const double* lg = nullptr;
   for (int k = 0; k < 4; k++) if (j.lg_n[k] == npix) lg = j.lg + j.lg_off[k];
-  for (int i = tid; i < c; i += NT) S.ent[i] = lg[1 + mh[i]];
-  __syncthreads();
+  if (phase == 0) {
+    if (!grid) {
+      // no search: the layer keeps the MED residuals (00 00 00 10 header)
+      const uint16_t* M = j.sym + med_plane_off(j, t, p);
+      for (uint32_t q = tid; q < npix; q += NT) D[q] = M[q];
+      for (int i = tid; i < 512; i += NT) fh[i] = mh[i];
+      if (tid == 0) {
+        PlaneInfo z; memset(&z, 0, sizeof(z));
+        z.present = 1; z.depth = depth; z.fixed_len = 5;
+        *pi = z;
+      }
+      return;
+    }
+    // the plane's data values, staged in the searched-residual slot (overwritten at the end)
+    for (uint32_t q = tid; q < npix; q += NT) D[q] = (uint16_t)plane_value(j, ti, t, p, q);
+    // entropy of the MED residuals over all pixels, freq = 1 + count (layer_encode.hpp:133-144)
+    for (int i = tid; i < c; i += NT) ent[i] = lg[1 + mh[i]];
+    return;
+  }
+  if (!grid) return;
   const int ncell = xt * yt, npred = j.speed * 5 < 14 ? j.speed * 5 : 14;
   const int tw = (w + xt - 1) / xt, th = (h + yt - 1) / yt;
   AllCtx a{D, w, h, tw, th, xt, c, half, S.plist};
-  for (int pass = 0; pass < (j.speed > 2 ? 2 : 1); pass++) {
-    if (pass == 1) {
-      // refine (:215-231): entropy of the first channelpredict_all residuals
-      for (int i = tid; i < 512; i += NT) S.hist[i] = 0;
-      __syncthreads();
-      for (uint32_t q = tid; q < npix; q += NT) {
-        const int y = (int)(q / (uint32_t)w), x = (int)(q - (uint32_t)y * w);
-        atomicAdd(&S.hist[resid_all(a, x, y)], 1u);
-      }
-      __syncthreads();
-      for (int i = tid; i < c; i += NT) S.ent[i] = lg[1 + S.hist[i]];
-      __syncthreads();
-    }
-    // mask-major task order: a wave's lanes share one or two masks, so the one-predictor masks
-    // (kMasks[0..3], ~7x fewer instructions per pixel) take whole waves off the full walk
-#ifdef HOH_SEARCH_NOCOST                                              // measurement knob (invalid files)
-    for (int k = tid; k < ncell * npred; k += NT) S.cost[(k % ncell) * 14 + k / ncell] = 0.0;
-    if (0)
-#endif
-    for (int k = tid; k < ncell * npred; k += NT) {
-      const int m = k / ncell, cell = k % ncell;
-      const uint32_t mk = kMasks[m];
-      S.cost[cell * 14 + m] =
-          m < 4 ? cell_cost_one(D, w, h, depth, xt, yt, cell % xt, cell / xt, (uint32_t)__builtin_ctz(mk), S.ent)
-#ifdef HOH_SEARCH_LDSWALK
-                : cell_cost(D, w, h, depth, xt, yt, cell % xt, cell / xt, mk, S.ent, S.top[tid], S.bp[tid]);
-#else
-                : cell_cost_reg(D, w, h, depth, xt, yt, cell % xt, cell / xt, mk, S.ent);
-#endif
-    }
-    __syncthreads();
+  {
     for (int cell = tid; cell < ncell; cell += NT) {
       double best = 99999999999.0;                                // :177
       int bi = 0;
       for (int m = 0; m < npred; m++) {
-        const double v = S.cost[cell * 14 + m];
+        const double v = cost[cell * 14 + m];
         if (v < best) { best = v; bi = m; }
       }
       S.plist[cell] = kMasks[bi];
       S.pidx[cell] = (uint8_t)bi;
     }
     __syncthreads();
+  }
+  if (j.speed > 2 && pass == 0) {
+    // refine (:215-231): entropy of the first channelpredict_all residuals, then a second walk
+    for (int i = tid; i < 512; i += NT) S.hist[i] = 0;
+    __syncthreads();
+    for (uint32_t q = tid; q < npix; q += NT) {
+      const int y = (int)(q / (uint32_t)w), x = (int)(q - (uint32_t)y * w);
+      atomicAdd(&S.hist[resid_all(a, x, y)], 1u);
+    }
+    __syncthreads();
+    for (int i = tid; i < c; i += NT) ent[i] = lg[1 + S.hist[i]];
+    return;
   }
   // final channelpredict_all residuals, in place over the staged data: rows from the last up,
   // each row read completely before it is overwritten (reads reach rows y-2..y only)
@@ -430,9 +394,6 @@ __global__ __launch_bounds__(NT) void k_search(EncodeJob j) {
   for (int i = tid; i < w; i += NT) bnext[i] = 0;
   for (int i = tid; i < 512; i += NT) S.hist[i] = 0;
   __syncthreads();
-#ifdef HOH_SEARCH_NOFINAL                                             // measurement knob (invalid files)
-  if (0)
-#endif
   for (int y = h - 1; y >= 0; y--) {
     if (y > 0)
       for (int x = tid; x < w; x += NT) bcur[x] = (uint8_t)bp_all(a, x, y - 1);
@@ -1332,7 +1293,17 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, void (*mark)(void*, const
   int ring = 1;
   while (ring < limit + NT) ring <<= 1;
   if (j.speed >= 3) hipLaunchKernelGGL(k_rawmed, dim3(j.ntiles), dim3(NT), 0, s, j);
-  hipLaunchKernelGGL(k_search, dim3(j.ntiles * HOH_NPLANE_S), dim3(NT), sizeof(SearchLds), s, j);
+  {
+    const int npred = j.speed * 5 < 14 ? j.speed * 5 : 14;
+    const int ncmax = ((j.tw + 39) / 40) * ((j.th + 39) / 40);
+    const uint64_t ntask = (uint64_t)npred * j.ntiles * HOH_NPLANE_S * ncmax;
+    const dim3 gs(j.ntiles * HOH_NPLANE_S), gw((unsigned)((ntask + 63) / 64));
+    hipLaunchKernelGGL(k_search, gs, dim3(NT), sizeof(SearchLds), s, j, 0, 0);
+    for (int pass = 0; pass < (j.speed > 2 ? 2 : 1); pass++) {
+      hipLaunchKernelGGL(k_search_walk, gw, dim3(64), 0, s, j, npred, ncmax);
+      hipLaunchKernelGGL(k_search, gs, dim3(NT), sizeof(SearchLds), s, j, 1, pass);
+    }
+  }
   mark(mc, "search");
   hipLaunchKernelGGL(k_lzfp, dim3(16, j.ntiles), dim3(NT), 0, s, j);
   hipLaunchKernelGGL(k_lzcand, dim3(j.ntiles), dim3(NT), (size_t)(ring + 3 * LZC_W + 2 * LZC_C) * 4, s, j, limit, ring);

@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round-3 (second session) bench evidence (outputs in gpurun_out/r03b/): the driver-shaped bench line (20 steps, 5
+# warmup: live PMC traffic, CPU baselines, no-index and natural legs), the 200-step line, the
+# N > 1 code path on a 1-rank RCCL group, config 4 (--strong), rocprofv3 kernel stats with one
+# image in flight and with 20, and the natural-image kernel stats at -s0 / -s1.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; O=gpurun_out/r03b; mkdir -p $O; export TMPDIR=/tmp
+timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > $O/bench_driver_shape.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+cat $O/bench_driver_shape.json
+timeout -k 10 300 python -u bench.py --steps 200 --no-cpu-baseline --no-pmc --no-config2 --no-legs > $O/bench_200.json 2> $O/bench200.err || { tail -20 $O/bench200.err; exit 1; }
+timeout -k 10 200 python -u bench.py --sharded --steps 40 --no-cpu-baseline --no-pmc --no-legs --no-config2 > $O/bench_sharded.json 2> $O/bench_sharded.err || { tail -20 $O/bench_sharded.err; exit 1; }
+timeout -k 10 200 python -u bench.py --strong --steps 20 --inflight 8 --no-cpu-baseline --no-pmc --no-legs --no-config2 > $O/bench_strong.json 2> $O/bench_strong.err || { tail -20 $O/bench_strong.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof1 -o run -- python3 bench.py --inflight 1 --steps 20 --warmup 2 --no-cpu-baseline --no-pmc --no-config2 --no-legs > $O/prof1_bench.json 2> $O/prof1.err || { tail -20 $O/prof1.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof20 -o run -- python3 bench.py --steps 200 --no-cpu-baseline --no-pmc --no-config2 --no-legs > $O/prof20_bench.json 2> $O/prof20.err || { tail -20 $O/prof20.err; exit 1; }
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/nat0 -o run -- python3 $GRAFT_REPO_ROOT/tools/scripts/natural_prof.py 8192 0 3 > $GRAFT_REPO_ROOT/$O/nat0.txt 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/nat1 -o run -- python3 $GRAFT_REPO_ROOT/tools/scripts/natural_prof.py 8192 1 2 > $GRAFT_REPO_ROOT/$O/nat1.txt 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/noix -o run -- python3 $GRAFT_REPO_ROOT/tools/scripts/noix_bench.py synth 8192 3 > $GRAFT_REPO_ROOT/$O/noix.txt 2>&1 || exit 1
+find $GRAFT_REPO_ROOT/$O -name "*stats*"
+cd $GRAFT_REPO_ROOT
+timeout -k 10 200 python3 tools/scripts/natural_prof.py 8192 3 1 > $O/nat3.txt 2>&1 || exit 1
+timeout -k 10 200 python3 tools/scripts/natural_prof.py 8192 4 1 > $O/nat4.txt 2>&1 || exit 1
+cat $O/nat3.txt $O/nat4.txt
