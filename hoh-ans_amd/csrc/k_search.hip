@@ -141,6 +141,7 @@ __global__ __launch_bounds__(NT) void k_rawmed(EncodeJob j) {
 struct SearchLds {         // the pick / refine / final phases of k_search
   uint32_t hist[512];
   uint8_t brow[2][1024];  // the final pass's best predictors of two rows
+  uint16_t rows[4][1024]; // the final pass's original rows y - 2..y and row y - 3 arriving
   uint16_t plist[HOH_MAPCAP];
   uint8_t pidx[HOH_MAPCAP];
 };
@@ -252,17 +253,22 @@ struct AllCtx {
   const uint16_t* D;
   int w, h, tw, th, xt, c, half;
   const uint16_t* plist;
+  const uint16_t* ring;   // k_search's final pass (use_ring): rows y - 2..y staged in LDS, row y at (y & 3) << 10
+  bool use_ring;
+  __device__ __forceinline__ uint32_t px(int y, int x) const {
+    return use_ring ? ring[((y & 3) << 10) + x] : D[(long)y * w + x];
+  }
 };
 
 __device__ __forceinline__ void preds_all_at(const AllCtx& a, int x, int y, Preds& p) {
   const int w = a.w;
-  const uint32_t L = x ? a.D[(long)y * w + x - 1] : (uint32_t)a.half;
-  const uint32_t T = y ? a.D[(long)(y - 1) * w + x] : (uint32_t)a.half;
-  const uint32_t TL = (x && y) ? a.D[(long)(y - 1) * w + x - 1] : (uint32_t)a.half;
+  const uint32_t L = x ? a.px(y, x - 1) : (uint32_t)a.half;
+  const uint32_t T = y ? a.px(y - 1, x) : (uint32_t)a.half;
+  const uint32_t TL = (x && y) ? a.px(y - 1, x - 1) : (uint32_t)a.half;
   uint32_t TR;
   if (w == 1) TR = T;                                        // top_row[0] not yet overwritten
-  else if (x == w - 1) TR = a.D[(long)y * w];                // top_row[0]: this row's first value
-  else TR = y ? a.D[(long)(y - 1) * w + x + 1] : (uint32_t)a.half;
+  else if (x == w - 1) TR = a.px(y, 0);                // top_row[0]: this row's first value
+  else TR = y ? a.px(y - 1, x + 1) : (uint32_t)a.half;
   preds16(L, T, TL, TR, true, p);
 }
 
@@ -270,7 +276,7 @@ __device__ __forceinline__ uint32_t bp_all(const AllCtx& a, int x, int y) {
   if (y + 1 >= a.h) return 0;                                // last row keeps 0 (:214-216)
   Preds p;
   preds_all_at(a, x, y, p);
-  return best_pred(a.D[(long)y * a.w + x], p, a.plist[((y + 1) / a.th) * a.xt + x / a.tw], a.c);
+  return best_pred(a.px(y, x), p, a.plist[((y + 1) / a.th) * a.xt + x / a.tw], a.c);
 }
 
 __device__ __forceinline__ uint32_t resid_all(const AllCtx& a, int x, int y) {
@@ -279,7 +285,7 @@ __device__ __forceinline__ uint32_t resid_all(const AllCtx& a, int x, int y) {
   Preds p;
   preds_all_at(a, x, y, p);
   const uint32_t pr = midp(pick(p, bA), pick(p, bB));
-  return ((uint32_t)((int)a.D[(long)y * a.w + x] - (int)pr + a.half + a.c)) & (uint32_t)(a.c - 1);   // > 0: % c
+  return ((uint32_t)((int)a.px(y, x) - (int)pr + a.half + a.c)) & (uint32_t)(a.c - 1);   // > 0: % c
 }
 
 // The mask costs of every searched plane: a lane per (mask, plane, cell) task, mask-major, so a
@@ -358,7 +364,7 @@ __global__ __launch_bounds__(NT) void k_search(EncodeJob j, int phase, int pass)
   if (!grid) return;
   const int ncell = xt * yt, npred = j.speed * 5 < 14 ? j.speed * 5 : 14;
   const int tw = (w + xt - 1) / xt, th = (h + yt - 1) / yt;
-  AllCtx a{D, w, h, tw, th, xt, c, half, S.plist};
+  AllCtx a{D, w, h, tw, th, xt, c, half, S.plist, D, false};
   {
     for (int cell = tid; cell < ncell; cell += NT) {
       double best = 99999999999.0;                                // :177
@@ -393,26 +399,36 @@ __global__ __launch_bounds__(NT) void k_search(EncodeJob j, int phase, int pass)
   uint8_t* bcur = S.brow[1];
   for (int i = tid; i < w; i += NT) bnext[i] = 0;
   for (int i = tid; i < 512; i += NT) S.hist[i] = 0;
+  // the original rows in an LDS ring (the global plane is overwritten row by row): rows y, y - 1
+  // and y - 2 are read at row y, row y - 3 is loaded meanwhile and lands in row y + 1's slot
+  for (int k = 0; k < 3 && h - 1 - k >= 0; k++)
+    for (int x = tid; x < w; x += NT) S.rows[(h - 1 - k) & 3][x] = D[(long)(h - 1 - k) * w + x];
+  a.ring = &S.rows[0][0];
+  a.use_ring = true;
   __syncthreads();
   for (int y = h - 1; y >= 0; y--) {
+    uint32_t nv[4];
+    int n = 0;
+    for (int x = tid; x < w && n < 4; x += NT) nv[n++] = y >= 3 ? D[(long)(y - 3) * w + x] : 0u;
     if (y > 0)
       for (int x = tid; x < w; x += NT) bcur[x] = (uint8_t)bp_all(a, x, y - 1);
     __syncthreads();
     uint32_t rv[4];
-    int n = 0;
+    n = 0;
     for (int x = tid; x < w && n < 4; x += NT) {                      // resid_all(a, x, y)
       const uint32_t bA = y ? bcur[x] : 4u;
       const uint32_t bB = x ? bnext[x - 1] : (y ? bcur[w - 1] : 4u);
       Preds p;
       preds_all_at(a, x, y, p);
       const uint32_t pr = midp(pick(p, bA), pick(p, bB));
-      rv[n++] = ((uint32_t)((int)D[(long)y * w + x] - (int)pr + half + c)) & (uint32_t)(c - 1);
+      rv[n++] = ((uint32_t)((int)a.px(y, x) - (int)pr + half + c)) & (uint32_t)(c - 1);
     }
     __syncthreads();
     n = 0;
     for (int x = tid; x < w && n < 4; x += NT) {
       D[(long)y * w + x] = (uint16_t)rv[n];
       atomicAdd(&S.hist[rv[n]], 1u);
+      if (y >= 3) S.rows[(y - 3) & 3][x] = (uint16_t)nv[n];
       n++;
     }
     __syncthreads();
@@ -480,7 +496,7 @@ __global__ void k_section_one(const uint16_t* D, int w, int h, int depth, int xt
 __global__ __launch_bounds__(NT) void k_all_plane(const uint16_t* D, int w, int h, int depth, int xt, int yt,
                                                   const uint16_t* map, uint16_t* out) {
   const int c = 1 << depth;
-  const AllCtx a{D, w, h, (w + xt - 1) / xt, (h + yt - 1) / yt, xt, c, c >> 1, map};
+  const AllCtx a{D, w, h, (w + xt - 1) / xt, (h + yt - 1) / yt, xt, c, c >> 1, map, D, false};
   const uint64_t n = (uint64_t)w * h;
   for (uint64_t q = (uint64_t)blockIdx.x * NT + threadIdx.x; q < n; q += (uint64_t)gridDim.x * NT) {
     const int y = (int)(q / (uint64_t)w), x = (int)(q - (uint64_t)y * w);
