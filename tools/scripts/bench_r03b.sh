@@ -5,6 +5,9 @@
 # image in flight and with 20, and the natural-image kernel stats at -s0 / -s1.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; O=gpurun_out/r03b; mkdir -p $O; export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gputests.log 2>&1 || { tail -30 $O/gputests.log; exit 1; }
+tail -2 $O/gputests.log
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
 timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > $O/bench_driver_shape.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 cat $O/bench_driver_shape.json
 timeout -k 10 300 python -u bench.py --steps 200 --no-cpu-baseline --no-pmc --no-config2 --no-legs > $O/bench_200.json 2> $O/bench200.err || { tail -20 $O/bench200.err; exit 1; }
