@@ -631,12 +631,13 @@ __global__ __launch_bounds__(NT) void k_lzfp(EncodeJob j) {
 //    a first position equal to q is an exact no for the chunk, an earlier one holding f a yes.
 // Only a lane whose every slot is held by other fingerprints is walked: the wave walks each such
 // lane's window together.  40 KB of LDS at -s1 (ring 8 KB, tables 24 + 8 KB): four tiles per CU.
+// -s2..-s4 (windows of 2048..16384 fill the tables) run without them (use_tab = 0).
 #define LZC_W 2048
 #define LZC_C 1024
 __device__ __forceinline__ uint32_t lzc_h(uint32_t f, int k) {
   return k == 0 ? (f >> 1) & (LZC_W - 1) : k == 1 ? (f >> 12) & (LZC_W - 1) : (f * 0x9E3779B1u) >> 21;
 }
-__global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring) {
+__global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring, int use_tab) {
   extern __shared__ uint32_t fr[];
   uint32_t* ht = fr + ring;                                            // window tables
   uint32_t* ct = ht + 3 * LZC_W;                                       // chunk tables
@@ -645,8 +646,10 @@ __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring)
   const uint32_t npix = (uint32_t)ti.w * ti.h, w = ti.w;
   const uint32_t* F = j.fpb + (size_t)t * j.npix_cap;
   uint64_t* cand = j.candbits + (size_t)t * (j.npix_cap / 64);
-  for (uint32_t e = tid; e < 3 * LZC_W; e += NT) ht[e] = 0u;
-  for (uint32_t e = tid; e < 2 * LZC_C; e += NT) ct[e] = 0xffffffffu;
+  if (use_tab) {
+    for (uint32_t e = tid; e < 3 * LZC_W; e += NT) ht[e] = 0u;
+    for (uint32_t e = tid; e < 2 * LZC_C; e += NT) ct[e] = 0xffffffffu;
+  }
   __syncthreads();
   uint32_t ncand = 0;
   for (uint32_t base = 0; base < npix; base += NT) {
@@ -656,14 +659,14 @@ __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring)
     const uint32_t hs0 = lzc_h(f, 0), hs1 = LZC_W + lzc_h(f, 1), hs2 = 2 * LZC_W + lzc_h(f, 2);
     const uint32_t cs0 = (f >> 1) & (LZC_C - 1), cs1 = LZC_C + ((f >> 12) & (LZC_C - 1));
     fr[q & (ring - 1)] = f;
-    if (f) {
+    if (f && use_tab) {
       atomicMin(&ct[cs0], tid);
       atomicMin(&ct[cs1], tid);
     }
     __syncthreads();
-    bool c = false, walk = false;
+    bool c = false, walk = f && !use_tab;
     const uint32_t bm = q < (uint32_t)limit ? q : (uint32_t)limit;
-    if (f) {
+    if (f && use_tab) {
       // earlier in the chunk
       const uint32_t m0 = ct[cs0], m1 = ct[cs1];
       const bool first = m0 == (uint32_t)tid || m1 == (uint32_t)tid;
@@ -686,8 +689,20 @@ __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring)
       }
     }
     // the uncertain lanes, one at a time by the whole wave: 64 window entries per LDS read
-    // (consecutive addresses), a ballot per read, out at the first equal fingerprint
-    for (uint64_t um = __ballot(walk && !c); um; um &= um - 1) {
+    // (consecutive addresses), a ballot per read, out at the first equal fingerprint.  With more
+    // than 8 of them (the long windows of -s3/-s4 fill the tables) every lane walks its own
+    // window instead, eight entries per LDS round trip.
+    const uint64_t um0 = __ballot(walk && !c);
+    if (__popcll(um0) > 8) {
+      for (uint32_t b0 = 1; walk && b0 <= bm && !c; b0 += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = fr[(q - b0 - u) & (ring - 1)];
+#pragma unroll
+        for (int u = 0; u < 8; u++) c |= b0 + u <= bm && v[u] == f;
+      }
+    } else
+    for (uint64_t um = um0; um; um &= um - 1) {
       const int l = __ffsll((unsigned long long)um) - 1;
       const uint32_t fl = __shfl(f, l), ql = __shfl(q, l), bl = __shfl(bm, l);
       bool hit = false;
@@ -716,7 +731,7 @@ __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring)
     if (lane == 0 && q < npix) cand[q >> 6] = word;
     ncand += lane == 0 ? (uint32_t)__popcll(word) : 0u;
     __syncthreads();                                                   // every check has read the tables
-    if (f) {
+    if (f && use_tab) {
       ct[cs0] = 0xffffffffu;
       ct[cs1] = 0xffffffffu;
       const uint32_t e = ((q + 1) << 8) | tag;
@@ -1322,7 +1337,11 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, void (*mark)(void*, const
   }
   mark(mc, "search");
   hipLaunchKernelGGL(k_lzfp, dim3(16, j.ntiles), dim3(NT), 0, s, j);
-  hipLaunchKernelGGL(k_lzcand, dim3(j.ntiles), dim3(NT), (size_t)(ring + 3 * LZC_W + 2 * LZC_C) * 4, s, j, limit, ring);
+  // the hash tables pay at -s1's window (1024); the longer windows of -s2..-s4 fill them, so
+  // there every lane walks its window and the LDS holds the ring alone (more tiles per CU)
+  const int use_tab = limit <= 1024;
+  hipLaunchKernelGGL(k_lzcand, dim3(j.ntiles), dim3(NT), (size_t)(ring + (use_tab ? 3 * LZC_W + 2 * LZC_C : 0)) * 4, s,
+                     j, limit, ring, use_tab);
   int rp = 1;
   while (rp < limit + 324) rp <<= 1;
   if (rp > 8192) rp = 0;                                              // -s4: pixels from the image
