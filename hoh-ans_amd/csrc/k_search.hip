@@ -631,25 +631,42 @@ __global__ __launch_bounds__(NT) void k_lzfp(EncodeJob j) {
 //    a first position equal to q is an exact no for the chunk, an earlier one holding f a yes.
 // Only a lane whose every slot is held by other fingerprints is walked: the wave walks each such
 // lane's window together.  40 KB of LDS at -s1 (ring 8 KB, tables 24 + 8 KB): four tiles per CU.
-// -s2..-s4 (windows of 2048..16384 fill the tables) run without them (use_tab = 0).
+// -s2..-s4 (windows of 2048..16384 fill the tables) take the global map below.
 #define LZC_W 2048
 #define LZC_C 1024
 __device__ __forceinline__ uint32_t lzc_h(uint32_t f, int k) {
   return k == 0 ? (f >> 1) & (LZC_W - 1) : k == 1 ? (f >> 12) & (LZC_W - 1) : (f * 0x9E3779B1u) >> 21;
 }
-__global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring, int use_tab) {
+// Modes: LZC_WALK every lane walks its window (ring >= limit + NT); LZC_TAB the LDS window tables
+// above (-s1); LZC_MAP (-s2..-s4, whose windows fill any LDS table) a per-tile open-addressing
+// map in global memory of every fingerprint seen so far -> its latest position, (p + 1) << 8 |
+// tag, linear probing from (f >> 1), at most half full, in the tab_gen buffer (k_tables writes
+// it later).  Fingerprints whose slot chain and tag coincide share an entry holding the larger
+// position, so "latest position older than q - bm" stays an exact no and only candidates are
+// added.  One workgroup owns a tile's map: workgroup-scope atomic loads / CAS / max, ordered
+// between chunks by the barrier; the chunk's own positions come from the chunk tables (a walk of
+// at most the chunk if they are unsure).
+enum { LZC_WALK = 0, LZC_TAB = 1, LZC_MAP = 2 };
+__device__ __forceinline__ uint32_t* lzc_map(const EncodeJob& j, int t) {
+  return (uint32_t*)((char*)j.tab_gen + (size_t)t * SPT_S * 512 * sizeof(EncGen));
+}
+__global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring, int mode, uint32_t mw) {
   extern __shared__ uint32_t fr[];
-  uint32_t* ht = fr + ring;                                            // window tables
-  uint32_t* ct = ht + 3 * LZC_W;                                       // chunk tables
+  uint32_t* ht = fr + ring;                                            // window tables (LZC_TAB)
+  uint32_t* ct = ht + (mode == LZC_TAB ? 3 * LZC_W : 0);               // chunk tables (TAB, MAP)
   const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const TileInfo ti = j.tiles[t];
   const uint32_t npix = (uint32_t)ti.w * ti.h, w = ti.w;
   const uint32_t* F = j.fpb + (size_t)t * j.npix_cap;
   uint64_t* cand = j.candbits + (size_t)t * (j.npix_cap / 64);
-  if (use_tab) {
+  uint32_t* mp = lzc_map(j, t);
+  const bool use_tab = mode != LZC_WALK;
+  if (mode == LZC_TAB)
     for (uint32_t e = tid; e < 3 * LZC_W; e += NT) ht[e] = 0u;
+  if (use_tab)
     for (uint32_t e = tid; e < 2 * LZC_C; e += NT) ct[e] = 0xffffffffu;
-  }
+  if (mode == LZC_MAP)
+    for (uint32_t e = tid; e < mw; e += NT) mp[e] = 0u;
   __syncthreads();
   uint32_t ncand = 0;
   for (uint32_t base = 0; base < npix; base += NT) {
@@ -673,7 +690,17 @@ __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring,
       c = (m0 < (uint32_t)tid && fr[(base + m0) & (ring - 1)] == f) ||
           (m1 < (uint32_t)tid && fr[(base + m1) & (ring - 1)] == f);
       walk = !first && !c;
-      if (!c) {
+      if (!c && mode == LZC_MAP) {
+        // the latest earlier position of f (or of a fingerprint sharing its entry)
+        for (uint32_t h = (f >> 1) & (mw - 1);; h = (h + 1) & (mw - 1)) {
+          const uint32_t v = __hip_atomic_load(mp + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (v == 0) break;
+          if ((v & 0xffu) == tag) {
+            c = q - ((v >> 8) - 1) <= bm;
+            break;
+          }
+        }
+      } else if (!c) {
         // in the window before the chunk
         bool none = false, yes = false;
         const uint32_t hw[3] = {ht[hs0], ht[hs1], ht[hs2]};
@@ -692,19 +719,20 @@ __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring,
     // (consecutive addresses), a ballot per read, out at the first equal fingerprint.  With more
     // than 8 of them (the long windows of -s3/-s4 fill the tables) every lane walks its own
     // window instead, eight entries per LDS round trip.
+    const uint32_t wb = mode == LZC_MAP ? min(bm, q - base) : bm;      // MAP: the chunk only
     const uint64_t um0 = __ballot(walk && !c);
     if (__popcll(um0) > 8) {
-      for (uint32_t b0 = 1; walk && b0 <= bm && !c; b0 += 8) {
+      for (uint32_t b0 = 1; walk && b0 <= wb && !c; b0 += 8) {
         uint32_t v[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) v[u] = fr[(q - b0 - u) & (ring - 1)];
 #pragma unroll
-        for (int u = 0; u < 8; u++) c |= b0 + u <= bm && v[u] == f;
+        for (int u = 0; u < 8; u++) c |= b0 + u <= wb && v[u] == f;
       }
     } else
     for (uint64_t um = um0; um; um &= um - 1) {
       const int l = __ffsll((unsigned long long)um) - 1;
-      const uint32_t fl = __shfl(f, l), ql = __shfl(q, l), bl = __shfl(bm, l);
+      const uint32_t fl = __shfl(f, l), ql = __shfl(q, l), bl = __shfl(wb, l);
       bool hit = false;
       for (uint32_t b0 = 1; b0 <= bl && !hit; b0 += 64) {
         const uint32_t b = b0 + lane;
@@ -735,9 +763,26 @@ __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring,
       ct[cs0] = 0xffffffffu;
       ct[cs1] = 0xffffffffu;
       const uint32_t e = ((q + 1) << 8) | tag;
-      atomicMax(&ht[hs0], e);
-      atomicMax(&ht[hs1], e);
-      atomicMax(&ht[hs2], e);
+      if (mode == LZC_TAB) {
+        atomicMax(&ht[hs0], e);
+        atomicMax(&ht[hs1], e);
+        atomicMax(&ht[hs2], e);
+      } else {
+        for (uint32_t h = (f >> 1) & (mw - 1);; h = (h + 1) & (mw - 1)) {
+          uint32_t v = __hip_atomic_load(mp + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (v == 0) {
+            uint32_t z = 0;
+            if (__hip_atomic_compare_exchange_strong(mp + h, &z, e, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP))
+              break;
+            v = z;                                                     // the winner's entry
+          }
+          if ((v & 0xffu) == tag) {
+            __hip_atomic_fetch_max(mp + h, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            break;
+          }
+        }
+      }
     }
     __syncthreads();
   }
@@ -1339,9 +1384,13 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, void (*mark)(void*, const
   hipLaunchKernelGGL(k_lzfp, dim3(16, j.ntiles), dim3(NT), 0, s, j);
   // the hash tables pay at -s1's window (1024); the longer windows of -s2..-s4 fill them, so
   // there every lane walks its window and the LDS holds the ring alone (more tiles per CU)
-  const int use_tab = limit <= 1024;
-  hipLaunchKernelGGL(k_lzcand, dim3(j.ntiles), dim3(NT), (size_t)(ring + (use_tab ? 3 * LZC_W + 2 * LZC_C : 0)) * 4, s,
-                     j, limit, ring, use_tab);
+  // -s2..-s4: the global map when a tile's (half-full) map fits its share of tab_gen
+  uint32_t mw = 1;
+  while (mw < 2u * (uint32_t)j.npix_cap) mw <<= 1;
+  const int mode = limit <= 1024 ? LZC_TAB : (size_t)mw * 4 <= (size_t)SPT_S * 512 * sizeof(EncGen) ? LZC_MAP : LZC_WALK;
+  const int lring = mode == LZC_MAP ? 2 * NT : ring;
+  const size_t lds = (size_t)(lring + (mode == LZC_TAB ? 3 * LZC_W : 0) + (mode != LZC_WALK ? 2 * LZC_C : 0)) * 4;
+  hipLaunchKernelGGL(k_lzcand, dim3(j.ntiles), dim3(NT), lds, s, j, limit, lring, mode, mw);
   int rp = 1;
   while (rp < limit + 324) rp <<= 1;
   if (rp > 8192) rp = 0;                                              // -s4: pixels from the image
