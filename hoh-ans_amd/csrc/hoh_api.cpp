@@ -62,6 +62,7 @@ struct hoh_ctx {
   int cus = 256;                // compute units of the device
   Scratch scr;
   hipStream_t own = nullptr;
+  SideStream side;              // -s>=1: the LZ screen beside the predictor search (created on first use)
   Buf idx8, fpb, pinfo, lg;     // -s>=1 workspaces
   uint32_t lg_key[4] = {0, 0, 0, 0};
   uint64_t lg_off[4] = {0, 0, 0, 0};
@@ -174,6 +175,9 @@ void hoh_ctx_destroy(hoh_ctx* c) {
   for (auto e : c->kev) (void)hipEventDestroy(e);
   if (c->pinned) (void)hipHostFree(c->pinned);
   if (c->own) (void)hipStreamDestroy(c->own);
+  if (c->side.s) (void)hipStreamDestroy(c->side.s);
+  if (c->side.fork) (void)hipEventDestroy(c->side.fork);
+  if (c->side.join) (void)hipEventDestroy(c->side.join);
   delete c;
 }
 
@@ -420,7 +424,13 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   launch_front(j, s);            prof.mark("front");
   launch_palette(j, s);          prof.mark("palette");
   if (speed) {
-    encode_speed_s(j, s, prof_cb, &prof);
+    if (!c->side.s) {
+      if (hipStreamCreateWithFlags(&c->side.s, hipStreamNonBlocking) != hipSuccess ||
+          hipEventCreateWithFlags(&c->side.fork, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&c->side.join, hipEventDisableTiming) != hipSuccess)
+        return HOH_E_HIP;
+    }
+    encode_speed_s(j, s, c->side, prof_cb, &prof);
     if (hipGetLastError() != hipSuccess) return HOH_E_HIP;
     idx = nullptr;
   } else {

@@ -263,7 +263,11 @@ void launch_rans_fast01(const EncodeJob& j, hipStream_t s, int np0, SidMap a0, i
 void launch_rans_gen(const EncodeJob& j, int nstreams, hipStream_t s, SidMap m = SidMap{0, 0});
 void launch_finalize(const EncodeJob& j, int nstreams, hipStream_t s, SidMap m = SidMap{0, 0});
 void launch_nuke(const EncodeJob& j, hipStream_t s);
-void encode_speed_s(const EncodeJob& j, hipStream_t s, void (*mark)(void*, const char*), void* mctx);
+struct SideStream {        // a context's second stream for work that forks off the main one
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, void (*mark)(void*, const char*), void* mctx);
 void launch_layout(const EncodeJob& j, hipStream_t s);
 void launch_assemble(const EncodeJob& j, int nstreams, hipStream_t s);
 void launch_streambytes(const EncodeJob& j, int nstreams, hipStream_t s);

@@ -148,9 +148,14 @@ struct SearchLds {         // the pick / refine / final phases of k_search
 
 // Search scratch per plane slot pl = t * HOH_NPLANE_S + p, in the tab_gen buffer (written only by
 // k_tables, after the search): the 512 entropy weights ent[] and the cells' mask costs [cell][14].
+// Per tile the region of its SPT_S streams' tables (860 KB); the scratch of its planes first,
+// then (from LZC_MAP_OFF) k_lzcand's map, so the LZ screen can run beside the search.
 #define SCR_STRIDE (512 + HOH_MAPCAP * 14)
+#define TAB_TILE_BYTES ((size_t)SPT_S * 512 * sizeof(EncGen))
+#define LZC_MAP_OFF ((size_t)143360)   // >= HOH_NPLANE_S * SCR_STRIDE * 8, 512-aligned
+static_assert(HOH_NPLANE_S * SCR_STRIDE * 8 <= LZC_MAP_OFF, "search scratch below the LZ map");
 __device__ __forceinline__ double* search_scr(const EncodeJob& j, int pl) {
-  return (double*)j.tab_gen + (size_t)pl * SCR_STRIDE;
+  return (double*)((char*)j.tab_gen + (size_t)(pl / HOH_NPLANE_S) * TAB_TILE_BYTES) + (size_t)(pl % HOH_NPLANE_S) * SCR_STRIDE;
 }
 
 // cost of mask m on cell (cx, cy): prediction.hpp:46-151 walked in the cell's raster order with
@@ -648,7 +653,7 @@ __device__ __forceinline__ uint32_t lzc_h(uint32_t f, int k) {
 // at most the chunk if they are unsure).
 enum { LZC_WALK = 0, LZC_TAB = 1, LZC_MAP = 2 };
 __device__ __forceinline__ uint32_t* lzc_map(const EncodeJob& j, int t) {
-  return (uint32_t*)((char*)j.tab_gen + (size_t)t * SPT_S * 512 * sizeof(EncGen));
+  return (uint32_t*)((char*)j.tab_gen + (size_t)t * TAB_TILE_BYTES + LZC_MAP_OFF);
 }
 __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring, int mode, uint32_t mw) {
   extern __shared__ uint32_t fr[];
@@ -1363,11 +1368,40 @@ __global__ __launch_bounds__(64) void k_tilebytes_s(EncodeJob j) {
 
 // ---------------------------------------------------------------- orchestration
 
-void encode_speed_s(const EncodeJob& j, hipStream_t s, void (*mark)(void*, const char*), void* mc) {
+void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, void (*mark)(void*, const char*), void* mc) {
   const int dist = j.speed == 1 ? 10 : j.speed == 2 ? 11 : j.speed == 3 ? 12 : 14;   // choh.cpp:125-137
   const int limit = 1 << dist;
   int ring = 1;
   while (ring < limit + NT) ring <<= 1;
+  // The LZ screen and scan (k_lzfp, k_lzcand, k_lzscan: RGB -> fingerprints -> matches) share
+  // nothing with the predictor search (RGB -> planes, residuals, histograms), so they run on the
+  // context's side stream beside it; k_nuke (which compacts the searched planes) joins the two.
+  // The search scratch and the LZ map lie in disjoint parts of each tile's tab_gen region.
+  hipStream_t sl = side.s ? side.s : s;
+  if (side.s) {
+    (void)hipEventRecord(side.fork, s);
+    (void)hipStreamWaitEvent(sl, side.fork, 0);
+  }
+  {
+    hipLaunchKernelGGL(k_lzfp, dim3(16, j.ntiles), dim3(NT), 0, sl, j);
+    // the hash tables pay at -s1's window (1024); the longer windows of -s2..-s4 fill them and
+    // take the global map when a tile's (half-full) map fits its share of tab_gen
+    uint32_t mw = 1;
+    while (mw < 2u * (uint32_t)j.npix_cap) mw <<= 1;
+    const int mode = limit <= 1024 ? LZC_TAB : (size_t)mw * 4 + LZC_MAP_OFF <= TAB_TILE_BYTES ? LZC_MAP : LZC_WALK;
+    const int lring = mode == LZC_MAP ? 2 * NT : ring;
+    const size_t lds = (size_t)(lring + (mode == LZC_TAB ? 3 * LZC_W : 0) + (mode != LZC_WALK ? 2 * LZC_C : 0)) * 4;
+    hipLaunchKernelGGL(k_lzcand, dim3(j.ntiles), dim3(NT), lds, sl, j, limit, lring, mode, mw);
+    int rp = 1;
+    while (rp < limit + 324) rp <<= 1;
+    if (rp > 8192) rp = 0;                                            // -s4: pixels from the image
+    // -s1 (ring 2048): four segment walks per tile (four rings: two workgroups per CU); the larger
+    // rings of -s2..-s4 keep one walk per tile
+    const int nseg = rp && rp <= 2048 ? LZS_SEG : 1;
+    hipLaunchKernelGGL(k_lzscan, dim3(j.ntiles), dim3(64 * LZS_SEG), (size_t)nseg * (rp ? rp + 16 : 1) * 4, sl, j, limit,
+                       rp, nseg);
+  }
+  if (side.s) (void)hipEventRecord(side.join, sl);
   if (j.speed >= 3) hipLaunchKernelGGL(k_rawmed, dim3(j.ntiles), dim3(NT), 0, s, j);
   {
     const int npred = j.speed * 5 < 14 ? j.speed * 5 : 14;
@@ -1381,24 +1415,7 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, void (*mark)(void*, const
     }
   }
   mark(mc, "search");
-  hipLaunchKernelGGL(k_lzfp, dim3(16, j.ntiles), dim3(NT), 0, s, j);
-  // the hash tables pay at -s1's window (1024); the longer windows of -s2..-s4 fill them, so
-  // there every lane walks its window and the LDS holds the ring alone (more tiles per CU)
-  // -s2..-s4: the global map when a tile's (half-full) map fits its share of tab_gen
-  uint32_t mw = 1;
-  while (mw < 2u * (uint32_t)j.npix_cap) mw <<= 1;
-  const int mode = limit <= 1024 ? LZC_TAB : (size_t)mw * 4 <= (size_t)SPT_S * 512 * sizeof(EncGen) ? LZC_MAP : LZC_WALK;
-  const int lring = mode == LZC_MAP ? 2 * NT : ring;
-  const size_t lds = (size_t)(lring + (mode == LZC_TAB ? 3 * LZC_W : 0) + (mode != LZC_WALK ? 2 * LZC_C : 0)) * 4;
-  hipLaunchKernelGGL(k_lzcand, dim3(j.ntiles), dim3(NT), lds, s, j, limit, lring, mode, mw);
-  int rp = 1;
-  while (rp < limit + 324) rp <<= 1;
-  if (rp > 8192) rp = 0;                                              // -s4: pixels from the image
-  // -s1 (ring 2048): four segment walks per tile (four rings: two workgroups per CU); the larger
-  // rings of -s2..-s4 keep one walk per tile
-  const int nseg = rp && rp <= 2048 ? LZS_SEG : 1;
-  hipLaunchKernelGGL(k_lzscan, dim3(j.ntiles), dim3(64 * LZS_SEG), (size_t)nseg * (rp ? rp + 16 : 1) * 4, s, j, limit, rp,
-                     nseg);
+  if (side.s) (void)hipStreamWaitEvent(s, side.join, 0);
   launch_nuke(j, s);
   mark(mc, "lz");
   hipLaunchKernelGGL(k_setup_s, dim3(j.ntiles), dim3(128), 0, s, j);
