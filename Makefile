@@ -5,6 +5,10 @@ ARCH ?= gfx950
 CSRC := hoh-ans_amd/csrc
 LIBDIR := hoh-ans_amd/lib
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-result
+# make DEBUG_READ=1: export hoh_debug_read (tools/scripts/*_dbg.py); never in the product build
+ifeq ($(DEBUG_READ),1)
+HIPFLAGS += -DHOH_DEBUG_READ
+endif
 SRCS := $(wildcard $(CSRC)/*.hip) $(wildcard $(CSRC)/*.cpp)
 OBJS := $(patsubst $(CSRC)/%,build/%.o,$(SRCS))
 HDRS := $(wildcard $(CSRC)/*.h) include/hoh_ans.h

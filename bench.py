@@ -42,7 +42,8 @@ when rocprofv3 is unavailable or the bench itself runs under a profiler.
 
 cpu_baseline (rank 0, N = 1): the reference compiled from its own sources (oracle/_ref):
 ref_bench = encode_tile(-s0) + decode_entropy/unpredict_all per tile on the same image, one
-process per host core over disjoint tile ranges (value; cores stated) and one thread on 512
+process per CPU of the box's quota (cgroup / worker-pool share, not nproc) over disjoint tile
+ranges (value; cores and their source stated, nproc beside) and one thread on 512
 tiles (single_thread), plus the reference's own choh binary (-s0, one thread, whole image;
 its file's sha256 is compared with the golden).
 """
@@ -91,12 +92,40 @@ def golden_sha(W, H, seed, noise):
 
 
 def host_cores():
-    """every CPU of this process's affinity mask (the host cores the reference may use)"""
+    """every CPU of this process's affinity mask"""
     try:
         n = len(os.sched_getaffinity(0))
     except Exception:
         n = os.cpu_count() or 1
     return max(1, n)
+
+
+def cpu_quota():
+    """(CPUs this process may actually use, where that number came from): the cgroup CPU quota
+    (v2 cpu.max, v1 cfs_quota_us / cfs_period_us) when one is set, else the box's worker-pool
+    setting (OMP_NUM_THREADS), else the affinity mask -- whichever is smallest.  A GPU box shows
+    hundreds of CPUs in its affinity mask but grants a share of ~16-20."""
+    aff = host_cores()
+    cands = [(aff, "affinity mask")]
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            cands.append((max(1, int(int(q) / int(per))), "cgroup v2 cpu.max %s/%s" % (q, per)))
+    except Exception:
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                cands.append((max(1, q // per), "cgroup v1 cfs_quota_us %d/%d" % (q, per)))
+        except Exception:
+            pass
+    try:
+        omp = int(os.environ.get("OMP_NUM_THREADS", "0"))
+        if omp > 0:
+            cands.append((omp, "OMP_NUM_THREADS=%d (the box's worker-pool share)" % omp))
+    except ValueError:
+        pass
+    return min(cands)
 
 
 # ------------------------------------------------------------------------------ PMC traffic
@@ -176,16 +205,19 @@ def cpu_baseline(rgb_host, W, H, args):
     if not os.path.exists(exe):
         return {"value": None, "error": "oracle/_ref/ref_bench not built (make -C oracle/ref)"}
     affinity = host_cores()
+    quota, quota_src = cpu_quota()
+    if args.cpu_procs > 0:
+        quota, quota_src = args.cpu_procs, "--cpu-procs"
     xt, yt = W // 256, H // 256
     ntiles = xt * yt
-    P = min(affinity, ntiles)
+    P = min(quota, ntiles)
     res = {}
     with tempfile.NamedTemporaryFile(suffix=".rgb", dir="/tmp", delete=False) as f:
         f.write(rgb_host.tobytes())
         path = f.name
     try:
-        # all cores: one process per CPU of the affinity mask, disjoint contiguous tile ranges
-        # covering the whole image; each process clocks only encode_tile and the decode calls
+        # all cores: one process per CPU of the quota, disjoint contiguous tile ranges covering
+        # the whole image; each process clocks only encode_tile and the decode calls
         # (ref_bench.cpp), and the image's time is the slowest process's
         per = -(-ntiles // P)
         t = time.perf_counter()
@@ -198,10 +230,12 @@ def cpu_baseline(rgb_host, W, H, args):
         bad = sum(d["mismatch_excl_last_row"] for d in ds)
         work = max(d["t_enc"] + d["t_dec"] for d in ds)
         res.update({"value": round(raw / work / 1e6, 3), "unit": "MB/s", "cores": len(procs), "kind": "reference",
-                    "nproc": os.cpu_count(), "affinity_cpus": affinity,
-                    "sample": "whole bench image (%d tiles), one ref_bench process per CPU of the affinity mask on "
-                              "disjoint tile ranges (%d tiles each); value = raw bytes / the slowest process's "
-                              "encode_tile -s0 + decode_entropy/unpredict_all time" % (ntiles, per),
+                    "cores_source": quota_src, "nproc": os.cpu_count(), "affinity_cpus": affinity,
+                    "sample": "whole bench image (%d tiles), one ref_bench process per CPU of the quota (%d) on "
+                              "disjoint tile ranges (%d tiles each); value = raw bytes of the tiles whose encode and "
+                              "decode were both timed / the slowest process's encode_tile -s0 + "
+                              "decode_entropy/unpredict_all time" % (ntiles, len(procs), per),
+                    "tiles_skipped": sum(d.get("tiles_skipped", 0) for d in ds),
                     "wall_clock_MBps": round(raw / wall / 1e6, 3),
                     "wall_clock_note": "process start, band read and the LZ locate of ref_bench included",
                     "ref_decode_mismatch_excl_last_row": bad})
@@ -215,7 +249,7 @@ def cpu_baseline(rgb_host, W, H, args):
                                 "sample": "first %d of %d tiles" % (nt1, ntiles),
                                 "enc_MBps": d["enc_MBps"], "dec_MBps": d["dec_MBps"]}
         res["all_cores_vs_single_x_cores"] = round(res["value"] / (st * len(procs)), 3)
-        res["effective_cores"] = round(res["value"] / st, 1)   # < cores: the host's CPU share is capped
+        res["effective_cores"] = round(res["value"] / st, 1)
         # the reference's own choh binary, -s0, one thread, whole image (dhoh cannot run: SURVEY Q1)
         choh = os.path.join(ROOT, "oracle", "_ref", "choh")
         if os.path.exists(choh) and not args.no_choh_binary:
@@ -374,6 +408,150 @@ def extra_legs(args, slots, W, H, D, status, torch, hoh_ans, hd):
 
 # ------------------------------------------------------------------------------ bench
 
+class GpuShardOps:
+    """Device side of hoh_ans.dist.run_sharded_leg for bench.py's N > 1 path: rank `rank` owns the
+    tile-row band of a W x H image; a step encodes the band (hoh_encode_tiles_async: tile sizes and
+    status stay on the device), copies the tile sizes to pinned host memory behind an event, and
+    when the step finishes all-gathers the sizes, sends the blob to rank 0 (straight into its
+    place in the file behind hoh_file_prefix) and decodes the band (hoh_decode_tiles_async, tile
+    sizes read on the device) on the slot's stream."""
+
+    def __init__(self, args, W, H, seed0, rank, world, dev, torch, hoh_ans, hd, nrows):
+        self.args, self.W, self.H, self.seed0 = args, W, H, seed0
+        self.torch, self.hoh_ans, self.hd, self.dev = torch, hoh_ans, hd, dev
+        self.device = dev
+        self.t0, self.nt, self.y0, y1 = hd.shard(W, H, rank, world)
+        self.rows = y1 - self.y0
+        self.L = hoh_ans.lib()
+        self.status = torch.zeros((nrows, 4), dtype=torch.int64, device=dev)
+
+    def new_slot(self, k):
+        torch, hoh_ans = self.torch, self.hoh_ans
+
+        class Slot:
+            pass
+        s = Slot()
+        s.seed = self.seed0 + k
+        s.ctx = hoh_ans.Context(self.dev.index)
+        s.stream = torch.cuda.Stream(device=self.dev)
+        s.rgb = hoh_ans.synth_rgb_dev(self.W, self.rows, s.seed, self.args.noise, ctx=s.ctx, row0=self.y0)
+        s.index = None if self.args.no_index else hoh_ans.Index()
+        s.out = torch.empty(self.L.hoh_encode_bound(self.W, self.rows), dtype=torch.uint8, device=self.dev)
+        s.dec = torch.empty(self.W * self.rows * 3, dtype=torch.uint8, device=self.dev)
+        s.events = []
+        s.sizes = torch.empty(self.nt, dtype=torch.int32, device=self.dev)
+        s.sizes_host = torch.empty(self.nt, dtype=torch.int32).pin_memory()
+        s.enc_done = torch.cuda.Event()
+        s.gather = self.hd.FileGather(self.W, self.H, self.dev)
+        s.ctx.profiling(True)
+        return s
+
+    def enqueue(self, s, i):
+        torch = self.torch
+        with torch.cuda.stream(s.stream):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            self.hoh_ans.encode_tiles_async(s.rgb, self.W, self.H, self.t0, self.nt, s.out, s.sizes,
+                                            self.status[i, 0:2], ctx=s.ctx, index=s.index, row0=self.y0)
+            e1.record()
+            s.sizes_host.copy_(s.sizes, non_blocking=True)
+            s.enc_done.record()
+            s.events.append((e0, e1))
+
+    def finish(self, s, i):
+        import numpy as np
+        torch = self.torch
+        s.enc_done.synchronize()
+        ts = s.sizes_host.numpy().astype(np.uint32)
+        with torch.cuda.stream(s.stream):
+            res = s.gather(s.out, int(ts.sum(dtype=np.int64)), ts, wait=False)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self.hoh_ans.decode_tiles_async(s.out, s.out.numel(), self.W, self.H, self.t0, self.nt, s.sizes, s.dec,
+                                            self.status[i, 2:4], ctx=s.ctx, index=s.index, row0=self.y0)
+            e2 = torch.cuda.Event(enable_timing=True)
+            e2.record()
+            s.events[-1] = s.events[-1] + (e1, e2)
+            for q in res[2]:
+                q.wait()              # RCCL: the slot's stream (not the host) waits before reusing the blob
+
+    def drain(self):
+        self.torch.cuda.synchronize()
+
+    def check(self, total):
+        st = self.status[:total].cpu().numpy()
+        for i in range(total):
+            self.hoh_ans.check_status(st[i, 0:2], "encode (step %d)" % i)
+            self.hoh_ans.check_status(st[i, 2:4], "decode (step %d)" % i)
+
+    def reset(self, slots):
+        for s in slots:
+            s.ctx.reset_stats()
+            s.events = []
+
+    def lossless(self, s):
+        return bool(self.torch.equal(s.dec, s.rgb))
+
+
+def sharded_leg(args, W, H, D, K, warm, seed0, rank, world, dev, torch, hoh_ans, hd):
+    """One N > 1 leg (or its one-rank rehearsal, --sharded): returns a dict of its numbers; on
+    rank 0 the gathered file of slot 0 (seed seed0) is hashed."""
+    import numpy as np
+    import torch.distributed as dist
+    ops = GpuShardOps(args, W, H, seed0, rank, world, dev, torch, hoh_ans, hd, max(K, warm, D))
+    slots, el, lossless = hd.run_sharded_leg(ops, D, K, warm)
+    t_enc = sum(ev[0].elapsed_time(ev[1]) for s in slots for ev in s.events) * 1e-3
+    t_dec = sum(ev[-2].elapsed_time(ev[-1]) for s in slots for ev in s.events) * 1e-3
+    stats = {}
+    for s in slots:
+        for k, (tot, cnt) in s.ctx.kernel_stats().items():
+            a0, c0 = stats.get(k, (0.0, 0))
+            stats[k] = (a0 + tot, c0 + cnt)
+        s.ctx.profiling(False)
+    tt = torch.tensor([t_enc, t_dec], dtype=torch.float64, device=dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    t_enc, t_dec = tt.tolist()
+    n_rank = int(slots[0].sizes_host.numpy().astype(np.int64).sum())
+    nn = torch.tensor([n_rank], dtype=torch.int64, device=dev)
+    dist.all_reduce(nn)
+    sha = None
+    if rank == 0:      # slot 0's file of its last step: header + tile table + every rank's blob
+        g = slots[0].gather
+        sha = hashlib.sha256(g.file[:g.total].cpu().numpy().tobytes()).hexdigest()
+    res = {"el": el, "K": K, "D": D, "lossless": lossless, "t_enc": t_enc, "t_dec": t_dec,
+           "comp_total": int(nn.item()), "sha": sha, "stats": stats, "rows": ops.rows,
+           "value": W * H * 3 * K / el / 1e6}
+    del slots, ops
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return res
+
+
+def golden_speed_sha(W, H, seed, noise, speed=0):
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "golden_speed.json")) as f:
+            for r in json.load(f)["files"]:
+                sp = r["spec"]
+                if (sp["W"], sp["H"], sp["seed"], sp["noise"], sp["speed"]) == (W, H, seed, noise, speed):
+                    return r["out"]["sha256"]
+    except Exception:
+        pass
+    return None
+
+
+def golden_bench_shas(W, H, noise):
+    """{seed: sha256} of the reference choh -s0 file of every bench seed (golden_bench.json)"""
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "golden_bench.json")) as f:
+            return {r["spec"]["seed"]: r["out"]["sha256"] for r in json.load(f)["files"]
+                    if (r["spec"]["W"], r["spec"]["H"], r["spec"]["noise"], r["spec"]["speed"]) == (W, H, noise, 0)}
+    except Exception:
+        return {}
+
+
+STRONG_SIDE, STRONG_SEED = 16384, 2     # configs[3]; seed 2 is the reference choh's golden file
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -386,21 +564,26 @@ def main():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--noise", type=int, default=4)
     ap.add_argument("--inflight", type=int, default=20, help="images in flight per GPU (1 = one at a time)")
+    ap.add_argument("--strong-inflight", type=int, default=8, help="images in flight per GPU in the 16384^2 leg")
     ap.add_argument("--no-index", action="store_true", help="decode without the side index (serial rANS)")
     ap.add_argument("--cpu-tiles", type=int, default=512)
+    ap.add_argument("--cpu-procs", type=int, default=0,
+                    help="reference processes of the all-cores CPU baseline (default: the cgroup CPU quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-choh-binary", action="store_true")
     ap.add_argument("--no-config2", action="store_true", help="skip the 1M-symbol single-stream leg")
     ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 --pmc traffic passes")
     ap.add_argument("--sharded", action="store_true",
                     help="N = 1: run the N > 1 code path (tile encode, RCCL gather on a 1-rank group, tile decode)")
+    ap.add_argument("--no-strong-leg", action="store_true",
+                    help="N > 1 / --sharded: skip the configs[3] leg (16384^2 sharded over the ranks)")
     ap.add_argument("--no-legs", action="store_true",
                     help="skip the detail legs (no-index pipeline, natural-statistic pipeline)")
     ap.add_argument("--leg-steps", type=int, default=40, help="timed steps of each detail leg")
     ap.add_argument("--pmc-probe", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.size <= 0:
-        args.size = 16384 if args.strong else 8192
+        args.size = STRONG_SIDE if args.strong else 8192
     if args.pmc_probe:
         pmc_probe(args)
         return
@@ -410,10 +593,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
+    sharded = world > 1 or args.sharded
 
     # live PMC traffic first, before this process initialises the GPU
     pmc, pmc_note = None, "skipped"
-    if world == 1 and not args.no_pmc:
+    if world == 1 and not args.no_pmc and not sharded:
         if under_profiler():
             pmc_note = "skipped: the bench itself runs under a profiler"
         else:
@@ -427,57 +611,161 @@ def main():
     if q < D:
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, D))
 
-    import numpy as np
     import torch
-    import torch.distributed as dist
     import hoh_ans
     from hoh_ans import dist as hd
 
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    sharded = world > 1 or args.sharded
     if sharded:
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        if world == 1:
-            import socket
-            so = socket.socket()
-            so.bind(("127.0.0.1", 0))
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            os.environ.setdefault("MASTER_PORT", str(so.getsockname()[1]))
-            so.close()
-            os.environ.setdefault("RANK", "0")
-        dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
-
-    L = hoh_ans.lib()
-    W = args.size
-    H = args.size if (args.strong or world == 1) else args.size * world
-    if not sharded:
-        t0, nt, y0, y1 = 0, (W // 256) * (H // 256), 0, H
+        sharded_main(args, D, world, rank, dev, torch, hoh_ans, hd)
     else:
-        t0, nt, y0, y1 = hd.shard(W, H, rank, world)
-    rows = y1 - y0
+        single_main(args, D, dev, torch, hoh_ans, hd, pmc, pmc_note)
+
+
+def roofline_obj(kms, kavg, ratio, rows_raw, raw_total, K, el, pmc):
+    """SURVEY 8(d)'s encode-side algorithmic bytes charged to one launch of the dominant kernel
+    (one launch = one image's or shard's encode): 3 B/px read + 3r B/px written = (1 + r) raw; the
+    design's own bytes (u16 residuals in + payload out) beside it as design_bytes."""
+    alg = int(round((1 + ratio) * rows_raw))
+    design = 2 * rows_raw + int(round(ratio * rows_raw))
+    achieved = alg / (kms * 1e-3) / 1e9 if kms else None
+    pipeline_gbs = 2 * (1 + ratio) * raw_total * K / el / 1e9
+    traffic = pmc.get(DOM, {}).get("hbm_bytes") if pmc else None
+    return {"bound": "hbm", "kernel": "k_rans_fast01 (" + DOM + ")",
+            "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
+            "traffic": traffic, "algorithmic_bytes": alg,
+            "algorithmic_bytes_note": "(1 + r) x raw bytes per launch (SURVEY 8(d) encode side)",
+            "design_bytes": design,
+            "design_achieved": round(design / (kms * 1e-3) / 1e9, 2) if kms else None,
+            "limiter": "latency of the serial rans64 coder chain (65,536 dependent steps per tile plane), "
+                       "not HBM: traffic ~ design bytes (u16 residuals in + payload out)",
+            "avg_launch_ms": round(kms, 4) if kms else None,
+            "avg_launch_ms_source": "HIP events on the encoder's stream, one image in flight, 5 launches",
+            "avg_launch_ms_under_load": round(kavg[DOM], 4) if DOM in kavg else None,
+            "pipeline_achieved": round(pipeline_gbs, 2), "pipeline_frac": round(pipeline_gbs / HBM_PEAK_GBS, 5),
+            "pipeline_bytes_per_image": round(2 * (1 + ratio) * raw_total)}
+
+
+def sharded_main(args, D, world, rank, dev, torch, hoh_ans, hd):
+    """N > 1 (one process per GPU, RCCL), or --sharded at N = 1 (the same code on a one-rank
+    group).  The line's value is the primary leg: weak scaling 8192 x (8192 N) by default (each
+    GPU always holds an 8192^2 band), or configs[3] with --strong.  Unless --strong or
+    --no-strong-leg, the same launch also runs configs[3] -- one 16384^2 image (seed 2, the
+    reference choh's golden file) sharded over the N ranks -- into detail.strong_16384_*, with
+    rank 0's gathered file hashed against tests/golden/golden_speed.json."""
+    import torch.distributed as dist
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if world == 1:
+        import socket
+        so = socket.socket()
+        so.bind(("127.0.0.1", 0))
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(so.getsockname()[1]))
+        so.close()
+        os.environ.setdefault("RANK", "0")
+    dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
+    W = args.size
+    H = args.size if args.strong else args.size * world
+    K, warm = args.steps, args.warmup
+    seed0 = STRONG_SEED if (args.strong and W == STRONG_SIDE) else args.seed
+    p = sharded_leg(args, W, H, D, K, warm, seed0, rank, world, dev, torch, hoh_ans, hd)
+    strong = None
+    if not args.strong and not args.no_strong_leg and STRONG_SIDE // 256 >= world:
+        Ds = max(1, min(args.strong_inflight, D))
+        strong = sharded_leg(args, STRONG_SIDE, STRONG_SIDE, Ds, max(1, args.leg_steps), Ds, STRONG_SEED, rank, world,
+                             dev, torch, hoh_ans, hd)
+    if rank == 0:
+        raw_total = W * H * 3
+        ratio = p["comp_total"] / raw_total
+        kavg = {k: v[0] / v[1] for k, v in p["stats"].items() if v[1]}
+        roof = roofline_obj(None, kavg, ratio, W * p["rows"] * 3, raw_total, K, p["el"], None)
+        roof["avg_launch_ms_source"] = "not measured at N > 1 (one image in flight is an N = 1 leg)"
+        gw = golden_speed_sha(W, H, seed0, args.noise) if args.strong else None
+        if gw is None:
+            gw = golden_sha(W, H, seed0, args.noise)
+        detail = {
+            "inflight": D,
+            "warmup_requested": args.warmup,
+            "latency_ms_enc": round(p["t_enc"] / K * 1e3, 3),
+            "latency_ms_dec": round(p["t_dec"] / K * 1e3, 3),
+            "compressed_bytes": p["comp_total"],
+            "ratio": round(ratio, 5),
+            "lossless": p["lossless"],
+            "file_sha256": p["sha"],
+            "bit_exact_vs_reference": (p["sha"] == gw) if gw else None,
+            "setup_steps": D,
+            "kernel_avg_ms_under_load": {k: round(v, 4) for k, v in kavg.items()},
+        }
+        if strong is not None:
+            g = golden_speed_sha(STRONG_SIDE, STRONG_SIDE, STRONG_SEED, args.noise)
+            detail.update({
+                "strong_16384_MBps": round(strong["value"], 1),
+                "strong_16384_ms_per_step": round(strong["el"] / strong["K"] * 1e3, 4),
+                "strong_16384_steps": strong["K"],
+                "strong_16384_inflight": strong["D"],
+                "strong_16384_lossless": strong["lossless"],
+                "strong_16384_file_sha256": strong["sha"],
+                "strong_16384_bit_exact_vs_reference": (strong["sha"] == g) if g else None,
+                "strong_16384_note": "BASELINE configs[3]: one 16384x16384 image (seed %d) sharded over the %d rank(s) "
+                                     "(strong scaling), RCCL gather of the sub-bitstreams to rank 0; sha256 of rank 0's "
+                                     "gathered file against the reference choh's (golden_speed.json)"
+                                     % (STRONG_SEED, world),
+            })
+        res = {
+            "metric": metric_name(),
+            "value": round(p["value"], 2),
+            "unit": "MB/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": warm,
+            "ms_per_step": round(p["el"] / K * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong" if args.strong else "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {
+                "workload": ("%dx%d synthetic RGB (gradient + triangular noise k=%d, seeds %d..%d: one image per "
+                             "slot), 256x256 tiles, choh -s0 encode + dhoh decode, %s, %d image(s) in flight per GPU"
+                             % (W, H, args.noise, seed0, seed0 + D - 1,
+                                "side index" if not args.no_index else "serial decode", D)),
+                "W": W, "H": H, "tiles": (W // 256) * (H // 256), "per_gpu": "%dx%d" % (W, p["rows"]),
+                "parallelism": "tile rows sharded over %d GPU(s), RCCL gather to rank 0" % world,
+            },
+            "roofline": roof,
+            "detail": detail,
+        }
+        print(json.dumps(res), flush=True)
+    ok = p["lossless"] and (strong is None or strong["lossless"])
+    dist.destroy_process_group()
+    if not ok:
+        sys.exit(3)
+
+
+def single_main(args, D, dev, torch, hoh_ans, hd, pmc, pmc_note):
+    """N = 1: D whole-image slots, enqueue-only encode + decode, no host round trip per step."""
+    L = hoh_ans.lib()
+    W = H = args.size
+    rows = H
     K = args.steps
     warm = args.warmup
     status = torch.zeros((max(K, warm, D), 4), dtype=torch.int64, device=dev)
 
     class Slot:
         """One in-flight image: its own input (seed args.seed + k), library context (HIP stream +
-        workspaces), side index, output buffers and (N > 1) file gather."""
+        workspaces), side index and output buffers."""
 
         def __init__(self, k):
             self.seed = args.seed + k
-            self.ctx = hoh_ans.Context(local)
+            self.ctx = hoh_ans.Context(dev.index)
             self.stream = torch.cuda.Stream(device=dev)
-            self.rgb = hoh_ans.synth_rgb_dev(W, rows, self.seed, args.noise, ctx=self.ctx, row0=y0)
+            self.rgb = hoh_ans.synth_rgb_dev(W, rows, self.seed, args.noise, ctx=self.ctx)
             self.index = None if args.no_index else hoh_ans.Index()
             self.out = torch.empty(L.hoh_encode_bound(W, rows), dtype=torch.uint8, device=dev)
             self.dec = torch.empty(W * rows * 3, dtype=torch.uint8, device=dev)
             self.events = []
-            if sharded:
-                self.sizes = torch.empty(nt, dtype=torch.int32, device=dev)
-                self.sizes_host = torch.empty(nt, dtype=torch.int32).pin_memory()
-                self.enc_done = torch.cuda.Event()
-                self.gather = hd.FileGather(W, H, dev)
 
     slots = [Slot(k) for k in range(D)]
     torch.cuda.synchronize()
@@ -487,41 +775,15 @@ def main():
         with torch.cuda.stream(s.stream):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            if not sharded:
-                hoh_ans.encode_image_async(s.rgb, W, H, s.out, status[i, 0:2], ctx=s.ctx, index=s.index)
-                e1.record()
-                hoh_ans.decode_image_async(s.out, s.out.numel(), W, H, s.dec, status[i, 2:4], ctx=s.ctx, index=s.index)
-                e2 = torch.cuda.Event(enable_timing=True)
-                e2.record()
-                s.events.append((e0, e1, e2))
-            else:
-                hoh_ans.encode_tiles_async(s.rgb, W, H, t0, nt, s.out, s.sizes, status[i, 0:2], ctx=s.ctx,
-                                           index=s.index, row0=y0)
-                e1.record()
-                s.sizes_host.copy_(s.sizes, non_blocking=True)
-                s.enc_done.record()
-                s.events.append((e0, e1))
-
-    def finish(k, i):
-        if not sharded:
-            return
-        s = slots[k]
-        s.enc_done.synchronize()
-        ts = s.sizes_host.numpy().astype(np.uint32)
-        with torch.cuda.stream(s.stream):
-            res = s.gather(s.out, int(ts.sum(dtype=np.int64)), ts, wait=False)
-            e1 = torch.cuda.Event(enable_timing=True)
+            hoh_ans.encode_image_async(s.rgb, W, H, s.out, status[i, 0:2], ctx=s.ctx, index=s.index)
             e1.record()
-            hoh_ans.decode_tiles_async(s.out, s.out.numel(), W, H, t0, nt, s.sizes, s.dec, status[i, 2:4], ctx=s.ctx,
-                                       index=s.index, row0=y0)
+            hoh_ans.decode_image_async(s.out, s.out.numel(), W, H, s.dec, status[i, 2:4], ctx=s.ctx, index=s.index)
             e2 = torch.cuda.Event(enable_timing=True)
             e2.record()
-            s.events[-1] = s.events[-1] + (e1, e2)
-            for q in res[2]:
-                q.wait()              # RCCL: the slot's stream (not the host) waits before reusing the blob
+            s.events.append((e0, e1, e2))
 
     def run(total):
-        hd.run_pipeline(D, total, enqueue, finish)
+        hd.run_pipeline(D, total, enqueue, lambda k, i: None)
 
     def check_status(total):
         st = status[:total].cpu().numpy()
@@ -544,14 +806,10 @@ def main():
     for s in slots:
         s.ctx.reset_stats()
         s.events = []
-    if sharded:
-        dist.barrier()
     torch.cuda.synchronize()
     t = time.perf_counter()
     run(K)
     torch.cuda.synchronize()
-    if sharded:
-        dist.barrier()
     el = time.perf_counter() - t
     check_status(K)
     stats = {}
@@ -567,153 +825,127 @@ def main():
             t_dec += ev[-2].elapsed_time(ev[-1]) * 1e-3
 
     # per-kernel durations and the per-image rate with ONE image in flight (host-synchronous
-    # calls), and the no-index (serial rANS) decode of slot 0's file -- N = 1 only
-    iso, single_ms, noix_ms, noix_ok, n0 = {}, None, None, None, None
+    # calls), and the no-index (serial rANS) decode of slot 0's file
     s0 = slots[0]
-    if not sharded:
-        with torch.cuda.stream(s0.stream):
-            s0.ctx.profiling(True)
-            s0.ctx.reset_stats()
+    noix_ms, noix_ok = None, None
+    with torch.cuda.stream(s0.stream):
+        s0.ctx.profiling(True)
+        s0.ctx.reset_stats()
+        times = []
+        for _ in range(5):
+            torch.cuda.synchronize()
+            ta = time.perf_counter()
+            _, n0, _ = hoh_ans.encode_image(s0.rgb, W, H, out_dev=s0.out, ctx=s0.ctx, index=s0.index)
+            hoh_ans.decode_image(s0.out, n0, out_dev=s0.dec, ctx=s0.ctx, index=s0.index)
+            s0.stream.synchronize()
+            times.append(time.perf_counter() - ta)
+        iso = {k: v[0] / v[1] for k, v in s0.ctx.kernel_stats().items() if v[1]}
+        s0.ctx.profiling(False)
+        single_ms = sorted(times)[len(times) // 2] * 1e3
+        if not args.no_index:
+            noix = torch.empty_like(s0.dec)
             times = []
-            for _ in range(5):
-                torch.cuda.synchronize()
+            for _ in range(3):
+                s0.stream.synchronize()
                 ta = time.perf_counter()
-                _, n0, _ = hoh_ans.encode_image(s0.rgb, W, H, out_dev=s0.out, ctx=s0.ctx, index=s0.index)
-                hoh_ans.decode_image(s0.out, n0, out_dev=s0.dec, ctx=s0.ctx, index=s0.index)
+                hoh_ans.decode_image(s0.out, n0, out_dev=noix, ctx=s0.ctx, index=None)
                 s0.stream.synchronize()
                 times.append(time.perf_counter() - ta)
-            iso = {k: v[0] / v[1] for k, v in s0.ctx.kernel_stats().items() if v[1]}
-            s0.ctx.profiling(False)
-            single_ms = sorted(times)[len(times) // 2] * 1e3
-            if not args.no_index:
-                noix = torch.empty_like(s0.dec)
-                times = []
-                for _ in range(3):
-                    s0.stream.synchronize()
-                    ta = time.perf_counter()
-                    hoh_ans.decode_image(s0.out, n0, out_dev=noix, ctx=s0.ctx, index=None)
-                    s0.stream.synchronize()
-                    times.append(time.perf_counter() - ta)
-                noix_ms = min(times) * 1e3
-                noix_ok = bool(torch.equal(noix, s0.rgb))
-                del noix
+            noix_ms = min(times) * 1e3
+            noix_ok = bool(torch.equal(noix, s0.rgb))
+            del noix
 
-    # checks outside the timed region
+    # checks outside the timed region: every slot lossless, and EVERY slot's file (its last
+    # timed step's) against the reference choh's sha256 for that slot's seed
+    # (tests/golden/golden_bench.json, made by tests/golden/make_golden_bench.py)
     lossless = all(bool(torch.equal(s.dec, s.rgb)) for s in slots)
-    sha = None
-    if not sharded:
-        n0 = n0 if n0 is not None else int(status[K - 1, 1].item())
-        sha = hashlib.sha256(s0.out[:n0].cpu().numpy().tobytes()).hexdigest()
-        comp_total = n0
-    else:
-        n_rank = int(slots[0].sizes_host.numpy().astype(np.int64).sum())
-        tt = torch.tensor([el, 0.0 if lossless else 1.0, t_enc, t_dec], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el, bad, t_enc, t_dec = tt.tolist()
-        lossless = bad == 0.0
-        nn = torch.tensor([n_rank], dtype=torch.int64, device=dev)
-        dist.all_reduce(nn)
-        comp_total = int(nn.item())          # slot 0's image (seed args.seed), all shards
+    sha = hashlib.sha256(s0.out[:n0].cpu().numpy().tobytes()).hexdigest()
+    gb = golden_bench_shas(W, H, args.noise)
+    st = status[:K].cpu().numpy()
+    slot_match, slot_checked, slot_nogolden = 0, 0, []
+    for k, s in enumerate(slots):
+        if k == 0:
+            n_k = n0                      # slot 0 was re-encoded by the one-in-flight leg (same image)
+        elif k < K:
+            n_k = int(st[k + ((K - 1 - k) // D) * D, 1])
+        else:
+            continue
+        want = gb.get(s.seed)
+        if want is None:
+            slot_nogolden.append(s.seed)
+            continue
+        slot_checked += 1
+        slot_match += hashlib.sha256(s.out[:n_k].cpu().numpy().tobytes()).hexdigest() == want
+    comp_total = n0
     raw_total = W * H * 3
     value = raw_total * K / el / 1e6
     legs = {}
-    if not sharded and not args.no_legs:      # after the checks: the legs reuse the slots' buffers
+    if not args.no_legs:      # after the checks: the legs reuse the slots' buffers
         legs = extra_legs(args, slots, W, H, D, status, torch, hoh_ans, hd)
 
-    if rank == 0:
-        kavg = {k: v[0] / v[1] for k, v in stats.items() if v[1]}
-        rows_raw = W * rows * 3
-        ratio = comp_total / raw_total
-        # SURVEY 8(d)'s encode-side algorithmic bytes charged to the launch (one launch = one shard's
-        # encode): 3 B/px read + 3r B/px written = (1 + r) raw; the design's own bytes (u16 residuals
-        # in + payload out) are reported beside it as design_bytes
-        alg = int(round((1 + ratio) * rows_raw))
-        design = 2 * rows_raw + int(round(ratio * rows_raw))
-        kms = iso.get(DOM) or None
-        achieved = alg / (kms * 1e-3) / 1e9 if kms else None
-        pipeline_gbs = 2 * (1 + ratio) * raw_total * K / el / 1e9
-        traffic = pmc.get(DOM, {}).get("hbm_bytes") if pmc else None
-        roof = {"bound": "hbm", "kernel": "k_rans_fast01 (" + DOM + ")",
-                "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
-                "traffic": traffic, "algorithmic_bytes": alg,
-                "algorithmic_bytes_note": "(1 + r) x raw bytes per launch (SURVEY 8(d) encode side)",
-                "design_bytes": design,
-                "design_achieved": round(design / (kms * 1e-3) / 1e9, 2) if kms else None,
-                "limiter": "latency of the serial rans64 coder chain (65,536 dependent steps per tile plane), "
-                           "not HBM: traffic ~ design bytes (u16 residuals in + payload out)",
-                "avg_launch_ms": round(kms, 4) if kms else None,
-                "avg_launch_ms_source": "HIP events on the encoder's stream, one image in flight, 5 launches",
-                "avg_launch_ms_under_load": round(kavg[DOM], 4) if DOM in kavg else None,
-                "pipeline_achieved": round(pipeline_gbs, 2), "pipeline_frac": round(pipeline_gbs / HBM_PEAK_GBS, 5),
-                "pipeline_bytes_per_image": round(2 * (1 + ratio) * raw_total)}
-        golden = golden_sha(W, H, args.seed, args.noise) if not sharded else None
-        if sharded and world == 1:
-            # 1-rank group: the gathered file is the whole image's .hoh
-            f, nf = slots[0].gather.file, None
-            ts = slots[0].sizes_host.numpy().astype(np.uint32)
-            nf = len(hoh_ans.file_prefix(W, H, ts)) + int(ts.sum(dtype=np.int64))
-            sha = hashlib.sha256(f[:nf].cpu().numpy().tobytes()).hexdigest()
-            golden = golden_sha(W, H, args.seed, args.noise)
-        res = {
-            "metric": metric_name(),
-            "value": round(value, 2),
-            "unit": "MB/s",
-            "n_gpus": world,
-            "steps": K,
-            "warmup": warm,
-            "ms_per_step": round(el / K * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "strong" if args.strong else "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic",
-            "config": {
-                "workload": ("%dx%d synthetic RGB (gradient + triangular noise k=%d, seeds %d..%d: one image per "
-                             "slot), 256x256 tiles, choh -s0 encode + dhoh decode, %s, %d image(s) in flight per GPU"
-                             % (W, H, args.noise, args.seed, args.seed + D - 1,
-                                "side index" if not args.no_index else "serial decode", D)),
-                "W": W, "H": H, "tiles": (W // 256) * (H // 256), "per_gpu": "%dx%d" % (W, rows),
-                "parallelism": ("tile rows sharded over %d GPU(s), RCCL gather to rank 0" % world) if sharded
-                               else "1 GPU",
-            },
-            "roofline": roof,
-            "detail": {
-                "inflight": D,
-                "warmup_requested": args.warmup,
-                "latency_ms_enc": round(t_enc / K * 1e3, 3),
-                "latency_ms_dec": round(t_dec / K * 1e3, 3),
-                "compressed_bytes": comp_total,
-                "ratio": round(ratio, 5),
-                "lossless": lossless,
-                "file_sha256": sha,
-                "bit_exact_vs_reference": (sha == golden) if golden else None,
-                "single_image_MBps": round(raw_total / single_ms / 1e3, 1) if single_ms else None,
-                "single_image_ms": round(single_ms, 3) if single_ms else None,
-                "no_index_decode_MBps": round(raw_total / noix_ms / 1e3, 1) if noix_ms else None,
-                "no_index_decode_lossless": noix_ok,
-                "setup_steps": D,
-                **legs,
-                "kernel_avg_ms_under_load": {k: round(v, 4) for k, v in kavg.items()},
-                "kernel_avg_ms_one_in_flight": {k: round(v, 4) for k, v in iso.items()},
-                "pmc_hbm_bytes_per_launch": pmc,
-                "pmc_source": pmc_note,
-            },
-        }
-        if not sharded and not args.no_config2:
-            try:
-                res["detail"]["config2_single_stream"] = config2_leg(args)
-            except Exception as e:      # reported, never silently replaced
-                res["detail"]["config2_single_stream"] = {"error": repr(e)[:300]}
-        if world == 1 and not args.no_cpu_baseline:
-            try:
-                res["cpu_baseline"] = cpu_baseline(s0.rgb.cpu().numpy(), W, H, args)
-            except Exception as e:      # reported, never silently replaced
-                res["cpu_baseline"] = {"value": None, "error": repr(e)[:300]}
-        print(json.dumps(res), flush=True)
-    if sharded:
-        dist.destroy_process_group()
-    if not lossless or noix_ok is False:
+    kavg = {k: v[0] / v[1] for k, v in stats.items() if v[1]}
+    ratio = comp_total / raw_total
+    roof = roofline_obj(iso.get(DOM) or None, kavg, ratio, W * rows * 3, raw_total, K, el, pmc)
+    golden = golden_sha(W, H, args.seed, args.noise)
+    res = {
+        "metric": metric_name(),
+        "value": round(value, 2),
+        "unit": "MB/s",
+        "n_gpus": 1,
+        "steps": K,
+        "warmup": warm,
+        "ms_per_step": round(el / K * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic",
+        "config": {
+            "workload": ("%dx%d synthetic RGB (gradient + triangular noise k=%d, seeds %d..%d: one image per "
+                         "slot), 256x256 tiles, choh -s0 encode + dhoh decode, %s, %d image(s) in flight per GPU"
+                         % (W, H, args.noise, args.seed, args.seed + D - 1,
+                            "side index" if not args.no_index else "serial decode", D)),
+            "W": W, "H": H, "tiles": (W // 256) * (H // 256), "per_gpu": "%dx%d" % (W, rows),
+            "parallelism": "1 GPU",
+        },
+        "roofline": roof,
+        "detail": {
+            "inflight": D,
+            "warmup_requested": args.warmup,
+            "latency_ms_enc": round(t_enc / K * 1e3, 3),
+            "latency_ms_dec": round(t_dec / K * 1e3, 3),
+            "compressed_bytes": comp_total,
+            "ratio": round(ratio, 5),
+            "lossless": lossless,
+            "file_sha256": sha,
+            "bit_exact_vs_reference": (sha == golden) if golden else None,
+            "slot_files_bit_exact": "%d of %d" % (slot_match, slot_checked),
+            "slot_files_bit_exact_all": (slot_match == slot_checked and not slot_nogolden) if slot_checked else None,
+            "slot_files_no_golden_seeds": slot_nogolden,
+            "single_image_MBps": round(raw_total / single_ms / 1e3, 1) if single_ms else None,
+            "single_image_ms": round(single_ms, 3) if single_ms else None,
+            "no_index_decode_MBps": round(raw_total / noix_ms / 1e3, 1) if noix_ms else None,
+            "no_index_decode_lossless": noix_ok,
+            "setup_steps": D,
+            **legs,
+            "kernel_avg_ms_under_load": {k: round(v, 4) for k, v in kavg.items()},
+            "kernel_avg_ms_one_in_flight": {k: round(v, 4) for k, v in iso.items()},
+            "pmc_hbm_bytes_per_launch": pmc,
+            "pmc_source": pmc_note,
+        },
+    }
+    if not args.no_config2:
+        try:
+            res["detail"]["config2_single_stream"] = config2_leg(args)
+        except Exception as e:      # reported, never silently replaced
+            res["detail"]["config2_single_stream"] = {"error": repr(e)[:300]}
+    if not args.no_cpu_baseline:
+        try:
+            res["cpu_baseline"] = cpu_baseline(s0.rgb.cpu().numpy(), W, H, args)
+        except Exception as e:      # reported, never silently replaced
+            res["cpu_baseline"] = {"value": None, "error": repr(e)[:300]}
+    print(json.dumps(res), flush=True)
+    if not lossless or noix_ok is False or slot_match != slot_checked:
         sys.exit(3)
 
 

@@ -208,8 +208,9 @@ int hoh_get_kernel_stats(hoh_ctx* c, const char** names, double* total_ms, uint6
   return k;
 }
 
-// measurement only (not in include/): copy a workspace of the last encode to the host
-// (0: the LZ match lists, 1: k_lz's segment walks)
+#ifdef HOH_DEBUG_READ
+// debug builds only (make DEBUG_READ=1; not in include/, not in the product library): copy a
+// workspace of the last encode to the host (0: the LZ match lists, 1: k_lz's segment walks)
 extern "C" int hoh_debug_read(hoh_ctx* c, int which, void* dst, size_t bytes) {
   if (!c || !dst) return HOH_E_ARG;
   if (which == 2) {                    // the tail of the decoder's back-distance map buffer
@@ -221,6 +222,7 @@ extern "C" int hoh_debug_read(hoh_ctx* c, int which, void* dst, size_t bytes) {
   if (bytes > b.n || !b.p) return HOH_E_ARG;
   return hipMemcpy(dst, b.p, bytes, hipMemcpyDeviceToHost) == hipSuccess ? HOH_OK : HOH_E_HIP;
 }
+#endif
 
 void hoh_reset_kernel_stats(hoh_ctx* c) {
   if (!c) return;
@@ -424,11 +426,17 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   launch_front(j, s);            prof.mark("front");
   launch_palette(j, s);          prof.mark("palette");
   if (speed) {
-    if (!c->side.s) {
-      if (hipStreamCreateWithFlags(&c->side.s, hipStreamNonBlocking) != hipSuccess ||
-          hipEventCreateWithFlags(&c->side.fork, hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&c->side.join, hipEventDisableTiming) != hipSuccess)
+    if (!c->side.s) {           // all three or none: a partial set is destroyed, never kept
+      SideStream t;
+      if (hipStreamCreateWithFlags(&t.s, hipStreamNonBlocking) != hipSuccess ||
+          hipEventCreateWithFlags(&t.fork, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&t.join, hipEventDisableTiming) != hipSuccess) {
+        if (t.s) (void)hipStreamDestroy(t.s);
+        if (t.fork) (void)hipEventDestroy(t.fork);
+        if (t.join) (void)hipEventDestroy(t.join);
         return HOH_E_HIP;
+      }
+      c->side = t;
     }
     encode_speed_s(j, s, c->side, prof_cb, &prof);
     if (hipGetLastError() != hipSuccess) return HOH_E_HIP;

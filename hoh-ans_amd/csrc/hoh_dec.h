@@ -36,9 +36,6 @@ struct DecTile {
 struct DecWork {
   void* bufs[16] = {nullptr};
   size_t sizes[16] = {0};
-  // a second stream for the chain tiles' decode, which overlaps the wavefront unpredict
-  hipStream_t side = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
 };
 
 void dec_free(DecWork& w);

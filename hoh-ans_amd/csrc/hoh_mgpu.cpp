@@ -266,8 +266,9 @@ int hoh_mgpu_decode_image(hoh_mgpu* m, const uint8_t* d_hoh, size_t size, uint8_
   };
   uint64_t v;
   if (!rv(v) || !rv(v) || p + 2 > tcap) return HOH_E_CORRUPT;              // W-1, H-1
-  // x_tiles-1, y_tiles-1 must be the tiling of W x H (as decode_image_impl checks)
-  if (xt != txt || yt != tyt || tb[p] != txt - 1 || tb[p + 1] != tyt - 1) return HOH_E_CORRUPT;
+  // x_tiles-1, y_tiles-1 must be the tiling of W x H (as decode_image_impl checks: one byte each,
+  // so 256 tiles on an axis wrap to 0, choh.cpp:457-458)
+  if (xt != txt || yt != tyt || tb[p] != (uint8_t)(txt - 1) || tb[p + 1] != (uint8_t)(tyt - 1)) return HOH_E_CORRUPT;
   p += 2;
   std::vector<uint64_t> tsz(ntiles);
   uint64_t sum = 0;

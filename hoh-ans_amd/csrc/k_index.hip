@@ -28,9 +28,4 @@ void dec_free(DecWork& w) {
     w.bufs[i] = nullptr;
     w.sizes[i] = 0;
   }
-  if (w.side) (void)hipStreamDestroy(w.side);
-  if (w.fork) (void)hipEventDestroy(w.fork);
-  if (w.join) (void)hipEventDestroy(w.join);
-  w.side = nullptr;
-  w.fork = w.join = nullptr;
 }

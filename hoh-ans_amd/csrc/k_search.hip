@@ -746,9 +746,6 @@ __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring,
       if (lane == l) c = hit;
     }
     if (f && !c) {
-#ifdef HOH_LZC_NOV                                                     // measurement knob (invalid files)
-      (void)w;
-#else
       // vertical backs beyond the window: sixteen rows per batch of (coalesced) global loads
       const uint32_t vlim = min(65536u, q);
       for (uint32_t b0 = (bm / w + 1) * w; b0 <= vlim && !c; b0 += 16 * w) {
@@ -758,7 +755,6 @@ __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring,
 #pragma unroll
         for (int u = 0; u < 16; u++) c |= v[u] == f;
       }
-#endif
     }
     const uint64_t word = __ballot(c);
     if (lane == 0 && q < npix) cand[q >> 6] = word;
@@ -816,7 +812,7 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
   __shared__ uint16_t hl_all[LZS_SEG][LZS_HB * 64];                    // a batch's hit list per wave
   __shared__ uint32_t s_cnt[LZS_SEG], s_exit[LZS_SEG];
   const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  TileInfo ti = j.tiles[t];
+  const TileInfo ti = j.tiles[t];
   const uint32_t npix = (uint32_t)ti.w * ti.h, nwords = (npix + 63) / 64, w = ti.w;
   const uint64_t* bits = j.candbits + (size_t)t * (j.npix_cap / 64);
   const uint32_t* F = j.fpb + (size_t)t * j.npix_cap;
@@ -1084,12 +1080,13 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
   uint32_t nk = 0;
   for (uint32_t m = lane; m < nmk; m += 64) nk += mt[3 * m + 1];
   for (int o = 32; o > 0; o >>= 1) nk += __shfl_xor(nk, o);
+  // only the fields this kernel owns: it runs on the side stream while k_rawmed / k_search read
+  // the same TileInfo (flags through an atomic OR, never a whole-struct store)
   if (lane == 0) {
-    if (overflow) ti.flags |= TF_OVERFLOW;
-    ti.nmatch = nm;
-    ti.nfut = nf;
-    ti.nclean = (overflow || !nmk) ? npix : npix - nk;
-    j.tiles[t] = ti;
+    if (overflow) atomicOr(&j.tiles[t].flags, (uint32_t)TF_OVERFLOW);
+    j.tiles[t].nmatch = nm;
+    j.tiles[t].nfut = nf;
+    j.tiles[t].nclean = (overflow || !nmk) ? npix : npix - nk;
   }
 }
 
@@ -1377,11 +1374,10 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, v
   // nothing with the predictor search (RGB -> planes, residuals, histograms), so they run on the
   // context's side stream beside it; k_nuke (which compacts the searched planes) joins the two.
   // The search scratch and the LZ map lie in disjoint parts of each tile's tab_gen region.
-  hipStream_t sl = side.s ? side.s : s;
-  if (side.s) {
-    (void)hipEventRecord(side.fork, s);
-    (void)hipStreamWaitEvent(sl, side.fork, 0);
-  }
+  // a failed fork runs the LZ kernels on s itself (ordered), never unordered on the side stream
+  const bool fork = side.s && side.fork && side.join && hipEventRecord(side.fork, s) == hipSuccess &&
+                    hipStreamWaitEvent(side.s, side.fork, 0) == hipSuccess;
+  hipStream_t sl = fork ? side.s : s;
   {
     hipLaunchKernelGGL(k_lzfp, dim3(16, j.ntiles), dim3(NT), 0, sl, j);
     // the hash tables pay at -s1's window (1024); the longer windows of -s2..-s4 fill them and
@@ -1401,7 +1397,8 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, v
     hipLaunchKernelGGL(k_lzscan, dim3(j.ntiles), dim3(64 * LZS_SEG), (size_t)nseg * (rp ? rp + 16 : 1) * 4, sl, j, limit,
                        rp, nseg);
   }
-  if (side.s) (void)hipEventRecord(side.join, sl);
+  // the join: if its record fails, s waits for the whole side stream instead
+  const bool joined = fork && hipEventRecord(side.join, sl) == hipSuccess;
   if (j.speed >= 3) hipLaunchKernelGGL(k_rawmed, dim3(j.ntiles), dim3(NT), 0, s, j);
   {
     const int npred = j.speed * 5 < 14 ? j.speed * 5 : 14;
@@ -1415,7 +1412,7 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, v
     }
   }
   mark(mc, "search");
-  if (side.s) (void)hipStreamWaitEvent(s, side.join, 0);
+  if (fork && (!joined || hipStreamWaitEvent(s, side.join, 0) != hipSuccess)) (void)hipStreamSynchronize(sl);
   launch_nuke(j, s);
   mark(mc, "lz");
   hipLaunchKernelGGL(k_setup_s, dim3(j.ntiles), dim3(128), 0, s, j);

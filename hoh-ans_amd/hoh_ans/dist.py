@@ -69,6 +69,7 @@ class FileGather:
     def __init__(self, W, H, device, group=None):
         self.W, self.H, self.device, self.group = W, H, device, group
         self.file = None
+        self.total = 0            # rank 0: bytes of the last assembled file
 
     def __call__(self, blob, size, tile_sizes, wait=True):
         """wait=False: return the pending point-to-point requests instead of waiting on them (the
@@ -95,6 +96,7 @@ class FileGather:
             return None, 0, reqs
         prefix = file_prefix(self.W, self.H, np.concatenate(sizes))
         total = len(prefix) + sum(blob_sizes)
+        self.total = total
         if self.file is None or self.file.numel() < total:
             self.file = torch.empty(total, dtype=torch.uint8, device=self.device)
         self.file[:len(prefix)] = torch.frombuffer(bytearray(prefix), dtype=torch.uint8).to(self.device)
@@ -130,3 +132,45 @@ def run_pipeline(nslots, total, enqueue, finish):
         finish(i % nslots, i)
         order.append(i)
     return order
+
+
+def run_sharded_leg(ops, nslots, steps, warmup):
+    """One timed leg of bench.py's N > 1 path, independent of the device: `nslots` images in
+    flight per rank, a set-up pass (one step per slot: workspaces are sized outside the timed
+    region), `warmup` steps, then exactly `steps` steps bracketed by a barrier and a device drain
+    on both sides; the leg's time is the maximum over ranks.  `ops` supplies the device side:
+      new_slot(k) -> slot;  enqueue(slot, i) (encode of the shard, sizes copied to the host);
+      finish(slot, i) (FileGather of the blobs to rank 0 + decode of the shard);  drain() (wait
+      for the device);  check(total) (statuses of steps 0..total-1);  reset(slots) (clear timing
+      state after the warmup);  lossless(slot) -> bool;  device (for the reductions).
+    bench.py passes its GPU ops (hoh_encode_tiles_async / hoh_decode_tiles_async over RCCL);
+    tests/test_dist_gloo.py passes CPU ops (the oracle) over gloo.
+    Returns (slots, max-over-ranks seconds, lossless on every rank)."""
+    import time
+    import torch
+    import torch.distributed as dist
+    slots = [ops.new_slot(k) for k in range(nslots)]
+    ops.drain()
+
+    def run(total):
+        run_pipeline(nslots, total, lambda k, i: ops.enqueue(slots[k], i), lambda k, i: ops.finish(slots[k], i))
+        ops.drain()
+        ops.check(total)
+
+    run(nslots)
+    if warmup:
+        run(warmup)
+    ops.reset(slots)
+    dist.barrier()
+    ops.drain()
+    t = time.perf_counter()
+    run_pipeline(nslots, steps, lambda k, i: ops.enqueue(slots[k], i), lambda k, i: ops.finish(slots[k], i))
+    ops.drain()
+    dist.barrier()
+    el = time.perf_counter() - t
+    ops.check(steps)
+    ok = all(ops.lossless(s) for s in slots)
+    tt = torch.tensor([el, 0.0 if ok else 1.0], dtype=torch.float64, device=ops.device)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    el, bad = tt.tolist()
+    return slots, el, bad == 0.0

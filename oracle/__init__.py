@@ -30,7 +30,10 @@ def build():
     if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
         subprocess.check_call(["gcc", "-O2", "-shared", "-fPIC", "-o", so, src, "-lm"])
     if os.path.isdir("/root/reference"):
-        subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "ref")])
+        subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "ref"), "all"])
+        # the reference's own callers against the drop-in headers + libhohgpu (needs the library)
+        if os.path.exists(os.path.join(os.path.dirname(HERE), "hoh-ans_amd", "lib", "libhohgpu.so")):
+            subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "ref"), "dropin"])
 
 
 def _p(a, t):

@@ -1,0 +1,82 @@
+"""The reference's own test flow, run through the GPU drop-ins.
+
+oracle/ref/Makefile `dropin` compiles the reference's callers UNCHANGED -- simple_entropy_encoder.cpp
+(:26-33, encode_entropy(bytes, n, 256, out, 12, 1)), simple_entropy_decoder.cpp (:28-34,
+decode_entropy_8bit) and layer_roundtrip_test.cpp (:7-59, layer_encode cruncher 2 -> decode_layer)
+-- against include/hoh/*.hpp, linked to libhohgpu.so, into oracle/_ref/dropin/.  These tests run
+the flow of entropy_roundtrip_test.sh:1-11 and the layer round trip with those binaries:
+  * the drop-in encoder's stream must equal the reference encoder's (oracle/_ref, the reference
+    binary built from the same source without the drop-ins) byte for byte;
+  * the drop-in decoder must restore the input (cmp), from its own stream and the reference's;
+  * the reference decoder must read the drop-in's stream back too (one stream: Q1 does not bite);
+  * layer_roundtrip_test must print "Layer roundtrip: OK" and exit 0 through the GPU.
+The inputs are repository files (the reference encodes its own source text; that file is not
+kept here), plus byte patterns that reach the stored fallback and a single-symbol table (Q6)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = os.path.join(ROOT, "oracle", "_ref")
+DROP = os.path.join(REF, "dropin")
+
+
+def _bin(d, name):
+    p = os.path.join(d, name)
+    assert os.path.exists(p), "%s not built (make -C oracle/ref all dropin, in the container)" % p
+    return p
+
+
+def _run(args, **kw):
+    return subprocess.run(args, capture_output=True, text=True, timeout=120, **kw)
+
+
+def _inputs(tmp_path):
+    files = [os.path.join(ROOT, "tools", "cli", "choh.cpp"), os.path.join(ROOT, "bench.py"),
+             os.path.join(ROOT, "include", "hoh_ans.h")]
+    rng = np.random.default_rng(5)
+    extra = {
+        "wide.bin": rng.integers(0, 256, 20000, dtype=np.uint8).tobytes(),          # stored fallback (Q7)
+        "one.bin": bytes([200]) * 4097,                                             # one symbol (Q6)
+        "geo.bin": np.minimum(rng.geometric(0.08, 70000) - 1, 255).astype(np.uint8).tobytes(),
+    }
+    for k, v in extra.items():
+        p = tmp_path / k
+        p.write_bytes(v)
+        files.append(str(p))
+    return files
+
+
+def test_entropy_roundtrip_flow(tmp_path):
+    """entropy_roundtrip_test.sh:1-11 with the drop-in binaries, plus byte equality with the
+    reference encoder and cross-decoding in both directions."""
+    enc_d, dec_d = _bin(DROP, "simple_entropy_encoder"), _bin(DROP, "simple_entropy_decoder")
+    enc_r, dec_r = _bin(REF, "simple_entropy_encoder"), _bin(REF, "simple_entropy_decoder")
+    for i, f in enumerate(_inputs(tmp_path)):
+        src = open(f, "rb").read()
+        cg, cr = tmp_path / ("c_gpu%d" % i), tmp_path / ("c_ref%d" % i)
+        r = _run([enc_d, f, str(cg)])
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert "wrote %d bytes" % cg.stat().st_size in r.stdout
+        r = _run([enc_r, f, str(cr)])
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert cg.read_bytes() == cr.read_bytes(), f
+        for dec, c in ((dec_d, cg), (dec_d, cr), (dec_r, cg)):
+            out = tmp_path / ("d%d" % i)
+            r = _run([dec, str(c), str(out)])
+            assert r.returncode == 0, r.stdout + r.stderr
+            assert out.read_bytes() == src, (dec, f)           # cmp -s
+            out.unlink()
+
+
+def test_layer_roundtrip_flow():
+    """layer_roundtrip_test.cpp:7-59 (5x4 plane, depth 8, cruncher 2, no LZ) through the GPU
+    drop-ins, beside the reference binary of the same source."""
+    r = _run([_bin(DROP, "layer_roundtrip_test")])
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Layer roundtrip: OK" in r.stdout
+    r = _run([_bin(REF, "layer_roundtrip_test")])
+    assert r.returncode == 0 and "Layer roundtrip: OK" in r.stdout

@@ -147,8 +147,9 @@ def test_normalize_steals_many_levels(seed, pb):
 def test_fast_chain_all_prob_bits(pb):
     """The f64-quotient chain (k_rans_fast KIND 1) at every prob_bits of the -s>=1 ladder
     (layer_encode.hpp:326-391) against the oracle (rans64.hpp:262-278): geometric, uniform and
-    peaked histograms (at prob_bits 19 a frequency above 2^18 hands the stream to k_rans_gen),
-    one-symbol streams and ranges 2..512."""
+    peaked histograms, one-symbol streams and ranges 2..512.  Every stream at prob_bits 7..19
+    takes the chain: its f64 floors are exact for every f <= 2^19 (k_rans_enc.hip, step15's
+    bound), so the peaked pb-19 cases (frequencies up to 2^19) check that bound."""
     import oracle
     import hoh_ans
     rng = np.random.default_rng(77 + pb)
