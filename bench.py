@@ -564,6 +564,8 @@ def main():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--noise", type=int, default=4)
     ap.add_argument("--inflight", type=int, default=20, help="images in flight per GPU (1 = one at a time)")
+    ap.add_argument("--hw-queues", type=int, default=0,
+                    help="GPU_MAX_HW_QUEUES for this process (default: one per in-flight image, at most 32)")
     ap.add_argument("--strong-inflight", type=int, default=8, help="images in flight per GPU in the 16384^2 leg")
     ap.add_argument("--no-index", action="store_true", help="decode without the side index (serial rANS)")
     ap.add_argument("--cpu-tiles", type=int, default=512)
@@ -608,7 +610,9 @@ def main():
         q = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
     except ValueError:
         q = 4
-    if q < D:
+    if args.hw_queues > 0:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, args.hw_queues))
+    elif q < D:
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, D))
 
     import torch

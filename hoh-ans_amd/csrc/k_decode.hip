@@ -485,6 +485,9 @@ typedef uint2 __attribute__((may_alias)) u2_ma;
 typedef uint4 __attribute__((may_alias)) u4_ma;
 __device__ __forceinline__ uint2 lds_u2(uint32_t a) { return *(const __attribute__((address_space(3))) u2_ma*)(size_t)a; }
 __device__ __forceinline__ uint32_t lds_u32(uint32_t a) { return *(const __attribute__((address_space(3))) u32_ma*)(size_t)a; }
+__device__ __forceinline__ uint32_t lds_u16(uint32_t a) { return *(const __attribute__((address_space(3))) u16_ma*)(size_t)a; }
+__device__ __forceinline__ void lds_st16(uint32_t a, uint32_t v) { *(__attribute__((address_space(3))) u16_ma*)(size_t)a = (uint16_t)v; }
+__device__ __forceinline__ void lds_st2(uint32_t a, uint2 v) { *(__attribute__((address_space(3))) u2_ma*)(size_t)a = v; }
 __device__ __forceinline__ void lds_st32(uint32_t a, uint32_t v) { *(__attribute__((address_space(3))) u32_ma*)(size_t)a = v; }
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(size_t)(const __attribute__((address_space(3))) unsigned char*)p;
@@ -494,6 +497,9 @@ __device__ uint32_t lds_addr(const void*);
 __device__ void lds_st32(uint32_t, uint32_t);
 __device__ uint2 lds_u2(uint32_t);
 __device__ uint32_t lds_u32(uint32_t);
+__device__ uint32_t lds_u16(uint32_t);
+__device__ void lds_st16(uint32_t, uint32_t);
+__device__ void lds_st2(uint32_t, uint2);
 #endif
 
 __device__ __forceinline__ uint32_t dstep(uint32_t bk, uint32_t sy, uint32_t bmask,
@@ -898,11 +904,11 @@ __device__ __forceinline__ uint32_t dstep_m(uint32_t bk, uint32_t sy, uint32_t b
 // One chain lane: the whole stream d with its tables at LDS bytes (bkb, syb) and its payload
 // ring in slots t4 + 256 s.  Payload words are fetched as raw dwords one 16-symbol group ahead and
 // aligned when they land in the ring (aligning at the fetch made every fetch wait for its load).
-__device__ __forceinline__ bool dm_chain(const DecJob& j, const DecStream& d, uint32_t* dm_lds, uint32_t bkb,
-                                      uint32_t syb) {
+template <class Step, class Look>
+__device__ __forceinline__ bool dm_chain_t(const DecJob& j, const DecStream& d, Step step, Look look) {
   const uint32_t t4 = (uint32_t)threadIdx.x * 4;
   uint16_t* out = j.dsym + d.out_off;
-  const uint32_t pb = d.pb, mask = (1u << pb) - 1, bmask = (mask >> 2) & ~7u;
+  const uint32_t pb = d.pb, mask = (1u << pb) - 1;
   const uint64_t P = d.payload_off;
   const uint32_t al = (uint32_t)(P & 3);
   const uint64_t szal = j.size & ~3ull;
@@ -960,9 +966,9 @@ __device__ __forceinline__ bool dm_chain(const DecJob& j, const DecStream& d, ui
 #pragma unroll
         for (int u = 0; u < 16; u += 2) {
           const uint32_t w0 = lds_u32(t4 | ((wi & (DR_RW - 1)) << 8));
-          const uint32_t a = dstep_m(bkb, syb, bmask, mask, pb, xh, xl, w0, wi);
+          const uint32_t a = step(xh, xl, w0, wi);
           const uint32_t w1 = lds_u32(t4 | ((wi & (DR_RW - 1)) << 8));
-          const uint32_t b = dstep_m(bkb, syb, bmask, mask, pb, xh, xl, w1, wi);
+          const uint32_t b = step(xh, xl, w1, wi);
           pk[gi * 8 + u / 2] = __builtin_amdgcn_perm(b, a, 0x07060302u);
         }
       }
@@ -982,15 +988,12 @@ __device__ __forceinline__ bool dm_chain(const DecJob& j, const DecStream& d, ui
   }
   // the last n % 64 symbols (or a whole stream with prob_bits < 7): one step at a time, payload
   // words from the file
-  DrTables tb;
-  tb.bk = (uint2*)((unsigned char*)dm_lds + bkb);
-  tb.sy = (uint2*)((unsigned char*)dm_lds + syb);
   uint64_t x = ((uint64_t)xh << 32) | xl;
   OutCursor oc(out, d.blk, 0);
   for (uint32_t i = ngrp * 64; i < d.n; i++) {
     const uint32_t slot = (uint32_t)x & mask;
     uint32_t sym, c, f;
-    tb.lookup(slot, sym, c, f);
+    look(slot, sym, c, f);
     oc.put(i, (uint16_t)sym);
     x = (uint64_t)f * (x >> pb) + (slot - c);                // Rans64DecAdvance
     if (x < (1ull << 31)) {
@@ -1000,6 +1003,20 @@ __device__ __forceinline__ bool dm_chain(const DecJob& j, const DecStream& d, ui
     }
   }
   return x == (1ull << 31) && wi <= d.words;
+}
+
+__device__ __forceinline__ bool dm_chain(const DecJob& j, const DecStream& d, uint32_t* dm_lds, uint32_t bkb,
+                                         uint32_t syb) {
+  const uint32_t pb = d.pb, mask = (1u << pb) - 1, bmask = (mask >> 2) & ~7u;
+  DrTables tb;
+  tb.bk = (uint2*)((unsigned char*)dm_lds + bkb);
+  tb.sy = (uint2*)((unsigned char*)dm_lds + syb);
+  return dm_chain_t(
+      j, d,
+      [&](uint32_t& xh, uint32_t& xl, uint32_t nw, uint32_t& wi) {
+        return dstep_m(bkb, syb, bmask, mask, pb, xh, xl, nw, wi);
+      },
+      [&](uint32_t slot, uint32_t& sym, uint32_t& c, uint32_t& f) { tb.lookup(slot, sym, c, f); });
 }
 
 template <int MS>
@@ -1059,6 +1076,179 @@ __global__ __launch_bounds__(64) void k_drans_multi(DecJob j, const uint32_t* li
     __syncthreads();
     if (lane < ns && !dm_chain(j, j.streams[entry(base + lane)], dm_lds, dm_bk(lane), dm_sy(MS, lane)))
       atomicOr(j.gerr, 4u);
+    __syncthreads();                                         // the tables are rebuilt next round
+  }
+}
+
+// ---------------------------------------------------------------- no index: compact chain tables
+// k_drans_lanes: a lane per chain like k_drans_multi, but with tables small enough that one
+// workgroup holds up to 64 chains (k_drans_multi's 12 KB per chain made a workgroup a whole CU's
+// LDS for 12 chains, 12 of 64 lanes busy, and one image's chains held every CU for 7 ms).
+// Per chain (P = symbols present, in cum order):
+//   B[b], b < 2^pb / 64: u16 index k0 of the symbol covering slot 64 b      (1 KB at prob_bits 15)
+//   E[k], k < P + 3:     {c | symbol << 16, f}, then three sentinels c = 0xffff
+// slot -> symbol: k0 = B[slot >> 6]; E[k0 .. k0 + 3] arrive in two ds_read2_b64; the covering
+// entry is the last of them whose start c <= slot -- exact while at most three symbols start in
+// (64 b, slot], i.e. everywhere but the rare-symbol tails, where the lane walks on entry by entry
+// (the sentinels end every walk).  Synthetic tiles (P ~ 30-55): ~1.5 KB per chain; the worst
+// case (P = 512) 5.1 KB.  Rounds are packed by table size: a workgroup claims the next list
+// entries whose tables fit its LDS budget (at most 64) with a CAS on a device head (gerr[10]), so
+// a round holds as many chains as fit and the grid (two workgroups per CU) keeps several images'
+// chains resident at once.
+#define DL_BSH 6
+#define DL_SCR 4096u             // abort word + list counts (payload rings below, [0, 4 KB))
+#define DL_TAB 4160u             // first table byte
+#define DL_HEAD 10               // gerr word: next list entry to claim
+
+__host__ __device__ __forceinline__ uint32_t dl_nb(uint32_t pb) { return pb > DL_BSH ? 1u << (pb - DL_BSH) : 1u; }
+__host__ __device__ __forceinline__ uint32_t dl_bytes(uint32_t pb, uint32_t npres) {
+  return ((dl_nb(pb) * 2 + 7) & ~7u) + 8 * (npres + 3);
+}
+
+// every multi_ok stream's compact table size; one wave per stream
+__global__ __launch_bounds__(64) void k_dlsize(DecJob j, uint32_t* tbytes) {
+  if (dec_abort(j)) return;
+  const int sid = blockIdx.x, lane = threadIdx.x;
+  const DecStream d = j.streams[sid];
+  if (!multi_ok(d)) return;
+  const uint32_t* cum = j.cum + (size_t)sid * j.cum_stride;
+  uint32_t cv[9], cnt = 0;
+#pragma unroll
+  for (int e = 0; e < 9; e++) cv[e] = 8 * lane + e <= d.range ? cum[8 * lane + e] : 0;
+#pragma unroll
+  for (int e = 0; e < 8; e++) cnt += (8 * lane + e < d.range && cv[e + 1] > cv[e]) ? 1u : 0u;
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+  if (lane == 0) tbytes[sid] = dl_bytes(d.pb, cnt);
+}
+
+// one decode step on a compact table (B at byte Bb, E at byte Eb); returns the entry's low word
+// (symbol in the high half)
+__device__ __forceinline__ uint32_t dstep_l(uint32_t Bb, uint32_t Eb, uint32_t mask, uint32_t pb, uint32_t& xh,
+                                           uint32_t& xl, uint32_t nw, uint32_t& wi) {
+  const uint32_t slot = xl & mask;
+  const uint32_t k0 = lds_u16(Bb + ((slot >> DL_BSH) << 1));
+  const uint32_t ea = Eb + (k0 << 3);
+  const uint2 e0 = lds_u2(ea), e1 = lds_u2(ea + 8), e2 = lds_u2(ea + 16), e3 = lds_u2(ea + 24);
+  uint2 t = (e1.x & 0xffffu) <= slot ? e1 : e0;
+  t = (e2.x & 0xffffu) <= slot ? e2 : t;
+  if ((e3.x & 0xffffu) <= slot) {                            // four or more starts: walk on
+    t = e3;
+    for (uint32_t a = ea + 32;; a += 8) {
+      const uint2 u = lds_u2(a);
+      if ((u.x & 0xffffu) > slot) break;
+      t = u;
+    }
+  }
+  const uint32_t d = slot - (t.x & 0xffffu);
+  const uint32_t yl = __builtin_amdgcn_alignbit(xh, xl, pb);
+  const uint64_t acc = ((uint64_t)__umul24(t.y, xh >> pb) << 32) | d;
+  uint64_t x, co;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(x), "=s"(co) : "v"(t.y), "v"(yl), "v"(acc));
+  const uint32_t nh = (uint32_t)(x >> 32), nl = (uint32_t)x;
+  const bool r = x < (1ull << 31);
+  xh = r ? nl : nh;
+  xl = r ? nw : nl;
+  wi += r;
+  return t.x;
+}
+
+__global__ __launch_bounds__(64) void k_drans_lanes(DecJob j, const uint32_t* list, int nlist, const uint32_t* tbytes,
+                                                    uint32_t budget) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t dm_lds[];
+  const int lane = threadIdx.x;
+  uint32_t* scr = dm_lds + DL_SCR / 4;
+  if (lane == 0) {
+    scr[0] = *(volatile const uint32_t*)j.gerr;
+    scr[1] = *(volatile const uint32_t*)(j.gerr + 5);
+    scr[2] = *(volatile const uint32_t*)(j.gerr + 6);
+  }
+  __syncthreads();
+  if (scr[0]) return;
+  const uint32_t cl = scr[1], total = scr[1] + scr[2];
+  auto entry = [&](uint32_t i) -> uint32_t { return i < cl ? list[i] : list[nlist - 1 - (i - cl)]; };
+  for (;;) {
+    // claim a round: the next entries (at most 64) whose tables fit the budget
+    uint32_t p, n, tb = 0;
+    for (;;) {
+      p = 0;
+      if (lane == 0) p = __hip_atomic_load(j.gerr + DL_HEAD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      p = __shfl(p, 0);
+      if (p >= total) break;
+      const uint32_t i = p + (uint32_t)lane;
+      const uint32_t sz = i < total ? min(tbytes[entry(i)], budget + 1) : budget + 1;
+      uint32_t incl = sz;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(incl, o);
+        if (lane >= o) incl += u;
+      }
+      n = (uint32_t)__popcll(__ballot(i < total && incl <= budget));
+      tb = DL_TAB + incl - sz;                              // this lane's table (lane m <-> chain m)
+      uint32_t won = 0;
+      if (lane == 0 && n) {
+        uint32_t exp = p;
+        won = __hip_atomic_compare_exchange_strong(j.gerr + DL_HEAD, &exp, p + n, __ATOMIC_RELAXED,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 1u : 0u;
+      }
+      if (__shfl(won, 0)) break;
+      if (__shfl(n, 0) == 0) {                               // cannot happen: budget >= dl_bytes(15, 512)
+        if (lane == 0) atomicOr(j.gerr, 4u);
+        return;
+      }
+    }
+    if (p >= total) break;
+    // tables of every chain of the round, the whole wave per stream
+    for (uint32_t m = 0; m < n; m++) {
+      const uint32_t sid = entry(p + m);
+      const DecStream d = j.streams[sid];
+      const uint32_t* cum = j.cum + (size_t)sid * j.cum_stride;
+      const uint32_t Bb = __shfl(tb, (int)m), Eb = Bb + ((dl_nb(d.pb) * 2 + 7) & ~7u);
+      uint32_t pres = 0, cv[9];
+#pragma unroll
+      for (int e = 0; e < 9; e++) cv[e] = 8 * lane + e <= d.range ? cum[8 * lane + e] : 0;
+#pragma unroll
+      for (int e = 0; e < 8; e++)
+        if (8 * lane + e < d.range && cv[e + 1] > cv[e]) pres |= 1u << e;
+      const uint32_t c = __popc(pres);
+      uint32_t incl = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o);
+        if (lane >= o) incl += t;
+      }
+      const uint32_t P = __shfl(incl, 63);
+      uint32_t k = incl - c;
+      for (int e = 0; e < 8; e++) {
+        if (!((pres >> e) & 1)) continue;
+        const uint32_t sv = 8 * lane + e, c0 = cv[e], c1 = cv[e + 1];
+        lds_st2(Eb + 8 * k, make_uint2(c0 | (sv << 16), c1 - c0));
+        for (uint32_t b = (c0 + (1u << DL_BSH) - 1) >> DL_BSH; b <= (c1 - 1) >> DL_BSH; b++) lds_st16(Bb + 2 * b, k);
+        k++;
+      }
+      if (lane < 3) lds_st2(Eb + 8 * (P + lane), make_uint2(0xffffu, 0u));
+    }
+    __syncthreads();
+    if ((uint32_t)lane < n) {
+      const DecStream d = j.streams[entry(p + lane)];
+      const uint32_t pb = d.pb, mask = (1u << pb) - 1, Bb = tb, Eb = tb + ((dl_nb(pb) * 2 + 7) & ~7u);
+      const bool ok = dm_chain_t(
+          j, d,
+          [&](uint32_t& xh, uint32_t& xl, uint32_t nw, uint32_t& wi) { return dstep_l(Bb, Eb, mask, pb, xh, xl, nw, wi); },
+          [&](uint32_t slot, uint32_t& sym, uint32_t& c, uint32_t& f) {
+            uint32_t a = Eb + (lds_u16(Bb + ((slot >> DL_BSH) << 1)) << 3);
+            uint2 t = lds_u2(a);
+            for (;;) {
+              const uint2 u = lds_u2(a + 8);
+              if ((u.x & 0xffffu) > slot) break;
+              t = u;
+              a += 8;
+            }
+            sym = t.x >> 16;
+            c = t.x & 0xffffu;
+            f = t.y;
+          });
+      if (!ok) atomicOr(j.gerr, 4u);
+    }
     __syncthreads();                                         // the tables are rebuilt next round
   }
 }
@@ -1671,13 +1861,9 @@ __device__ __forceinline__ void backmap_tile(const DecJob& j, int t) {
 }
 
 #ifdef __HIP_DEVICE_COMPILE__
-__device__ __forceinline__ uint32_t lds_u16(uint32_t a) { return *(const __attribute__((address_space(3))) u16_ma*)(size_t)a; }
-__device__ __forceinline__ void lds_st16(uint32_t a, uint32_t v) { *(__attribute__((address_space(3))) u16_ma*)(size_t)a = (uint16_t)v; }
 __device__ __forceinline__ uint4 lds_u4(uint32_t a) { return *(const __attribute__((address_space(3))) u4_ma*)(size_t)a; }
 __device__ __forceinline__ void lds_st4(uint32_t a, uint4 v) { *(__attribute__((address_space(3))) u4_ma*)(size_t)a = v; }
 #else
-__device__ uint32_t lds_u16(uint32_t);
-__device__ void lds_st16(uint32_t, uint32_t);
 __device__ uint4 lds_u4(uint32_t);
 __device__ void lds_st4(uint32_t, uint4);
 #endif
@@ -2242,6 +2428,26 @@ static int noix_wave() {
   return v;
 }
 
+// HOH_NOIX_MULTI=1: no-index decodes with k_drans_multi (12 chains per CU, round 3) instead of k_drans_lanes
+static int noix_multi() {
+  static const int v = [] { const char* e = getenv("HOH_NOIX_MULTI"); return e ? atoi(e) : 0; }();
+  return v;
+}
+// k_drans_lanes: LDS table budget per workgroup (HOH_DL_BUDGET_KB, >= the 5.1 KB worst-case table)
+// and workgroups per CU (HOH_DL_WG)
+static uint32_t dl_budget() {
+  static const uint32_t v = [] {
+    const char* e = getenv("HOH_DL_BUDGET_KB");
+    const uint32_t kb = e ? (uint32_t)atoi(e) : 56u;
+    return std::max<uint32_t>(std::min<uint32_t>(kb, 150u) * 1024u, dl_bytes(15, 512));
+  }();
+  return v;
+}
+static int dl_wg_per_cu() {
+  static const int v = [] { const char* e = getenv("HOH_DL_WG"); return e ? std::max(1, atoi(e)) : 2; }();
+  return v;
+}
+
 static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s, const AsyncDec* as) {
   j.npix_cap = (uint32_t)(((size_t)j.tw * j.th + 63) / 64 * 64);
   j.lz_cap = (uint32_t)((j.npix_cap / 4 + j.npix_cap / 255 + 16 + 7) / 8 * 8);
@@ -2290,15 +2496,25 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   } else if (noix_wave()) {                                   // the one-wave-per-stream decoder alone
     hipLaunchKernelGGL(k_drans_wave, dim3(S), dim3(64), DL_SMEM, s, j, S, 0);
   } else {
-    // every plane / LZ stream: a chain lane of k_drans_multi; anything else: k_drans_wave
+    // every plane / LZ stream: a chain lane of k_drans_lanes (k_drans_multi with HOH_NOIX_MULTI=1);
+    // anything else: k_drans_wave
     void* q2;
-    if ((e = dbuf(w, 13, (size_t)S * 4, &q2))) return e;
+    if ((e = dbuf(w, 13, (size_t)S * 8, &q2))) return e;
     uint32_t* mlist = (uint32_t*)q2;
+    uint32_t* tbytes = mlist + S;
     hipLaunchKernelGGL(k_dmlist, dim3((S + 255) / 256), dim3(256), 0, s, j, S, mlist);
-    // one workgroup per CU (its LDS is a whole CU's), rounds of DM_MS streams per workgroup
-    const int nmax = std::min(S, 6 * j.ntiles);
-    const int grid = std::min((nmax + DM_MS - 1) / DM_MS, ctx_cus(c));
-    hipLaunchKernelGGL(k_drans_multi<DM_MS>, dim3(grid), dim3(64), dm_smem(DM_MS), s, j, (const uint32_t*)mlist, S);
+    if (noix_multi()) {
+      // one workgroup per CU (its LDS is a whole CU's), rounds of DM_MS streams per workgroup
+      const int nmax = std::min(S, 6 * j.ntiles);
+      const int grid = std::min((nmax + DM_MS - 1) / DM_MS, ctx_cus(c));
+      hipLaunchKernelGGL(k_drans_multi<DM_MS>, dim3(grid), dim3(64), dm_smem(DM_MS), s, j, (const uint32_t*)mlist, S);
+    } else {
+      hipLaunchKernelGGL(k_dlsize, dim3(S), dim3(64), 0, s, j, tbytes);
+      const uint32_t budget = dl_budget();
+      const int grid = std::min(S, dl_wg_per_cu() * ctx_cus(c));
+      hipLaunchKernelGGL(k_drans_lanes, dim3(grid), dim3(64), DL_TAB + budget, s, j, (const uint32_t*)mlist, S,
+                         (const uint32_t*)tbytes, budget);
+    }
     hipLaunchKernelGGL(k_drans_wave, dim3(S), dim3(64), DL_SMEM, s, j, S, 1);
   }
   ctx_mark(c, s, "drans", false);

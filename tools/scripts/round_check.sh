@@ -1,0 +1,40 @@
+#!/bin/bash
+# Round-4 GPU check, in stages (each under its own time limit; stops at the first failure):
+#   tests   all -m gpu tests
+#   bench   the driver-shaped bench line (N = 1) and the N > 1 code path on a one-rank group
+#           (--sharded, with the configs[3] strong leg)
+#   ab      bench.py A/B of the variant libraries listed in $VARS (var/*.so, see mkvar.sh)
+# usage: round_check.sh OUTDIR stage...
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp
+O=gpurun_out/$1; shift; mkdir -p $O
+for st in "$@"; do
+  case $st in
+    tests)
+      timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 170 --timeout-method thread > $O/gputests.log 2>&1 \
+        || { tail -30 $O/gputests.log; exit 1; }
+      tail -2 $O/gputests.log ;;
+    bench)
+      timeout -k 10 240 python -u bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail $O/bench.err; exit 1; }
+      timeout -k 10 240 python -u bench.py --sharded --steps 20 --warmup 5 > $O/sharded.json 2> $O/sharded.err \
+        || { tail $O/sharded.err; exit 1; }
+      python3 - $O <<'PY'
+import json, sys
+for f in ("bench", "sharded"):
+    d = json.load(open(sys.argv[1] + "/%s.json" % f))
+    det = d["detail"]
+    print(f, d["value"], {k: det.get(k) for k in ("bit_exact_vs_reference", "slot_files_bit_exact", "no_index_decode_MBps",
+          "no_index_pipeline_MBps", "natural_s0_single_MBps", "strong_16384_MBps", "strong_16384_bit_exact_vs_reference")})
+PY
+      ;;
+    ab)
+      B="--no-legs --no-pmc --no-cpu-baseline --no-config2"
+      for v in base $VARS; do
+        n=$(basename $v .so)
+        if [ "$v" = base ]; then unset HOH_LIB; else export HOH_LIB=$GRAFT_REPO_ROOT/$v; fi
+        timeout -k 10 200 python -u bench.py --steps 100 --warmup 5 $B > $O/ab_${n}.json 2> $O/ab_err || { tail $O/ab_err; exit 1; }
+        python3 -c "import json; d=json.load(open('$O/ab_${n}.json')); r=d['roofline']; print('$n', d['value'], r['avg_launch_ms'], r['avg_launch_ms_under_load'], d['detail']['bit_exact_vs_reference'], d['detail']['slot_files_bit_exact'])"
+      done
+      unset HOH_LIB ;;
+  esac
+done
