@@ -64,6 +64,7 @@ struct hoh_ctx {
   hipStream_t own = nullptr;
   SideStream side;              // -s>=1: the LZ screen beside the predictor search (created on first use)
   Buf idx8, fpb, pinfo, lg;     // -s>=1 workspaces
+  Buf lzs;                      // -s>=2: LZ posting lists (k_lzsort): sorted + ping-pong + ranks
   uint32_t lg_key[4] = {0, 0, 0, 0};
   uint64_t lg_off[4] = {0, 0, 0, 0};
   Buf sym, hist, candbits, matches, lzspec, pal, streams, tiles, hdr, tab_fast, tab_gen, slabs, ckpt, misc, tsizes;
@@ -162,12 +163,18 @@ int hoh_ctx_create(hoh_ctx** out, int device) {
   return HOH_OK;
 }
 
+// HOH_LZ_POSTING=0: -s2..-s4 LZ scans walk every back distance (the round-3 scan, for comparison)
+static int lz_posting() {
+  static const int v = [] { const char* e = getenv("HOH_LZ_POSTING"); return e ? atoi(e) : 1; }();
+  return v;
+}
+
 static void freebuf(Buf& b) { if (b.p) (void)hipFree(b.p); b.p = nullptr; b.n = 0; }
 
 void hoh_ctx_destroy(hoh_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  Buf* all[] = {&c->idx8, &c->fpb, &c->pinfo, &c->lg, &c->sym, &c->hist, &c->candbits, &c->matches, &c->lzspec, &c->pal, &c->streams, &c->tiles, &c->hdr,
+  Buf* all[] = {&c->idx8, &c->fpb, &c->lzs, &c->pinfo, &c->lg, &c->sym, &c->hist, &c->candbits, &c->matches, &c->lzspec, &c->pal, &c->streams, &c->tiles, &c->hdr,
                 &c->tab_fast, &c->tab_gen, &c->slabs, &c->ckpt, &c->misc, &c->tsizes};
   for (Buf* b : all) freebuf(*b);
   for (Buf& b : c->scr.chunks) freebuf(b);
@@ -346,7 +353,7 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   if (speed && ((size_t)((tw + 39) / 40) * ((th + 39) / 40) > HOH_MAPCAP || tw > 1024)) return HOH_E_UNSUPPORTED;
   if (t0 < 0 || ntiles <= 0 || t0 + ntiles > xt * yt) return HOH_E_ARG;
   Prof prof(c, s, async);
-  EncodeJob j;
+  EncodeJob j{};
   memset(&j, 0, sizeof(j));
   j.speed = speed;
   j.spt = speed ? SPT_S : SK_PER_TILE;
@@ -375,6 +382,15 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
     if ((e = ensure_log2_tables(c, W, H, j))) return e;
     j.idx8 = (uint8_t*)c->idx8.p;
     j.fpb = (uint32_t*)c->fpb.p;
+    j.lzs = nullptr;
+    j.lzrank = nullptr;
+    // posting lists for the long LZ windows (-s2..-s4) of tiles whose positions fit 16 bits
+    if (speed >= 2 && j.npix_cap <= 65536 && lz_posting()) {
+      const size_t per = (size_t)ntiles * j.npix_cap;
+      if ((e = ensure(c->lzs, per * 10))) return e;
+      j.lzs = (uint32_t*)c->lzs.p;
+      j.lzrank = (uint16_t*)((uint32_t*)c->lzs.p + 2 * per);
+    }
     j.pinfo = (PlaneInfo*)c->pinfo.p;
   }
   if ((e = ensure(c->sym, nsym * 2 + 64))) return e;
@@ -641,7 +657,7 @@ int encode_streams_impl(hoh_ctx* c, const uint16_t* d_syms, const uint64_t* off,
     st[i].mode = SM_EMPTY;
     st[i].fast = fast ? 1 : 0;
   }
-  EncodeJob j;
+  EncodeJob j{};
   memset(&j, 0, sizeof(j));
   j.sym = (uint16_t*)d_syms;
   j.streams = (StreamInfo*)c->streams.p;

@@ -790,6 +790,95 @@ __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring,
   if (lane == 0 && ncand) atomicAdd(&j.tiles[t].ncand, ncand);
 }
 
+// LZ posting lists (-s2..-s4: windows of 2048..16384 positions).  Per tile, the positions sorted
+// by a 16-bit hash of their window fingerprint, ascending inside a hash group: every position with
+// the same fingerprint as q and before it is in q's group, before q, in descending order when
+// walked back from q's rank -- so k_lzscan visits only equal-hash positions of q's window, back
+// distances ascending, instead of every fingerprint of the window (lz.hpp:32-50 at seek 11..14).
+// Two stable counting-sort passes (LSD, 8-bit digits) of pos | hash << 16 per tile, one 1024-thread
+// workgroup per tile: per 1024-position chunk, a wave ranks its lanes by digit with 8 ballots, the
+// 16 waves' per-digit counts are prefix-summed in LDS, and each position lands at its digit's base
+// + the counts of the waves before + its rank in its wave (stable).
+__device__ __forceinline__ uint32_t lzs_hash(uint32_t f) { return (f * 0x9E3779B1u) >> 16; }
+#define LZSORT_T 1024
+__global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
+  __shared__ uint32_t base[256];
+  __shared__ uint32_t cnt[LZSORT_T / 64][256];
+  const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const TileInfo ti = j.tiles[t];
+  const uint32_t n = (uint32_t)ti.w * ti.h;
+  const size_t per = (size_t)j.ntiles * j.npix_cap;
+  const uint32_t* F = j.fpb + (size_t)t * j.npix_cap;
+  uint32_t* S = j.lzs + (size_t)t * j.npix_cap;                   // final order
+  uint32_t* T = j.lzs + per + (size_t)t * j.npix_cap;             // after the first pass
+  uint16_t* R = j.lzrank + (size_t)t * j.npix_cap;
+  const uint64_t lt = (1ull << lane) - 1;
+  for (int e = tid; e < (LZSORT_T / 64) * 256; e += LZSORT_T) (&cnt[0][0])[e] = 0;
+  for (int pass = 0; pass < 2; pass++) {
+    const uint32_t sh = 16 + 8 * pass;
+    const uint32_t* in = pass ? T : nullptr;
+    uint32_t* out = pass ? S : T;
+    if (tid < 256) base[tid] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += LZSORT_T) {
+      const uint32_t key = pass ? in[i] : (i | (lzs_hash(F[i]) << 16));
+      atomicAdd(&base[(key >> sh) & 255], 1u);
+    }
+    __syncthreads();
+    if (tid < 64) {                                              // exclusive scan of the 256 counts
+      uint32_t v[4], sum = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) { v[k] = base[4 * tid + k]; sum += v[k]; }
+      uint32_t incl = sum;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(incl, o);
+        if (lane >= o) incl += u;
+      }
+      uint32_t run = incl - sum;
+#pragma unroll
+      for (int k = 0; k < 4; k++) { base[4 * tid + k] = run; run += v[k]; }
+    }
+    __syncthreads();
+    for (uint32_t c0 = 0; c0 < n; c0 += LZSORT_T) {
+      const uint32_t i = c0 + tid;
+      const bool valid = i < n;
+      const uint32_t key = !valid ? 0u : pass ? in[i] : (i | (lzs_hash(F[i]) << 16));
+      const uint32_t d = (key >> sh) & 255;
+      uint64_t peers = __ballot(valid);
+#pragma unroll
+      for (int b = 0; b < 8; b++) {
+        const uint64_t m = __ballot((d >> b) & 1);
+        peers &= ((d >> b) & 1) ? m : ~m;
+      }
+      const uint32_t wr = (uint32_t)__popcll(peers & lt);
+      if (valid && wr == 0) cnt[wv][d] = (uint32_t)__popcll(peers);
+      __syncthreads();
+      if (tid < 256) {                                           // per digit: the waves in order
+        uint32_t run = base[tid];
+#pragma unroll
+        for (int w = 0; w < LZSORT_T / 64; w++) {
+          const uint32_t c = cnt[w][tid];
+          cnt[w][tid] = run;
+          run += c;
+        }
+        base[tid] = run;
+      }
+      __syncthreads();
+      if (valid) {
+        const uint32_t o = cnt[wv][d] + wr;
+        out[o] = key;
+        if (pass) R[key & 0xffffu] = (uint16_t)o;
+      }
+      __syncthreads();
+      if (tid < 256)
+#pragma unroll
+        for (int w = 0; w < LZSORT_T / 64; w++) cnt[w][tid] = 0;
+    }
+    __syncthreads();
+  }
+}
+
 #define LZS_KB 0x1ffffu      // k_lzscan keys: (L << 17) | (LZS_KB - b)
 #define LZS_HB 16        // horizontal back-distance chunks of 64 whose fingerprints load at once
 #define LZS_VB 4         // vertical chunks (k * w <= 65536: 256 rows of a 256-wide tile)
@@ -825,6 +914,9 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
     else if (ti.colours <= 32) bonus = 2;
   }
   const uint32_t thr = 4 + bonus;
+  const bool post = j.lzs != nullptr;                                  // posting lists (k_lzsort)
+  const uint32_t* PS = post ? j.lzs + (size_t)t * j.npix_cap : nullptr;
+  const uint16_t* PR = post ? j.lzrank + (size_t)t * j.npix_cap : nullptr;
   const bool lds_bits = nwords <= LZS_BITS;
   const uint32_t nseg = (lds_bits && rp && nwords >= 4 * LZS_SEG && nseg_req > 1) ? (uint32_t)nseg_req : 1u;
   const uint32_t segcap = j.lz_cap / LZS_SEG;
@@ -909,7 +1001,7 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
 #pragma unroll
     for (int c = 0; c < LZS_HB; c++) {
       const uint32_t b = 1 + 64 * c + lane;
-      fv[c] = b <= bm ? F[q - b] : 0u;
+      fv[c] = b <= bm && !post ? F[q - b] : 0u;
     }
 #pragma unroll
     for (int c = 0; c < LZS_VB; c++) {
@@ -924,6 +1016,32 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
     // walk.  Keys (L << 17) | (LZS_KB - b): L <= 259, b <= 65536 < LZS_KB.
     uint32_t mine = 0;
     bool done = false;
+    if (post) {
+      // posting list: q's hash group walked back from q's rank, 64 positions a batch (back
+      // distances ascending); the batch in which the group or the window ends is the last
+      const uint32_t hq = lzs_hash(f);
+      const uint64_t lt = (1ull << lane) - 1;
+      for (int32_t i0 = (int32_t)PR[q] - 1; i0 >= 0 && !done; i0 -= 64) {
+        const int32_t i = i0 - lane;
+        const uint32_t e = i >= 0 ? PS[i] : 0u;
+        const uint32_t p = e & 0xffffu;
+        const bool inside = i >= 0 && (e >> 16) == hq && q - p <= bm;
+        const uint64_t inm = __ballot(inside);
+        const bool hit = inside && F[p] == f;
+        const uint64_t m = __ballot(hit);
+        if (hit) hl[__popcll(m & lt)] = (uint16_t)(q - p);
+        const uint32_t tot = (uint32_t)__popcll(m);
+        bool top = false;
+        for (uint32_t k = lane; k < tot; k += 64) {
+          const uint32_t b = hl[k], L = runl(q, b);
+          const uint32_t key = (L << 17) | (LZS_KB - b);
+          if (key > mine) mine = key;
+          top = top || L >= 259;
+        }
+        done = __ballot(top) != 0 || inm != ~0ull;
+      }
+      done = true;
+    }
     for (uint32_t g0 = 1; g0 <= bm && !done; g0 += 64 * LZS_HB) {
       if (g0 > 1) {
 #pragma unroll
@@ -1365,6 +1483,11 @@ __global__ __launch_bounds__(64) void k_tilebytes_s(EncodeJob j) {
 
 // ---------------------------------------------------------------- orchestration
 
+static int lzs_ring_max() {
+  static const int v = [] { const char* e = getenv("HOH_LZS_RING_MAX"); return e ? atoi(e) : 32768; }();
+  return v;
+}
+
 void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, void (*mark)(void*, const char*), void* mc) {
   const int dist = j.speed == 1 ? 10 : j.speed == 2 ? 11 : j.speed == 3 ? 12 : 14;   // choh.cpp:125-137
   const int limit = 1 << dist;
@@ -1388,9 +1511,12 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, v
     const int lring = mode == LZC_MAP ? 2 * NT : ring;
     const size_t lds = (size_t)(lring + (mode == LZC_TAB ? 3 * LZC_W : 0) + (mode != LZC_WALK ? 2 * LZC_C : 0)) * 4;
     hipLaunchKernelGGL(k_lzcand, dim3(j.ntiles), dim3(NT), lds, sl, j, limit, lring, mode, mw);
+    if (j.lzs) hipLaunchKernelGGL(k_lzsort, dim3(j.ntiles), dim3(LZSORT_T), 0, sl, j);
     int rp = 1;
     while (rp < limit + 324) rp <<= 1;
-    if (rp > 8192) rp = 0;                                            // -s4: pixels from the image
+    // -s4's 32768-position ring (128 KB: one workgroup per CU) pays once the posting lists cut the
+    // per-candidate scan; without them (or HOH_LZS_RING_MAX < 32768) -s4 reads pixels from the image
+    if (rp > lzs_ring_max() || (rp > 8192 && !j.lzs)) rp = 0;
     // -s1 (ring 2048): four segment walks per tile (four rings: two workgroups per CU); the larger
     // rings of -s2..-s4 keep one walk per tile
     const int nseg = rp && rp <= 2048 ? LZS_SEG : 1;

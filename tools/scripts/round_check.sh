@@ -4,6 +4,7 @@
 #   bench   the driver-shaped bench line (N = 1) and the N > 1 code path on a one-rank group
 #           (--sharded, with the configs[3] strong leg)
 #   ab      bench.py A/B of the variant libraries listed in $VARS (var/*.so, see mkvar.sh)
+#   nat     natural 8192^2 encodes at -s1..-s4 (one image at a time) + rocprofv3 kernel stats per speed
 # usage: round_check.sh OUTDIR stage...
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp
@@ -36,5 +37,12 @@ PY
         python3 -c "import json; d=json.load(open('$O/ab_${n}.json')); r=d['roofline']; print('$n', d['value'], r['avg_launch_ms'], r['avg_launch_ms_under_load'], d['detail']['bit_exact_vs_reference'], d['detail']['slot_files_bit_exact'])"
       done
       unset HOH_LIB ;;
+    nat)
+      for sp in 1 2 3 4; do
+        (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/nat$sp -o run \
+          -- python3 $GRAFT_REPO_ROOT/tools/scripts/natural_prof.py 8192 $sp 2) > $O/nat$sp.txt 2>&1 || { tail $O/nat$sp.txt; exit 1; }
+        grep "^natural" $O/nat$sp.txt
+        python3 tools/scripts/kstats.py $O/nat$sp 6 2>/dev/null || head -7 $O/nat$sp/run_kernel_stats.csv | cut -d, -f1-4
+      done ;;
   esac
 done
