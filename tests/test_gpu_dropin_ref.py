@@ -8,7 +8,8 @@ the flow of entropy_roundtrip_test.sh:1-11 and the layer round trip with those b
   * the drop-in encoder's stream must equal the reference encoder's (oracle/_ref, the reference
     binary built from the same source without the drop-ins) byte for byte;
   * the drop-in decoder must restore the input (cmp), from its own stream and the reference's;
-  * the reference decoder must read the drop-in's stream back too (one stream: Q1 does not bite);
+  * the reference decoder must read the drop-in's stream back too (one stream: Q1 does not bite),
+    except the single-symbol table it cannot read (Q6);
   * layer_roundtrip_test must print "Layer roundtrip: OK" and exit 0 through the GPU.
 The inputs are repository files (the reference encodes its own source text; that file is not
 kept here), plus byte patterns that reach the stored fallback and a single-symbol table (Q6)."""
@@ -64,7 +65,10 @@ def test_entropy_roundtrip_flow(tmp_path):
         r = _run([enc_r, f, str(cr)])
         assert r.returncode == 0, r.stdout + r.stderr
         assert cg.read_bytes() == cr.read_bytes(), f
-        for dec, c in ((dec_d, cg), (dec_d, cr), (dec_r, cg)):
+        # the reference decoder cannot read a single-symbol table (its frequency overflows the
+        # field): only the drop-in decoder reads that one back
+        pairs = ((dec_d, cg), (dec_d, cr)) + (((dec_r, cg),) if not f.endswith("one.bin") else ())
+        for dec, c in pairs:
             out = tmp_path / ("d%d" % i)
             r = _run([dec, str(c), str(out)])
             assert r.returncode == 0, r.stdout + r.stderr

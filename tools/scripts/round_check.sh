@@ -5,6 +5,8 @@
 #           (--sharded, with the configs[3] strong leg)
 #   ab      bench.py A/B of the variant libraries listed in $VARS (var/*.so, see mkvar.sh)
 #   nat     natural 8192^2 encodes at -s1..-s4 (one image at a time) + rocprofv3 kernel stats per speed
+#   pmc     rocprofv3 --pmc passes over bench.py --pmc-probe (one image encoded + decoded twice), one
+#           pass per ';'-separated counter set in $PMC_SETS (default: the SQ instruction / wait mix)
 # usage: round_check.sh OUTDIR stage...
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp
@@ -37,6 +39,16 @@ PY
         python3 -c "import json; d=json.load(open('$O/ab_${n}.json')); r=d['roofline']; print('$n', d['value'], r['avg_launch_ms'], r['avg_launch_ms_under_load'], d['detail']['bit_exact_vs_reference'], d['detail']['slot_files_bit_exact'])"
       done
       unset HOH_LIB ;;
+    pmc)
+      SETS=${PMC_SETS:-"SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_BRANCH SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_WAVES;SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_SALU SQ_LDS_IDX_ACTIVE"}
+      k=0
+      IFS=';' read -ra SA <<< "$SETS"
+      for set in "${SA[@]}"; do
+        k=$((k+1))
+        (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d $GRAFT_REPO_ROOT/$O/pmc$k -o p \
+          -- python3 $GRAFT_REPO_ROOT/bench.py --pmc-probe) > $O/pmc$k.log 2>&1 || { tail -5 $O/pmc$k.log; exit 1; }
+      done
+      python3 tools/scripts/pmc_summary2.py $O/pmc* > $O/pmc_summary.txt; cat $O/pmc_summary.txt ;;
     nat)
       for sp in 1 2 3 4; do
         (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/nat$sp -o run \
