@@ -5,6 +5,8 @@
 #           (--sharded, with the configs[3] strong leg)
 #   ab      bench.py A/B of the variant libraries listed in $VARS (var/*.so, see mkvar.sh)
 #   nat     natural 8192^2 encodes at -s1..-s4 (one image at a time) + rocprofv3 kernel stats per speed
+#   inflight  bench.py (100 steps) over images in flight x GPU_MAX_HW_QUEUES ($INFLIGHT: "D:Q ..."; Q 0 =
+#           one queue per image)
 #   pmc     rocprofv3 --pmc passes over bench.py --pmc-probe (one image encoded + decoded twice), one
 #           pass per ';'-separated counter set in $PMC_SETS (default: the SQ instruction / wait mix)
 # usage: round_check.sh OUTDIR stage...
@@ -39,6 +41,14 @@ PY
         python3 -c "import json; d=json.load(open('$O/ab_${n}.json')); r=d['roofline']; print('$n', d['value'], r['avg_launch_ms'], r['avg_launch_ms_under_load'], d['detail']['bit_exact_vs_reference'], d['detail']['slot_files_bit_exact'])"
       done
       unset HOH_LIB ;;
+    inflight)
+      B="--no-legs --no-pmc --no-cpu-baseline --no-config2"
+      for dq in ${INFLIGHT:-"16:0 20:0 24:0 28:0 32:0 24:16 24:20 32:16 32:20"}; do
+        d=${dq%:*}; q=${dq#*:}
+        timeout -k 10 200 python -u bench.py --steps 100 --warmup 5 --inflight $d --hw-queues $q $B > $O/if_${d}_${q}.json 2> $O/if_err \
+          || { tail $O/if_err; exit 1; }
+        python3 -c "import json; d=json.load(open('$O/if_${d}_${q}.json')); print('inflight $d queues $q', d['value'], d['detail']['latency_ms_enc'], d['detail']['latency_ms_dec'])"
+      done ;;
     pmc)
       SETS=${PMC_SETS:-"SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_BRANCH SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_WAVES;SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_SALU SQ_LDS_IDX_ACTIVE"}
       k=0
