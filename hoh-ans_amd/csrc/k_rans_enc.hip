@@ -69,42 +69,11 @@ struct Coder {
 __device__ __forceinline__ void flush_win(Coder& c) {
   uint32_t m = c.mask;
   const uint32_t shift = WIN - c.slot;
-#if defined(HOH_FLUSH2) || defined(HOH_FLUSH4)
-  // several words per LDS round trip: the reads of one pass are issued together and awaited once
-#ifdef HOH_FLUSH4
-  constexpr int FW = 4;
-#else
-  constexpr int FW = 2;
-#endif
-  while (m) {
-    uint32_t t[FW], v[FW];
-    uint32_t mm = m;
-#pragma unroll
-    for (int k = 0; k < FW; k++) {
-      t[k] = mm ? (uint32_t)__builtin_clz(mm) : t[0];            // no word left: re-read the first
-      mm &= ~(0x80000000u >> t[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < FW; k++) v[k] = c.win[t[k] - shift];
-#pragma unroll
-    for (int k = 0; k < FW; k++) asm volatile("" : "+v"(v[k]));   // all reads issued before any store
-    c.slab[--c.widx] = v[0];
-    m &= ~(0x80000000u >> t[0]);
-#pragma unroll
-    for (int k = 1; k < FW; k++) {
-      if (m) {
-        c.slab[--c.widx] = v[k];
-        m &= ~(0x80000000u >> t[k]);
-      }
-    }
-  }
-#else
   while (m) {
     const uint32_t t = __builtin_clz(m) - shift;
     c.slab[--c.widx] = c.win[t];
     m &= ~(0x80000000u >> (t + shift));
   }
-#endif
   c.mask = 0;
   c.slot = 0;
 }

@@ -795,12 +795,13 @@ __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring,
 // the same fingerprint as q and before it is in q's group, before q, in descending order when
 // walked back from q's rank -- so k_lzscan visits only equal-hash positions of q's window, back
 // distances ascending, instead of every fingerprint of the window (lz.hpp:32-50 at seek 11..14).
-// Two stable counting-sort passes (LSD, 8-bit digits) of pos | hash << 16 per tile, one 1024-thread
-// workgroup per tile: per 1024-position chunk, a wave ranks its lanes by digit with 8 ballots, the
-// 16 waves' per-digit counts are prefix-summed in LDS, and each position lands at its digit's base
-// + the counts of the waves before + its rank in its wave (stable).
+// Two stable counting-sort passes (LSD, 8-bit digits) of pos | hash << 16 per tile, one 256-thread
+// workgroup per tile (small, so it schedules beside the predictor search it overlaps): per
+// 256-position chunk, a wave ranks its lanes by digit with 8 ballots, the 4 waves' per-digit counts
+// are prefix-summed in LDS, and each position lands at its digit's base + the counts of the waves
+// before + its rank in its wave (stable).
 __device__ __forceinline__ uint32_t lzs_hash(uint32_t f) { return (f * 0x9E3779B1u) >> 16; }
-#define LZSORT_T 1024
+#define LZSORT_T 256
 __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
   __shared__ uint32_t base[256];
   __shared__ uint32_t cnt[LZSORT_T / 64][256];
@@ -1514,9 +1515,9 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, v
     if (j.lzs) hipLaunchKernelGGL(k_lzsort, dim3(j.ntiles), dim3(LZSORT_T), 0, sl, j);
     int rp = 1;
     while (rp < limit + 324) rp <<= 1;
-    // -s4's 32768-position ring (128 KB: one workgroup per CU) pays once the posting lists cut the
-    // per-candidate scan; without them (or HOH_LZS_RING_MAX < 32768) -s4 reads pixels from the image
-    if (rp > lzs_ring_max() || (rp > 8192 && !j.lzs)) rp = 0;
+    // -s4's 32768-position ring (128 KB: one workgroup per CU); HOH_LZS_RING_MAX < 32768 makes -s4
+    // read pixels from the image (round 3)
+    if (rp > lzs_ring_max()) rp = 0;
     // -s1 (ring 2048): four segment walks per tile (four rings: two workgroups per CU); the larger
     // rings of -s2..-s4 keep one walk per tile
     const int nseg = rp && rp <= 2048 ? LZS_SEG : 1;

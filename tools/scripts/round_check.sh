@@ -7,6 +7,10 @@
 #   nat     natural 8192^2 encodes at -s1..-s4 (one image at a time) + rocprofv3 kernel stats per speed
 #   inflight  bench.py (100 steps) over images in flight x GPU_MAX_HW_QUEUES ($INFLIGHT: "D:Q ..."; Q 0 =
 #           one queue per image)
+#   noix    no-index decode (synthetic + natural, one image at a time) and the no-index pipeline leg,
+#           once per environment setting in $NOIX_ENVS ("A=1,B=2 C=3 ..."; "-" = defaults)
+#   natab   natural 8192^2 encodes at the speeds in $NAT_SPEEDS once per setting in $NAT_ENVS
+#   trace   rocprofv3 --kernel-trace of a 40-step bench run (20 in flight): every dispatch's start / end
 #   pmc     rocprofv3 --pmc passes over bench.py --pmc-probe (one image encoded + decoded twice), one
 #           pass per ';'-separated counter set in $PMC_SETS (default: the SQ instruction / wait mix)
 # usage: round_check.sh OUTDIR stage...
@@ -26,7 +30,7 @@ for st in "$@"; do
       python3 - $O <<'PY'
 import json, sys
 for f in ("bench", "sharded"):
-    d = json.load(open(sys.argv[1] + "/%s.json" % f))
+    d = json.loads(open(sys.argv[1] + "/%s.json" % f).read().strip().splitlines()[-1])
     det = d["detail"]
     print(f, d["value"], {k: det.get(k) for k in ("bit_exact_vs_reference", "slot_files_bit_exact", "no_index_decode_MBps",
           "no_index_pipeline_MBps", "natural_s0_single_MBps", "strong_16384_MBps", "strong_16384_bit_exact_vs_reference")})
@@ -38,7 +42,7 @@ PY
         n=$(basename $v .so)
         if [ "$v" = base ]; then unset HOH_LIB; else export HOH_LIB=$GRAFT_REPO_ROOT/$v; fi
         timeout -k 10 200 python -u bench.py --steps 100 --warmup 5 $B > $O/ab_${n}.json 2> $O/ab_err || { tail $O/ab_err; exit 1; }
-        python3 -c "import json; d=json.load(open('$O/ab_${n}.json')); r=d['roofline']; print('$n', d['value'], r['avg_launch_ms'], r['avg_launch_ms_under_load'], d['detail']['bit_exact_vs_reference'], d['detail']['slot_files_bit_exact'])"
+        python3 -c "import json; d=json.loads(open('$O/ab_${n}.json').read().strip().splitlines()[-1]); r=d['roofline']; print('$n', d['value'], r['avg_launch_ms'], r['avg_launch_ms_under_load'], d['detail']['bit_exact_vs_reference'], d['detail']['slot_files_bit_exact'])"
       done
       unset HOH_LIB ;;
     inflight)
@@ -49,6 +53,30 @@ PY
           || { tail $O/if_err; exit 1; }
         python3 -c "import json; d=json.load(open('$O/if_${d}_${q}.json')); print('inflight $d queues $q', d['value'], d['detail']['latency_ms_enc'], d['detail']['latency_ms_dec'])"
       done ;;
+    noix)
+      for ev in ${NOIX_ENVS:-"-"}; do
+        E=""; [ "$ev" != "-" ] && E=$(echo $ev | tr ',' ' ')
+        for kind in synth natural; do
+          timeout -k 10 120 env $E python3 tools/scripts/noix_bench.py $kind 8192 5 > $O/noix.txt 2>&1 || { tail $O/noix.txt; exit 1; }
+          echo "[$ev] $(grep no-index $O/noix.txt | cut -c1-160)"
+        done
+        timeout -k 10 200 env $E python -u bench.py --steps 20 --warmup 5 --no-pmc --no-cpu-baseline --no-config2 > $O/noixb.json 2> $O/noixb.err \
+          || { tail $O/noixb.err; exit 1; }
+        python3 -c "import json; d=json.loads(open('$O/noixb.json').read().strip().splitlines()[-1])['detail']; print('[$ev] pipeline', d.get('no_index_pipeline_MBps'), d.get('no_index_pipeline_lossless'), 'single', d.get('no_index_decode_MBps'))"
+      done ;;
+    natab)
+      for ev in ${NAT_ENVS:-"-"}; do
+        E=""; [ "$ev" != "-" ] && E=$(echo $ev | tr ',' ' ')
+        for sp in ${NAT_SPEEDS:-"3 4"}; do
+          timeout -k 10 300 env $E python3 tools/scripts/natural_prof.py 8192 $sp 2 > $O/natab.txt 2>&1 || { tail $O/natab.txt; exit 1; }
+          echo "[$ev] $(grep ^natural $O/natab.txt)"
+        done
+      done ;;
+    trace)
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/$O/trace -o run \
+        -- python3 $GRAFT_REPO_ROOT/bench.py --steps 40 --warmup 5 --no-legs --no-pmc --no-cpu-baseline --no-config2) \
+        > $O/trace.log 2>&1 || { tail $O/trace.log; exit 1; }
+      ls -la $(find $O/trace -name "*kernel_trace.csv") ;;
     pmc)
       SETS=${PMC_SETS:-"SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_BRANCH SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_WAVES;SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_SALU SQ_LDS_IDX_ACTIVE"}
       k=0
