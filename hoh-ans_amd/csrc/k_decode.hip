@@ -1085,17 +1085,18 @@ __global__ __launch_bounds__(64) void k_drans_multi(DecJob j, const uint32_t* li
 // workgroup holds up to 64 chains (k_drans_multi's 12 KB per chain made a workgroup a whole CU's
 // LDS for 12 chains, 12 of 64 lanes busy, and one image's chains held every CU for 7 ms).
 // Per chain (P = symbols present, in cum order):
-//   B[b], b < 2^pb / 64: u16 index k0 of the symbol covering slot 64 b      (1 KB at prob_bits 15)
+//   B[b], b < 2^pb / 32: u16 index k0 of the symbol covering slot 32 b      (2 KB at prob_bits 15)
 //   E[k], k < P + 3:     {c | symbol << 16, f}, then three sentinels c = 0xffff
-// slot -> symbol: k0 = B[slot >> 6]; E[k0 .. k0 + 3] arrive in two ds_read2_b64; the covering
+// slot -> symbol: k0 = B[slot >> 5]; E[k0 .. k0 + 3] arrive in two ds_read2_b64; the covering
 // entry is the last of them whose start c <= slot -- exact while at most three symbols start in
-// (64 b, slot], i.e. everywhere but the rare-symbol tails, where the lane walks on entry by entry
-// (the sentinels end every walk).  Synthetic tiles (P ~ 30-55): ~1.5 KB per chain; the worst
-// case (P = 512) 5.1 KB.  Rounds are packed by table size: a workgroup claims the next list
+// (32 b, slot], i.e. everywhere but the rare-symbol tails, where the lane walks on entry by entry
+// (the sentinels end every walk; 64-slot buckets sent ~6 % of a synthetic stream's steps there,
+// which with tens of chain lanes per wave meant nearly every step).  Synthetic tiles (P ~ 30-55):
+// ~2.5 KB per chain; the worst case (P = 512) 6.1 KB.  Rounds are packed by table size: a workgroup claims the next list
 // entries whose tables fit its LDS budget (at most 64) with a CAS on a device head (gerr[10]), so
 // a round holds as many chains as fit and the grid (two workgroups per CU) keeps several images'
 // chains resident at once.
-#define DL_BSH 6
+#define DL_BSH 5
 #define DL_SCR 4096u             // abort word + list counts (payload rings below, [0, 4 KB))
 #define DL_TAB 4160u             // first table byte
 #define DL_HEAD 10               // gerr word: next list entry to claim
@@ -1126,13 +1127,15 @@ __global__ __launch_bounds__(64) void k_dlsize(DecJob j, uint32_t* tbytes) {
 __device__ __forceinline__ uint32_t dstep_l(uint32_t Bb, uint32_t Eb, uint32_t mask, uint32_t pb, uint32_t& xh,
                                            uint32_t& xl, uint32_t nw, uint32_t& wi) {
   const uint32_t slot = xl & mask;
-  const uint32_t k0 = lds_u16(Bb + ((slot >> DL_BSH) << 1));
+  const uint32_t k0 = lds_u16(Bb + (__builtin_amdgcn_ubfe(xl, DL_BSH, pb - DL_BSH) << 1));
   const uint32_t ea = Eb + (k0 << 3);
   const uint2 e0 = lds_u2(ea), e1 = lds_u2(ea + 8), e2 = lds_u2(ea + 16), e3 = lds_u2(ea + 24);
-  uint2 t = (e1.x & 0xffffu) <= slot ? e1 : e0;
-  t = (e2.x & 0xffffu) <= slot ? e2 : t;
-  if ((e3.x & 0xffffu) <= slot) {                            // four or more starts: walk on
-    t = e3;
+  // the three compares are independent; the starts ascend, so the last one <= slot wins
+  const bool s1 = (e1.x & 0xffffu) <= slot, s2 = (e2.x & 0xffffu) <= slot, s3 = (e3.x & 0xffffu) <= slot;
+  uint2 t = s1 ? e1 : e0;
+  t = s2 ? e2 : t;
+  t = s3 ? e3 : t;
+  if (s3) {                                                  // four or more starts: walk on (rare)
     for (uint32_t a = ea + 32;; a += 8) {
       const uint2 u = lds_u2(a);
       if ((u.x & 0xffffu) > slot) break;

@@ -27,6 +27,11 @@
 #include <atomic>
 
 #define WIN 32
+// lane row pitch of the LDS window in dwords: odd, so the 64 lanes' writes of one step fall in 64
+// different banks (a 32-dword pitch put every lane in one of two banks: a 32-way conflict per write)
+#ifndef WIN_PITCH
+#define WIN_PITCH (WIN + 1)
+#endif
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 
 // plane index -> stream: [0, na) through map a, then map b (e.g. the sub-green planes of every
@@ -200,7 +205,7 @@ __device__ __forceinline__ void rans_fast_body(const EncodeJob& j, int nplane, S
   c.xh = 0; c.xl = 1u << 31; c.mask = 0; c.slot = 0;
   c.slab = j.slabs + st.slab_off;
   c.widx = st.slab_cap;
-  c.win = (uint32_t*)(lds + threadIdx.x * WIN * 4);
+  c.win = (uint32_t*)(lds + threadIdx.x * WIN_PITCH * 4);
   Checkpoint* ck = j.ckpt ? j.ckpt + st.ckpt_off : nullptr;
   const uint16_t* sp = j.sym + st.sym_off;
   // prologue: the top n % 32 symbols one at a time (descending); the rest is whole windows
@@ -389,7 +394,7 @@ void launch_rans_fast(const EncodeJob& j, int nplane, hipStream_t s, SidMap a, i
   if (kind == 0)
     hipLaunchKernelGGL(k_rans_fast<0>, dim3(grid), dim3(64), chain_lds(), s, j, nplane, a, na, b, nblk, rot);
   else if (kind == 1)   // short or few chains (LZ / map streams, the ladder's winners): the window only
-    hipLaunchKernelGGL(k_rans_fast<1>, dim3(grid), dim3(64), WIN * 4 * 64, s, j, nplane, a, na, b, nblk, rot);
+    hipLaunchKernelGGL(k_rans_fast<1>, dim3(grid), dim3(64), WIN_PITCH * 4 * 64, s, j, nplane, a, na, b, nblk, rot);
   else   // size-only trial encodes: no window; one chain per SIMD (40 KB), all at once
     hipLaunchKernelGGL(k_rans_fast<2>, dim3(grid), dim3(64), 40 * 1024, s, j, nplane, a, na, b, nblk, rot);
 }
@@ -398,7 +403,7 @@ void launch_rans_fast_s(const EncodeJob& j, hipStream_t s, int np0, SidMap a0, i
                         int na2, int np1, SidMap a1, int na1) {
   const int nblk0 = (np0 + 63) / 64, nblk2 = (np2 + 63) / 64, nblk1 = (np1 + 63) / 64;
   if (nblk0 + nblk2 + nblk1 == 0) return;
-  static_assert(WIN * 4 * 64 <= 40 * 1024, "the window fits the 40 KB request");
+  static_assert(WIN_PITCH * 4 * 64 <= 40 * 1024, "the window fits the 40 KB request");
   hipLaunchKernelGGL(k_rans_fast_s, dim3(nblk0 + nblk2 + nblk1), dim3(64), 40 * 1024, s, j, np0, a0, na0, b0, nblk0,
                      np2, a2, na2, nblk2, np1, a1, na1, nblk1);
 }
