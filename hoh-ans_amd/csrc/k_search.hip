@@ -969,7 +969,22 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
         if (run < 16 || L >= lim) break;
       }
     } else {
-      while (L < lim && (rp ? pring[(q + L) & rmask] : tile_px(j, ti, q + L)) == tile_px(j, ti, q + L - b)) L++;
+      // backs beyond the ring (vertical ones past the window; every back at -s4 without a ring):
+      // the older side from the image, eight positions per round trip of loads
+      while (L < lim) {
+        uint32_t a[8], c[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const uint32_t p = min(q + L + (uint32_t)u, npix - 1);
+          a[u] = rp ? pring[p & rmask] : tile_px(j, ti, p);
+          c[u] = tile_px(j, ti, p - b);
+        }
+        uint32_t run = 8;
+#pragma unroll
+        for (int u = 7; u >= 0; u--) run = a[u] != c[u] ? (uint32_t)u : run;
+        L = min(L + run, lim);
+        if (run < 8) break;
+      }
     }
     return L;
   };
