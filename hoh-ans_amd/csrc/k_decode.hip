@@ -1085,21 +1085,23 @@ __global__ __launch_bounds__(64) void k_drans_multi(DecJob j, const uint32_t* li
 // workgroup holds up to 64 chains (k_drans_multi's 12 KB per chain made a workgroup a whole CU's
 // LDS for 12 chains, 12 of 64 lanes busy, and one image's chains held every CU for 7 ms).
 // Per chain (P = symbols present, in cum order):
-//   B[b], b < 2^pb / 32: u16 index k0 of the symbol covering slot 32 b      (2 KB at prob_bits 15)
+//   B[b], b < 2^pb / 64: u16 index k0 of the symbol covering slot 64 b      (1 KB at prob_bits 15)
 //   E[k], k < P + 3:     {c | symbol << 16, f}, then three sentinels c = 0xffff
-// slot -> symbol: k0 = B[slot >> 5]; E[k0 .. k0 + 3] arrive in two ds_read2_b64; the covering
+// slot -> symbol: k0 = B[slot >> 6]; E[k0 .. k0 + 3] arrive in two ds_read2_b64; the covering
 // entry is the last of them whose start c <= slot -- exact while at most three symbols start in
-// (32 b, slot], i.e. everywhere but the rare-symbol tails, where the lane walks on entry by entry
-// (the sentinels end every walk; 64-slot buckets sent ~6 % of a synthetic stream's steps there,
-// which with tens of chain lanes per wave meant nearly every step).  Synthetic tiles (P ~ 30-55):
-// ~2.5 KB per chain; the worst case (P = 512) 6.1 KB.  Rounds are packed by table size: a workgroup claims the next list
-// entries whose tables fit its LDS budget (at most 64) with a CAS on a device head (gerr[10]), so
-// a round holds as many chains as fit and the grid (two workgroups per CU) keeps several images'
-// chains resident at once.
-#define DL_BSH 5
+// (64 b, slot], i.e. everywhere but the rare-symbol tails, where the lane walks on entry by entry
+// (the sentinels end every walk).  Synthetic tiles (P ~ 30-55): ~1.5 KB per chain; the worst case
+// (P = 512) 5.1 KB.  (32-slot buckets walk less often but hold fewer chains per workgroup:
+// measured slower in the pipeline, no faster alone.)
+// Rounds are packed by table size before the launch (k_dlpack, one wave, greedy over the list in
+// order: a round is the next entries -- at most 64 -- whose tables fit the LDS budget), and
+// workgroup w takes rounds w, w + grid, ...: a round holds as many chains as fit and the grid keeps
+// several images' chains resident at once.  (A first version claimed rounds from a device head by
+// CAS at run time: hundreds of workgroups serialised on that one word before their first round.)
+#define DL_BSH 6
 #define DL_SCR 4096u             // abort word + list counts (payload rings below, [0, 4 KB))
 #define DL_TAB 4160u             // first table byte
-#define DL_HEAD 10               // gerr word: next list entry to claim
+#define DL_NR 10                 // gerr word: rounds packed by k_dlpack
 
 __host__ __device__ __forceinline__ uint32_t dl_nb(uint32_t pb) { return pb > DL_BSH ? 1u << (pb - DL_BSH) : 1u; }
 __host__ __device__ __forceinline__ uint32_t dl_bytes(uint32_t pb, uint32_t npres) {
@@ -1120,6 +1122,49 @@ __global__ __launch_bounds__(64) void k_dlsize(DecJob j, uint32_t* tbytes) {
   for (int e = 0; e < 8; e++) cnt += (8 * lane + e < d.range && cv[e + 1] > cv[e]) ? 1u : 0u;
   for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
   if (lane == 0) tbytes[sid] = dl_bytes(d.pb, cnt);
+}
+
+// Greedy round packing over the multi list in k_drans_lanes' order (long streams from the front,
+// short ones from the back): rounds[r] = first entry of round r, rounds[nr] = total, nr in
+// gerr[DL_NR].  One wave; the sizes are staged in LDS 8192 at a time, 64 entries per step.
+#define DLP_CH 8192
+__global__ __launch_bounds__(64) void k_dlpack(DecJob j, const uint32_t* list, int nlist, const uint32_t* tbytes,
+                                               uint32_t budget, uint32_t* rounds) {
+  __shared__ uint32_t sz[DLP_CH];
+  if (dec_abort(j)) return;
+  const int lane = threadIdx.x;
+  const uint32_t cl = *(volatile const uint32_t*)(j.gerr + 5), total = cl + *(volatile const uint32_t*)(j.gerr + 6);
+  auto entry = [&](uint32_t i) -> uint32_t { return i < cl ? list[i] : list[nlist - 1 - (i - cl)]; };
+  uint32_t nr = 0, p = 0;
+  for (uint32_t c0 = 0; c0 < total; c0 += DLP_CH) {
+    const uint32_t c1 = min(total, c0 + DLP_CH);
+    for (uint32_t i = c0 + lane; i < c1; i += 64) sz[i - c0] = min(tbytes[entry(i)], budget + 1);
+    __syncthreads();
+    // rounds that start inside this chunk (a round may run past its end: sizes there are re-read)
+    while (p < c1) {
+      const uint32_t i = p + (uint32_t)lane;
+      const uint32_t v = i < total ? (i < c1 ? sz[i - c0] : min(tbytes[entry(i)], budget + 1)) : budget + 1;
+      uint32_t incl = v;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(incl, o);
+        if (lane >= o) incl += u;
+      }
+      uint32_t n = (uint32_t)__popcll(__ballot(i < total && incl <= budget));
+      if (n == 0) {                                          // cannot happen: budget >= dl_bytes(15, 512)
+        if (lane == 0) atomicOr(j.gerr, 4u);
+        return;
+      }
+      if (lane == 0) rounds[nr] = p;
+      nr++;
+      p += n;
+    }
+    __syncthreads();
+  }
+  if (lane == 0) {
+    rounds[nr] = total;
+    j.gerr[DL_NR] = nr;
+  }
 }
 
 // one decode step on a compact table (B at byte Bb, E at byte Eb); returns the entry's low word
@@ -1156,50 +1201,30 @@ __device__ __forceinline__ uint32_t dstep_l(uint32_t Bb, uint32_t Eb, uint32_t m
 }
 
 __global__ __launch_bounds__(64) void k_drans_lanes(DecJob j, const uint32_t* list, int nlist, const uint32_t* tbytes,
-                                                    uint32_t budget) {
+                                                    uint32_t budget, const uint32_t* rounds) {
   extern __shared__ __attribute__((aligned(16))) uint32_t dm_lds[];
   const int lane = threadIdx.x;
   uint32_t* scr = dm_lds + DL_SCR / 4;
   if (lane == 0) {
     scr[0] = *(volatile const uint32_t*)j.gerr;
     scr[1] = *(volatile const uint32_t*)(j.gerr + 5);
-    scr[2] = *(volatile const uint32_t*)(j.gerr + 6);
+    scr[2] = *(volatile const uint32_t*)(j.gerr + DL_NR);
   }
   __syncthreads();
   if (scr[0]) return;
-  const uint32_t cl = scr[1], total = scr[1] + scr[2];
+  const uint32_t cl = scr[1], nr = scr[2];
   auto entry = [&](uint32_t i) -> uint32_t { return i < cl ? list[i] : list[nlist - 1 - (i - cl)]; };
-  for (;;) {
-    // claim a round: the next entries (at most 64) whose tables fit the budget
-    uint32_t p, n, tb = 0;
-    for (;;) {
-      p = 0;
-      if (lane == 0) p = __hip_atomic_load(j.gerr + DL_HEAD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      p = __shfl(p, 0);
-      if (p >= total) break;
-      const uint32_t i = p + (uint32_t)lane;
-      const uint32_t sz = i < total ? min(tbytes[entry(i)], budget + 1) : budget + 1;
-      uint32_t incl = sz;
+  for (uint32_t r = blockIdx.x; r < nr; r += gridDim.x) {
+    const uint32_t p = rounds[r], n = rounds[r + 1] - p;
+    // this lane's table: the exclusive prefix of the round's sizes (lane m <-> chain m)
+    const uint32_t sz = (uint32_t)lane < n ? tbytes[entry(p + lane)] : 0u;
+    uint32_t incl = sz;
 #pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t u = __shfl_up(incl, o);
-        if (lane >= o) incl += u;
-      }
-      n = (uint32_t)__popcll(__ballot(i < total && incl <= budget));
-      tb = DL_TAB + incl - sz;                              // this lane's table (lane m <-> chain m)
-      uint32_t won = 0;
-      if (lane == 0 && n) {
-        uint32_t exp = p;
-        won = __hip_atomic_compare_exchange_strong(j.gerr + DL_HEAD, &exp, p + n, __ATOMIC_RELAXED,
-                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 1u : 0u;
-      }
-      if (__shfl(won, 0)) break;
-      if (__shfl(n, 0) == 0) {                               // cannot happen: budget >= dl_bytes(15, 512)
-        if (lane == 0) atomicOr(j.gerr, 4u);
-        return;
-      }
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(incl, o);
+      if (lane >= o) incl += u;
     }
-    if (p >= total) break;
+    const uint32_t tb = DL_TAB + incl - sz;
     // tables of every chain of the round, the whole wave per stream
     for (uint32_t m = 0; m < n; m++) {
       const uint32_t sid = entry(p + m);
@@ -2502,9 +2527,10 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
     // every plane / LZ stream: a chain lane of k_drans_lanes (k_drans_multi with HOH_NOIX_MULTI=1);
     // anything else: k_drans_wave
     void* q2;
-    if ((e = dbuf(w, 13, (size_t)S * 8, &q2))) return e;
+    if ((e = dbuf(w, 13, (size_t)S * 12 + 8, &q2))) return e;
     uint32_t* mlist = (uint32_t*)q2;
     uint32_t* tbytes = mlist + S;
+    uint32_t* rounds = tbytes + S;                           // S + 1 words
     hipLaunchKernelGGL(k_dmlist, dim3((S + 255) / 256), dim3(256), 0, s, j, S, mlist);
     if (noix_multi()) {
       // one workgroup per CU (its LDS is a whole CU's), rounds of DM_MS streams per workgroup
@@ -2514,9 +2540,11 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
     } else {
       hipLaunchKernelGGL(k_dlsize, dim3(S), dim3(64), 0, s, j, tbytes);
       const uint32_t budget = dl_budget();
+      hipLaunchKernelGGL(k_dlpack, dim3(1), dim3(64), 0, s, j, (const uint32_t*)mlist, S, (const uint32_t*)tbytes, budget,
+                         rounds);
       const int grid = std::min(S, dl_wg_per_cu() * ctx_cus(c));
       hipLaunchKernelGGL(k_drans_lanes, dim3(grid), dim3(64), DL_TAB + budget, s, j, (const uint32_t*)mlist, S,
-                         (const uint32_t*)tbytes, budget);
+                         (const uint32_t*)tbytes, budget, (const uint32_t*)rounds);
     }
     hipLaunchKernelGGL(k_drans_wave, dim3(S), dim3(64), DL_SMEM, s, j, S, 1);
   }
