@@ -515,13 +515,17 @@ __global__ __launch_bounds__(NT) void k_front256(EncodeJob j) {
   // (rewritten after the chunk's checks) the largest lane, for the next chunk's lookups
   __shared__ uint32_t tpos[4][2][F2_TAB + 1];
   __shared__ uint32_t pring[4][F2_RING];
-  __shared__ uint32_t hist[3 * 512 - 256];
+#ifndef F2_HC
+#define F2_HC 1               // histogram copies (lane & (F2_HC - 1) picks one): fewer same-address atomics
+#endif
+  __shared__ uint32_t hist[F2_HC][3 * 512 - 256];
   __shared__ int s_notgrey, s_ncand;
   const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int gt = j.t0 + t;
   const int x0 = (gt % j.xt) * 256, y0 = (gt / j.xt) * 256;
   const uint32_t npix = 256u * 256u;
-  for (int i = tid; i < 3 * 512 - 256; i += NT) hist[i] = 0;
+  for (int i = tid; i < F2_HC * (3 * 512 - 256); i += NT) (&hist[0][0])[i] = 0;
+  uint32_t* hl = hist[lane & (F2_HC - 1)];
   for (int i = lane; i < 2 * (F2_TAB + 1); i += 64) tab[wv][i / (F2_TAB + 1)][i % (F2_TAB + 1)] = 0;
   for (int i = lane; i < 2 * (F2_TAB + 1); i += 64) tpos[wv][i / (F2_TAB + 1)][i % (F2_TAB + 1)] = 0;
   if (tid == 0) { s_notgrey = 0; s_ncand = 0; }
@@ -599,9 +603,9 @@ __global__ __launch_bounds__(NT) void k_front256(EncodeJob j) {
       res0[q] = (uint16_t)rg;
       res1[q] = (uint16_t)rr;
       res2[q] = (uint16_t)rb;
-      atomicAdd(&hist[rg], 1u);
-      atomicAdd(&hist[256 + rr], 1u);
-      atomicAdd(&hist[768 + rb], 1u);
+      atomicAdd(&hl[rg], 1u);
+      atomicAdd(&hl[256 + rr], 1u);
+      atomicAdd(&hl[768 + rb], 1u);
       if (!lz) continue;
       // the window q .. q+3 (the next chunk's first pixels for the last lanes)
       const uint32_t nx = k < 3 ? cur[k + 1] : nxt[0];
@@ -669,7 +673,10 @@ __global__ __launch_bounds__(NT) void k_front256(EncodeJob j) {
   __syncthreads();
   for (int i = tid; i < 3 * 512; i += NT) {
     const int k = i / 512, sv = i % 512;
-    j.hist[(size_t)(t * j.spt + med_kind(j, k)) * 512 + sv] = k == 0 ? (sv < 256 ? hist[sv] : 0u) : hist[k * 512 - 256 + sv];
+    uint32_t v = 0;
+#pragma unroll
+    for (int hc = 0; hc < F2_HC; hc++) v += k == 0 ? (sv < 256 ? hist[hc][sv] : 0u) : hist[hc][k * 512 - 256 + sv];
+    j.hist[(size_t)(t * j.spt + med_kind(j, k)) * 512 + sv] = v;
   }
   if (tid == 0) {
     TileInfo ti;

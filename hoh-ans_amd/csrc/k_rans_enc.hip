@@ -184,7 +184,10 @@ __device__ __forceinline__ void rans_fast_body(const EncodeJob& j, int nplane, S
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int lane = threadIdx.x;
   // the chain is the critical path of an image: win issue arbitration against co-resident waves
-  __builtin_amdgcn_s_setprio(3);
+#ifndef CHAIN_PRIO
+#define CHAIN_PRIO 3
+#endif
+  __builtin_amdgcn_s_setprio(CHAIN_PRIO);
   // f64 rounding toward zero (MODE.FP_ROUND[3:2] = 3) for step15's floor-by-fma, this wave only.
   // Set in asm so the compiler's mode tracking does not restore round-to-nearest before its own
   // f64 instructions: the only other f64 operations here are the exact 2^52 subtractions.
