@@ -12,7 +12,8 @@
 #   natab   natural 8192^2 encodes at the speeds in $NAT_SPEEDS once per setting in $NAT_ENVS
 #   trace   rocprofv3 --kernel-trace of a 40-step bench run (20 in flight): every dispatch's start / end
 #   pmc     rocprofv3 --pmc passes over bench.py --pmc-probe (one image encoded + decoded twice), one
-#           pass per ';'-separated counter set in $PMC_SETS (default: the SQ instruction / wait mix)
+#           pass per ';'-separated counter set in $PMC_SETS (default: the SQ instruction / wait mix);
+#           $PMC_PROG replaces the probe (e.g. "tools/scripts/natural_prof.py 8192 0 1")
 # usage: round_check.sh OUTDIR stage...
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp
@@ -84,7 +85,7 @@ PY
       for set in "${SA[@]}"; do
         k=$((k+1))
         (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d $GRAFT_REPO_ROOT/$O/pmc$k -o p \
-          -- python3 $GRAFT_REPO_ROOT/bench.py --pmc-probe) > $O/pmc$k.log 2>&1 || { tail -5 $O/pmc$k.log; exit 1; }
+          -- python3 $GRAFT_REPO_ROOT/${PMC_PROG:-bench.py --pmc-probe}) > $O/pmc$k.log 2>&1 || { tail -5 $O/pmc$k.log; exit 1; }
       done
       python3 tools/scripts/pmc_summary2.py $O/pmc* > $O/pmc_summary.txt; cat $O/pmc_summary.txt ;;
     nat)
