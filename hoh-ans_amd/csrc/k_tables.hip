@@ -239,44 +239,85 @@ __global__ __launch_bounds__(64) void k_tables(EncodeJob j, SidMap sm) {
     }
   }
   if (first == range) { first = 0; lastnz = range - 1; }
+  // The clamp scans (entropy_encoding.hpp:48-122), wave-parallel.  The serial scan only ever raises
+  // size_bits (0 -> 1 -> 4 -> 8 -> ...), so after symbol i it is level(max of the frequencies
+  // scanned so far), lower[idx] is the first symbol whose frequency reaches the idx-th raise's
+  // threshold (1, 2, 16, 256, ...), and the scan stops at the first symbol whose level reaches pb.
+  // Each 64-symbol chunk: a prefix max, the levels, one ballot for the stop and one per raise.
+  auto level = [&](uint32_t m) -> uint32_t {        // smallest of 0, 1, 4, 8, 12, ... with m < 2^s
+    const uint32_t bl = m ? 32u - __builtin_clz(m) : 0u;
+    return bl <= 1 ? bl : 4u * ((bl + 3) / 4);
+  };
+  auto nraise = [&](uint32_t sb) -> uint32_t { return sb == 0 ? 0u : sb == 1 ? 1u : sb / 4 + 1; };
+  auto thr = [&](uint32_t idx) -> uint32_t { return idx == 0 ? 1u : idx == 1 ? 2u : 1u << (4 * (idx - 1)); };
+  const uint32_t ncl = cn < 16 ? cn : 16u;
+  // one direction: dir = +1 from `from` up to range - 1, dir = -1 from `from` down to 0.  Returns
+  // the sum of the levels up to the stop (pb at the stop); sets the stop position (range / 0, as
+  // the serial loop leaves it, if the scan never stops), the final size_bits, the maximum
+  // frequency scanned (stop symbol included: it decides how many raises happened) and the first
+  // crossing of every raise threshold.
+  auto scan = [&](int dir, uint32_t from, uint32_t* cross, uint32_t& stop, uint32_t& sbf, uint32_t& mx) -> uint64_t {
+    uint64_t sum = 0;
+    uint32_t carry = 0, found = 0;
+    for (uint32_t c = 0;; c++) {
+      const int64_t ii = (int64_t)from + dir * (int64_t)(64 * c + lane);
+      const bool valid = ii >= 0 && ii < (int64_t)range;
+      if (!__ballot(valid)) break;
+      const uint32_t v = valid ? fr[(uint32_t)ii] : 0u;
+      uint32_t m = v;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(m, o);
+        if (lane >= o) m = max(m, u);
+      }
+      m = max(m, carry);
+      const uint32_t sl = level(m);
+#pragma unroll
+      for (uint32_t idx = 0; idx < 16; idx++) {              // constant indices: cross stays in registers
+        if (idx >= ncl || ((found >> idx) & 1)) continue;
+        const uint64_t b = __ballot(valid && v >= thr(idx));
+        if (b) {
+          cross[idx] = (uint32_t)((int64_t)from + dir * (int64_t)(64 * c + __builtin_ctzll(b)));
+          found |= 1u << idx;
+        }
+      }
+      const uint64_t hb = __ballot(valid && sl >= pb);
+      const uint32_t k = hb ? (uint32_t)__builtin_ctzll(hb) : 64u;
+      uint32_t part = valid && (uint32_t)lane < k ? sl : 0u;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+      sum += part;
+      if (hb) {
+        stop = (uint32_t)((int64_t)from + dir * (int64_t)(64 * c + k));
+        sum += pb;
+        sbf = pb;
+        mx = __shfl(m, (int)k);
+        return sum;
+      }
+      carry = __shfl(m, 63);
+    }
+    stop = dir > 0 ? range : 0u;
+    sbf = level(carry);
+    mx = carry;
+    return sum;
+  };
+  uint32_t lo_x[16] = {0}, up_x[16] = {0}, climb, climb2, sbf1, sbf2, mf, mb;
+  const uint64_t s1 = scan(1, first, lo_x, climb, sbf1, mf);
+  const uint64_t s2 = scan(-1, lastnz, up_x, climb2, sbf2, mb);
   if (lane == 0) {
     uint64_t exp_cl = (uint64_t)(uint32_t)((uint32_t)(2 * ((int)maxbits - 1)) * cn32);
     exp_cl += (uint64_t)(uint32_t)(pb * 2);
-    uint16_t lower[16], upper[16];
-    for (int i = 0; i < 16; i++) { lower[i] = 0; upper[i] = 0; }
-    uint64_t size_bits = 0, climb = first, lci = 0;
-    for (; climb < range; climb++) {
-      while ((uint64_t)fr[climb] >= (uint64_t)(1u << size_bits)) {
-        uint64_t idx;
-        if (size_bits == 0) { size_bits = 1; idx = 0; lci = 1; }
-        else if (size_bits == 1) { size_bits = 4; idx = 1; lci = 2; }
-        else { idx = size_bits / 4 + 1; size_bits += 4; lci++; }
-        if (idx < cn && idx < 16) lower[idx] = (uint16_t)climb;    // overrun write dropped (see oracle)
-      }
-      if (size_bits >= pb) { size_bits = pb; exp_cl += size_bits; break; }
-      exp_cl += size_bits;
+    exp_cl += s1 + s2;
+    const uint32_t nf = nraise(level(mf)), nb = nraise(level(mb));
+#pragma unroll
+    for (uint32_t i = 0; i < 16; i++) {
+      s_lower[i] = (uint16_t)(i < ncl ? (i < nf ? lo_x[i] : range - 1) : 0u);
+      s_upper[i] = (uint16_t)(i < ncl && i < nb ? up_x[i] : 0u);
     }
-    while (lci < cn && lci < 16) lower[lci++] = (uint16_t)(range - 1);
-    size_bits = 0;
-    uint64_t climb2 = lastnz, uci = 0;
-    for (;; climb2--) {
-      while ((uint64_t)fr[climb2] >= (uint64_t)(1u << size_bits)) {
-        uint64_t idx;
-        if (size_bits == 0) { size_bits = 1; idx = 0; uci = 1; }
-        else if (size_bits == 1) { size_bits = 4; idx = 1; uci = 2; }
-        else { idx = size_bits / 4 + 1; size_bits += 4; uci++; }
-        if (idx < cn && idx < 16) upper[idx] = (uint16_t)climb2;
-      }
-      if (size_bits >= pb) { size_bits = pb; exp_cl += size_bits; break; }
-      exp_cl += size_bits;
-      if (climb2 == 0) break;
-    }
-    while (uci < cn && uci < 16) upper[uci++] = 0;
-    exp_cl += size_bits * (climb2 - climb - 1);                          // size_t wrap (Q5)
+    exp_cl += (uint64_t)sbf2 * ((uint64_t)climb2 - (uint64_t)climb - 1);     // size_t wrap (Q5)
     exp_cl = (exp_cl + 8 - 1) / 8;
     const bool raw = expected_raw < exp_cl;
     hd[vlen] = (uint8_t)((1u << 7) + (pb << 2) + (raw ? 1 : 2));
-    for (int i = 0; i < 16; i++) { s_lower[i] = lower[i]; s_upper[i] = upper[i]; }
     s_mode = raw ? 1 : 2;
   }
   __syncthreads();
