@@ -892,7 +892,7 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
 // 64 positions at a time as the scan moves: each pixel read once per tile), sixteen positions per
 // LDS round trip; vertical backs beyond the ring read the image.  rp = ring size (0: -s4, whose
 // 16384-position window does not fit next to the other workgroups; pixels from the image).
-// nseg waves per tile (-s1: LZS_SEG; the larger rings of -s2..-s4 leave one): the tile's walk
+// nseg waves per tile (LZS_SEG, each with its own pixel ring): the tile's walk
 // is cut into segments walked at once and stitched by wave 0, exactly as k_lz does at -s0
 // (segment matches packed into lzspec as two words: pos | (len - 4) << 16, back).
 __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit, int rp, int nseg_req) {
@@ -932,6 +932,9 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
   uint32_t* pring = pring_all + (size_t)(wv < (int)nseg ? wv : 0) * (uint32_t)(rp + 16);
   uint16_t* hl = hl_all[wv];
   const uint32_t rmask = (uint32_t)rp - 1;
+  // backs the ring serves: it holds [wend - rp, wend) with wend < q + 260 + 64, so q - b .. is in
+  // it for b <= rp - 324 (and b <= limit); longer backs read the older side from the image
+  const uint32_t reach = rp ? min((uint32_t)limit, (uint32_t)rp - 324u) : 0u;
   uint32_t wend = 0;
   auto fill_to = [&](uint32_t lo, uint32_t need) {
     if (lo > wend) wend = lo & ~63u;
@@ -949,7 +952,7 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
   auto runl = [&](uint32_t q, uint32_t b) -> uint32_t {
     const uint32_t lim = min(259u, npix - q);
     uint32_t L = 0;
-    if (rp && b <= (uint32_t)limit) {
+    if (rp && b <= reach) {
       for (;;) {
         // sixteen positions per LDS round trip from two bases (the mirror spares every read its
         // wrap), the first unequal one by two select chains
@@ -1024,7 +1027,7 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
       const uint32_t k = 1 + 64 * c + lane;
       fw[c] = k <= kmax ? F[q - k * w] : 0u;
     }
-    if (rp) fill_to(q >= (uint32_t)limit ? q - (uint32_t)limit : 0u, q + 260);
+    if (rp) fill_to(q >= reach ? q - reach : 0u, q + 260);
     // horizontal: b = 1 .. min(limit, q), longest first, then the smallest b.  Each batch's hits
     // (equal fingerprints) are listed in LDS and measured 64 at a time; every hit is measured
     // (no stop at the first 259): the maximum key is the same, the smallest b of length 259
@@ -1500,7 +1503,11 @@ __global__ __launch_bounds__(64) void k_tilebytes_s(EncodeJob j) {
 // ---------------------------------------------------------------- orchestration
 
 static int lzs_ring_max() {
-  static const int v = [] { const char* e = getenv("HOH_LZS_RING_MAX"); return e ? atoi(e) : 32768; }();
+  static const int v = [] { const char* e = getenv("HOH_LZS_RING_MAX"); return e ? atoi(e) : 8192; }();
+  return v;
+}
+static int lzs_seg() {
+  static const int v = [] { const char* e = getenv("HOH_LZS_SEG"); const int n = e ? atoi(e) : LZS_SEG; return n < 1 ? 1 : n > LZS_SEG ? LZS_SEG : n; }();
   return v;
 }
 
@@ -1530,12 +1537,13 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, v
     if (j.lzs) hipLaunchKernelGGL(k_lzsort, dim3(j.ntiles), dim3(LZSORT_T), 0, sl, j);
     int rp = 1;
     while (rp < limit + 324) rp <<= 1;
-    // -s4's 32768-position ring (128 KB: one workgroup per CU); HOH_LZS_RING_MAX < 32768 makes -s4
-    // read pixels from the image (round 3)
-    if (rp > lzs_ring_max()) rp = 0;
-    // -s1 (ring 2048): four segment walks per tile (four rings: two workgroups per CU); the larger
-    // rings of -s2..-s4 keep one walk per tile
-    const int nseg = rp && rp <= 2048 ? LZS_SEG : 1;
+    // Four segment walks per tile (stitched as in k_lz), each with a pixel ring of up to 8192
+    // positions (4 x 32 KB + the static 24 KB: one workgroup per CU at -s3/-s4); the ring serves
+    // backs up to rp - 324, the rest (-s4's backs of 7869..16384, vertical ones) read the image.
+    // HOH_LZS_RING_MAX / HOH_LZS_SEG override (measurement).
+    if (rp > lzs_ring_max()) rp = lzs_ring_max();
+    if (rp < 1024) rp = 0;
+    const int nseg = rp ? lzs_seg() : 1;
     hipLaunchKernelGGL(k_lzscan, dim3(j.ntiles), dim3(64 * LZS_SEG), (size_t)nseg * (rp ? rp + 16 : 1) * 4, sl, j, limit,
                        rp, nseg);
   }
