@@ -552,6 +552,18 @@ def golden_bench_shas(W, H, noise):
 STRONG_SIDE, STRONG_SEED = 16384, 2     # configs[3]; seed 2 is the reference choh's golden file
 
 
+HW_QUEUE_CAP = 20
+
+
+def hw_queues_for(d):
+    """Hardware queues for d images in flight: d up to HW_QUEUE_CAP, else the fewest images per
+    queue that fit the cap, spread evenly (24 -> 12 queues of 2, 32 -> 16 of 2, 40 -> 20 of 2)."""
+    if d <= HW_QUEUE_CAP:
+        return max(1, d)
+    per = -(-d // HW_QUEUE_CAP)
+    return -(-d // per)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -565,7 +577,7 @@ def main():
     ap.add_argument("--noise", type=int, default=4)
     ap.add_argument("--inflight", type=int, default=20, help="images in flight per GPU (1 = one at a time)")
     ap.add_argument("--hw-queues", type=int, default=0,
-                    help="GPU_MAX_HW_QUEUES for this process (default: one per in-flight image, at most 32)")
+                    help="GPU_MAX_HW_QUEUES for this process (default: hw_queues_for(--inflight), at most 20)")
     ap.add_argument("--strong-inflight", type=int, default=8, help="images in flight per GPU in the 16384^2 leg")
     ap.add_argument("--no-index", action="store_true", help="decode without the side index (serial rANS)")
     ap.add_argument("--cpu-tiles", type=int, default=512)
@@ -605,15 +617,13 @@ def main():
         else:
             pmc, pmc_note = pmc_traffic_live(args)
 
-    # one hardware queue per in-flight image (HIP reads this at runtime init; <= 32 allowed here)
-    try:
-        q = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
-    except ValueError:
-        q = 4
+    # hardware queues (HIP reads this at runtime init): one per in-flight image up to HW_QUEUE_CAP;
+    # past that the images share queues evenly ("in-flight sweep": more than ~20 queues
+    # per process cost 15-30% of the throughput, however many images they carry)
     if args.hw_queues > 0:
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, args.hw_queues))
-    elif q < D:
-        os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, D))
+    else:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(hw_queues_for(D))
 
     import torch
     import hoh_ans

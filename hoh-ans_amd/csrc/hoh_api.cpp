@@ -14,6 +14,7 @@
 #include <stdio.h>
 #include <string>
 #include <atomic>
+#include <atomic>
 
 void launch_synth(uint8_t* rgb, int W, int H, int y0, uint64_t seed, int noise, hipStream_t s);
 void launch_natural(uint8_t* rgb, int W, int rows, int y0, uint64_t seed, hipStream_t s);
@@ -64,7 +65,7 @@ struct hoh_ctx {
   hipStream_t own = nullptr;
   SideStream side;              // -s>=1: the LZ screen beside the predictor search (created on first use)
   Buf idx8, fpb, pinfo, lg;     // -s>=1 workspaces
-  Buf lzs;                      // -s>=2: LZ posting lists (k_lzsort): sorted + ping-pong + ranks
+  Buf lzs;                      // -s>=2: LZ posting lists (k_lzsort): sorted positions + ping-pong (then the sorted fingerprints) + ranks
   uint32_t lg_key[4] = {0, 0, 0, 0};
   uint64_t lg_off[4] = {0, 0, 0, 0};
   Buf sym, hist, candbits, matches, lzspec, pal, streams, tiles, hdr, tab_fast, tab_gen, slabs, ckpt, misc, tsizes;
@@ -153,6 +154,16 @@ int hoh_ctx_create(hoh_ctx** out, int device) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) return HOH_E_NODEV;
   if (hipSetDevice(device) != hipSuccess) return HOH_E_NODEV;
+  {
+    // More hardware queues than ~20 per process oversubscribe the device's queue slots: measured
+    // -15% at 24 and -28% at 28 images in flight, each on its own queue (in-flight
+    // sweep).  HIP reads the variable once, before this library can act on it, so say it once.
+    static std::atomic<int> warned{0};
+    const char* q = getenv("GPU_MAX_HW_QUEUES");
+    if (q && atoi(q) > 20 && !getenv("HOH_QUIET") && !warned.exchange(1))
+      fprintf(stderr, "hoh: GPU_MAX_HW_QUEUES=%s: more than 20 hardware queues per process cost 15-30%% "
+                      "throughput on MI355X; share queues between streams instead\n", q);
+  }
   hoh_ctx* c = new hoh_ctx();
   c->device = device;
   if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || c->cus <= 0)

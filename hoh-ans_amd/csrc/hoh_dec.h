@@ -36,9 +36,13 @@ struct DecTile {
 struct DecWork {
   void* bufs[16] = {nullptr};
   size_t sizes[16] = {0};
+  hipEvent_t noix_ev = nullptr;   // recorded after this context's last no-index chain kernel
+  int noix_dev = -1;              // device it is registered on (k_decode.hip, noix_busy)
+  int64_t noix_t = 0;             // host time (steady clock, us) of its last no-index decode
 };
 
 void dec_free(DecWork& w);
+void noix_release(DecWork& w);
 int index_capture(hoh_index* idx, const EncodeJob& j, hipStream_t s);
 int index_reserve(hoh_index* idx, size_t nstreams, size_t nck);
 Checkpoint* index_ckpt_buf(hoh_index* idx);

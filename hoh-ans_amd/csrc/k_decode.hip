@@ -22,6 +22,8 @@
 
 extern std::atomic<uint64_t> g_device_allocs;   // hoh_api.cpp
 #include <vector>
+#include <mutex>
+#include <chrono>
 #include <stdio.h>
 
 #define DSEG HOH_SEG
@@ -2456,23 +2458,71 @@ static int noix_wave() {
   return v;
 }
 
-// HOH_NOIX_MULTI=1: no-index decodes with k_drans_multi (12 chains per CU, round 3) instead of k_drans_lanes
+// No-index chain kernel choice.  k_drans_multi (12 chains per CU, full tables) has the shorter
+// step (~260 cycles against k_drans_lanes' ~400) but holds a whole CU per 12 chains; k_drans_lanes
+// packs up to 64 chains per workgroup into compact tables and fills the device when several
+// decodes run at once.  So a decode that has the device to itself takes k_drans_multi, one that
+// finds another context's no-index chain kernel still in flight takes k_drans_lanes.
+// HOH_NOIX_MULTI=1 / 0 pins the choice (k_drans_multi / k_drans_lanes); unset: adaptive.
 static int noix_multi() {
-  static const int v = [] { const char* e = getenv("HOH_NOIX_MULTI"); return e ? atoi(e) : 0; }();
+  static const int v = [] { const char* e = getenv("HOH_NOIX_MULTI"); return e ? atoi(e) : -1; }();
   return v;
+}
+
+// Contexts' completion events per device, to count the no-index decodes in flight beside this one.
+static std::mutex g_noix_mu;
+static std::vector<DecWork*> g_noix;
+
+void noix_release(DecWork& w) {
+  if (!w.noix_ev) return;
+  {
+    std::lock_guard<std::mutex> g(g_noix_mu);
+    g_noix.erase(std::remove(g_noix.begin(), g_noix.end(), &w), g_noix.end());
+  }
+  (void)hipEventDestroy(w.noix_ev);
+  w.noix_ev = nullptr;
+  w.noix_dev = -1;
+}
+
+// HOH_NOIX_WINDOW_MS: another context's no-index decode issued this recently counts as
+// concurrent traffic even when its chain kernel has finished (a pipeline's decodes leave gaps
+// between kernels; one k_drans_multi among them takes every CU's LDS for its 7 ms)
+static int64_t noix_window_us() {
+  static const int64_t v = [] { const char* e = getenv("HOH_NOIX_WINDOW_MS"); return (int64_t)(e ? atof(e) * 1000 : 20000); }();
+  return v;
+}
+
+// 1 if another context on this device issued a no-index decode within the window or its chain
+// kernel has not finished (hipEventQuery only: nothing waits); registers w on first use and stamps
+// its issue time.  A failure to create the event reads as busy.
+static int noix_busy(DecWork& w, int dev) {
+  const int64_t now = std::chrono::duration_cast<std::chrono::microseconds>(
+                          std::chrono::steady_clock::now().time_since_epoch()).count();
+  if (!w.noix_ev) {
+    if (hipEventCreateWithFlags(&w.noix_ev, hipEventDisableTiming) != hipSuccess) { w.noix_ev = nullptr; return 1; }
+    w.noix_dev = dev;
+    std::lock_guard<std::mutex> g(g_noix_mu);
+    g_noix.push_back(&w);
+  }
+  std::lock_guard<std::mutex> g(g_noix_mu);
+  w.noix_t = now;
+  for (DecWork* o : g_noix)
+    if (o != &w && o->noix_dev == dev &&
+        (now - o->noix_t < noix_window_us() || hipEventQuery(o->noix_ev) == hipErrorNotReady)) return 1;
+  return 0;
 }
 // k_drans_lanes: LDS table budget per workgroup (HOH_DL_BUDGET_KB, >= the 5.1 KB worst-case table)
 // and workgroups per CU (HOH_DL_WG)
 static uint32_t dl_budget() {
   static const uint32_t v = [] {
     const char* e = getenv("HOH_DL_BUDGET_KB");
-    const uint32_t kb = e ? (uint32_t)atoi(e) : 56u;
+    const uint32_t kb = e ? (uint32_t)atoi(e) : 20u;
     return std::max<uint32_t>(std::min<uint32_t>(kb, 150u) * 1024u, dl_bytes(15, 512));
   }();
   return v;
 }
 static int dl_wg_per_cu() {
-  static const int v = [] { const char* e = getenv("HOH_DL_WG"); return e ? std::max(1, atoi(e)) : 2; }();
+  static const int v = [] { const char* e = getenv("HOH_DL_WG"); return e ? std::max(1, atoi(e)) : 4; }();
   return v;
 }
 
@@ -2524,7 +2574,7 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   } else if (noix_wave()) {                                   // the one-wave-per-stream decoder alone
     hipLaunchKernelGGL(k_drans_wave, dim3(S), dim3(64), DL_SMEM, s, j, S, 0);
   } else {
-    // every plane / LZ stream: a chain lane of k_drans_lanes (k_drans_multi with HOH_NOIX_MULTI=1);
+    // every plane / LZ stream: a chain lane of k_drans_multi or k_drans_lanes (noix_multi above);
     // anything else: k_drans_wave
     void* q2;
     if ((e = dbuf(w, 13, (size_t)S * 12 + 8, &q2))) return e;
@@ -2532,7 +2582,9 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
     uint32_t* tbytes = mlist + S;
     uint32_t* rounds = tbytes + S;                           // S + 1 words
     hipLaunchKernelGGL(k_dmlist, dim3((S + 255) / 256), dim3(256), 0, s, j, S, mlist);
-    if (noix_multi()) {
+    const int pin = noix_multi();
+    const bool multi = pin >= 0 ? pin != 0 : !noix_busy(w, ctx_device(c));
+    if (multi) {
       // one workgroup per CU (its LDS is a whole CU's), rounds of DM_MS streams per workgroup
       const int nmax = std::min(S, 6 * j.ntiles);
       const int grid = std::min((nmax + DM_MS - 1) / DM_MS, ctx_cus(c));
@@ -2546,6 +2598,7 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
       hipLaunchKernelGGL(k_drans_lanes, dim3(grid), dim3(64), DL_TAB + budget, s, j, (const uint32_t*)mlist, S,
                          (const uint32_t*)tbytes, budget, (const uint32_t*)rounds);
     }
+    if (w.noix_ev) (void)hipEventRecord(w.noix_ev, s);
     hipLaunchKernelGGL(k_drans_wave, dim3(S), dim3(64), DL_SMEM, s, j, S, 1);
   }
   ctx_mark(c, s, "drans", false);

@@ -518,13 +518,16 @@ __global__ __launch_bounds__(NT) void k_front256(EncodeJob j) {
 #ifndef F2_HC
 #define F2_HC 1               // histogram copies (lane & (F2_HC - 1) picks one): fewer same-address atomics
 #endif
-  __shared__ uint32_t hist[F2_HC][3 * 512 - 256];
+#ifndef F2_AGG
+#define F2_AGG 0              // 1: wave-aggregated histogram adds for lane 0's bin (+ 64 spare words)
+#endif
+  __shared__ uint32_t hist[F2_HC][3 * 512 - 256 + 64 * F2_AGG];
   __shared__ int s_notgrey, s_ncand;
   const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int gt = j.t0 + t;
   const int x0 = (gt % j.xt) * 256, y0 = (gt / j.xt) * 256;
   const uint32_t npix = 256u * 256u;
-  for (int i = tid; i < F2_HC * (3 * 512 - 256); i += NT) (&hist[0][0])[i] = 0;
+  for (int i = tid; i < F2_HC * (3 * 512 - 256 + 64 * F2_AGG); i += NT) (&hist[0][0])[i] = 0;
   uint32_t* hl = hist[lane & (F2_HC - 1)];
   for (int i = lane; i < 2 * (F2_TAB + 1); i += 64) tab[wv][i / (F2_TAB + 1)][i % (F2_TAB + 1)] = 0;
   for (int i = lane; i < 2 * (F2_TAB + 1); i += 64) tpos[wv][i / (F2_TAB + 1)][i % (F2_TAB + 1)] = 0;
@@ -603,9 +606,23 @@ __global__ __launch_bounds__(NT) void k_front256(EncodeJob j) {
       res0[q] = (uint16_t)rg;
       res1[q] = (uint16_t)rr;
       res2[q] = (uint16_t)rb;
+#if F2_AGG
+      // lanes holding lane 0's bin add once, through lane 0 (smooth tiles put most of a chunk on
+      // one bin, and same-address LDS atomics serialise); the others' adds of 0 go to spare words
+      auto hadd = [&](uint32_t i) {
+        const uint32_t i0 = __builtin_amdgcn_readfirstlane(i);
+        const uint32_t n0 = (uint32_t)__popcll(__ballot(i == i0));
+        const bool dup = i == i0 && lane != 0;
+        atomicAdd(&hl[dup ? 3 * 512 - 256 + lane : i], lane == 0 ? n0 : dup ? 0u : 1u);
+      };
+      hadd(rg);
+      hadd(256 + rr);
+      hadd(768 + rb);
+#else
       atomicAdd(&hl[rg], 1u);
       atomicAdd(&hl[256 + rr], 1u);
       atomicAdd(&hl[768 + rb], 1u);
+#endif
       if (!lz) continue;
       // the window q .. q+3 (the next chunk's first pixels for the last lanes)
       const uint32_t nx = k < 3 ? cur[k + 1] : nxt[0];
@@ -619,8 +636,25 @@ __global__ __launch_bounds__(NT) void k_front256(EncodeJob j) {
       uint32_t* pc = tpos[wv][cb];
       const uint32_t* tp = tab[wv][cb ^ 1];
       const uint32_t* pp = tpos[wv][cb ^ 1];
+#if F2_AGG
+      // lanes holding lane 0's key leave the table work to lane 0 (flat runs give most of a chunk
+      // one key, and same-address LDS atomics serialise): lane 0's min lane is itself, and it writes
+      // the group's max lane for the next chunk
+      const uint32_t h0 = __builtin_amdgcn_readfirstlane(hq);
+      const uint64_t m0 = __ballot(hq == h0);
+      const bool kdup = hq == h0 && lane != 0;
+      uint32_t sq = hq && !kdup ? wt_put(tc, hq) : F2_TAB;
+      {
+        const uint32_t s0 = __builtin_amdgcn_readfirstlane(sq);
+        if (kdup) sq = s0;
+      }
+      if (sq < F2_TAB && !kdup) wt_max(pc, sq, 63u - lane);
+#else
       const uint32_t sq = hq ? wt_put(tc, hq) : F2_TAB;
+      const bool kdup = false;
+      const uint64_t m0 = 1;
       if (sq < F2_TAB) wt_max(pc, sq, 63u - lane);
+#endif
       const uint32_t sp = hq ? wt_find(tp, hq) : F2_TAB;
       // Equal windows have equal fingerprints, so the windows before q equal to q's can only be
       // at the positions holding hq: in this chunk at lanes min..lane-1 (the earliest is checked),
@@ -654,14 +688,14 @@ __global__ __launch_bounds__(NT) void k_front256(EncodeJob j) {
       }
       // this chunk's words turn into the largest lane for the next chunk's lookups (program order
       // on one address: the fcur reads above come first)
-      if (sq < F2_TAB) { pc[sq] = 0; wt_max(pc, sq, lane); }
+      if (sq < F2_TAB && !kdup) { pc[sq] = 0; wt_max(pc, sq, lane ? (uint32_t)lane : 63u - (uint32_t)__builtin_clzll(m0)); }
       if (lane == 0) cand[q >> 6] = word;
       ncand += lane == 0 ? __popcll(word) : 0;
       // empty the previous chunk's table for the next chunk (wave-ordered: every lookup is done)
       uint32_t* tpw = tab[wv][cb ^ 1];
       tpw[slot_prev] = 0;                             // slot F2_TAB is a spare: no branch
       tpos[wv][cb ^ 1][slot_prev] = 0;
-      slot_prev = sq;
+      slot_prev = kdup ? F2_TAB : sq;
       cb ^= 1;
     }
 #pragma unroll

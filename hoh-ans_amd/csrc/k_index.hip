@@ -23,6 +23,7 @@ void launch_index_capture(const EncodeJob& j, IndexStream* is, size_t per, hipSt
 }
 
 void dec_free(DecWork& w) {
+  noix_release(w);
   for (int i = 0; i < 16; i++) {
     if (w.bufs[i]) (void)hipFree(w.bufs[i]);
     w.bufs[i] = nullptr;

@@ -878,6 +878,9 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
     }
     __syncthreads();
   }
+  // the fingerprints in sorted order, over the ping-pong half (free now): k_lzscan's hit test reads
+  // them coalesced beside the positions instead of gathering F[p] after them
+  for (uint32_t i = tid; i < n; i += LZSORT_T) T[i] = F[S[i] & 0xffffu];
 }
 
 #define LZS_KB 0x1ffffu      // k_lzscan keys: (L << 17) | (LZS_KB - b)
@@ -895,11 +898,12 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
 // nseg waves per tile (LZS_SEG, each with its own pixel ring): the tile's walk
 // is cut into segments walked at once and stitched by wave 0, exactly as k_lz does at -s0
 // (segment matches packed into lzspec as two words: pos | (len - 4) << 16, back).
-__global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit, int rp, int nseg_req) {
-  extern __shared__ uint32_t pring_all[];                              // nseg rings of rp + 16
+__global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit, int rp, int nseg_req, int hls) {
+  // dynamic LDS: nseg rings of rp + 16 positions, then nseg hit lists of hls entries (a batch's
+  // hits: 64 with posting lists, LZS_HB * 64 for the window walk)
+  extern __shared__ uint32_t pring_all[];
   __shared__ uint64_t cb[LZS_BITS];
   __shared__ uint32_t vis[2 * LZS_BITS];                               // visited candidates
-  __shared__ uint16_t hl_all[LZS_SEG][LZS_HB * 64];                    // a batch's hit list per wave
   __shared__ uint32_t s_cnt[LZS_SEG], s_exit[LZS_SEG];
   const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const TileInfo ti = j.tiles[t];
@@ -918,6 +922,7 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
   const bool post = j.lzs != nullptr;                                  // posting lists (k_lzsort)
   const uint32_t* PS = post ? j.lzs + (size_t)t * j.npix_cap : nullptr;
   const uint16_t* PR = post ? j.lzrank + (size_t)t * j.npix_cap : nullptr;
+  const uint32_t* PF = post ? j.lzs + (size_t)j.ntiles * j.npix_cap + (size_t)t * j.npix_cap : nullptr;
   const bool lds_bits = nwords <= LZS_BITS;
   const uint32_t nseg = (lds_bits && rp && nwords >= 4 * LZS_SEG && nseg_req > 1) ? (uint32_t)nseg_req : 1u;
   const uint32_t segcap = j.lz_cap / LZS_SEG;
@@ -930,7 +935,7 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
   }
   __syncthreads();
   uint32_t* pring = pring_all + (size_t)(wv < (int)nseg ? wv : 0) * (uint32_t)(rp + 16);
-  uint16_t* hl = hl_all[wv];
+  uint16_t* hl = (uint16_t*)(pring_all + (size_t)nseg_req * (rp ? rp + 16 : 1)) + (size_t)(wv < (int)nseg ? wv : 0) * hls;
   const uint32_t rmask = (uint32_t)rp - 1;
   // backs the ring serves: it holds [wend - rp, wend) with wend < q + 260 + 64, so q - b .. is in
   // it for b <= rp - 324 (and b <= limit); longer backs read the older side from the image
@@ -1042,11 +1047,11 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
       const uint64_t lt = (1ull << lane) - 1;
       for (int32_t i0 = (int32_t)PR[q] - 1; i0 >= 0 && !done; i0 -= 64) {
         const int32_t i = i0 - lane;
-        const uint32_t e = i >= 0 ? PS[i] : 0u;
+        const uint32_t e = i >= 0 ? PS[i] : 0u, fe = i >= 0 ? PF[i] : ~f;
         const uint32_t p = e & 0xffffu;
         const bool inside = i >= 0 && (e >> 16) == hq && q - p <= bm;
         const uint64_t inm = __ballot(inside);
-        const bool hit = inside && F[p] == f;
+        const bool hit = inside && fe == f;
         const uint64_t m = __ballot(hit);
         if (hit) hl[__popcll(m & lt)] = (uint16_t)(q - p);
         const uint32_t tot = (uint32_t)__popcll(m);
@@ -1503,7 +1508,7 @@ __global__ __launch_bounds__(64) void k_tilebytes_s(EncodeJob j) {
 // ---------------------------------------------------------------- orchestration
 
 static int lzs_ring_max() {
-  static const int v = [] { const char* e = getenv("HOH_LZS_RING_MAX"); return e ? atoi(e) : 8192; }();
+  static const int v = [] { const char* e = getenv("HOH_LZS_RING_MAX"); return e ? atoi(e) : 2048; }();
   return v;
 }
 static int lzs_seg() {
@@ -1537,15 +1542,18 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, v
     if (j.lzs) hipLaunchKernelGGL(k_lzsort, dim3(j.ntiles), dim3(LZSORT_T), 0, sl, j);
     int rp = 1;
     while (rp < limit + 324) rp <<= 1;
-    // Four segment walks per tile (stitched as in k_lz), each with a pixel ring of up to 8192
-    // positions (4 x 32 KB + the static 24 KB: one workgroup per CU at -s3/-s4); the ring serves
-    // backs up to rp - 324, the rest (-s4's backs of 7869..16384, vertical ones) read the image.
+    // Four segment walks per tile (stitched as in k_lz), each with a pixel ring of up to
+    // lzs_ring_max() positions; the ring serves backs up to rp - 324, the rest (long backs of
+    // -s3/-s4, vertical ones) read the image.  The scan waits on its loads, so workgroups per CU
+    // (LDS) count for more than the ring's reach: at -s4 rings of 8192 positions (one workgroup
+    // per CU) took 185 ms per natural 8192^2 encode, 2048 (three) 166 ms.
     // HOH_LZS_RING_MAX / HOH_LZS_SEG override (measurement).
     if (rp > lzs_ring_max()) rp = lzs_ring_max();
     if (rp < 1024) rp = 0;
     const int nseg = rp ? lzs_seg() : 1;
-    hipLaunchKernelGGL(k_lzscan, dim3(j.ntiles), dim3(64 * LZS_SEG), (size_t)nseg * (rp ? rp + 16 : 1) * 4, sl, j, limit,
-                       rp, nseg);
+    const int hls = j.lzs ? 64 : LZS_HB * 64;
+    const size_t dyn = (size_t)nseg * (rp ? rp + 16 : 1) * 4 + (size_t)nseg * hls * 2;
+    hipLaunchKernelGGL(k_lzscan, dim3(j.ntiles), dim3(64 * LZS_SEG), dyn, sl, j, limit, rp, nseg, hls);
   }
   // the join: if its record fails, s waits for the whole side stream instead
   const bool joined = fork && hipEventRecord(side.join, sl) == hipSuccess;

@@ -4,9 +4,10 @@
 #   bench   the driver-shaped bench line (N = 1) and the N > 1 code path on a one-rank group
 #           (--sharded, with the configs[3] strong leg)
 #   ab      bench.py A/B of the variant libraries listed in $VARS (var/*.so, see mkvar.sh)
-#   nat     natural 8192^2 encodes at -s1..-s4 (one image at a time) + rocprofv3 kernel stats per speed
+#   abenv   bench.py A/B over environment settings ($AB_ENVS)
+#   nat     natural 8192^2 encodes at -s1..-s4 ($NAT_PROF_SPEEDS; one image at a time) + rocprofv3 kernel stats per speed
 #   inflight  bench.py (100 steps) over images in flight x GPU_MAX_HW_QUEUES ($INFLIGHT: "D:Q ..."; Q 0 =
-#           one queue per image)
+#           the bench default, hw_queues_for(D))
 #   noix    no-index decode (synthetic + natural, one image at a time) and the no-index pipeline leg,
 #           once per environment setting in $NOIX_ENVS ("A=1,B=2 C=3 ..."; "-" = defaults)
 #   natab   natural 8192^2 encodes at the speeds in $NAT_SPEEDS once per setting in $NAT_ENVS
@@ -46,16 +47,25 @@ PY
         python3 -c "import json; d=json.loads(open('$O/ab_${n}.json').read().strip().splitlines()[-1]); r=d['roofline']; print('$n', d['value'], r['avg_launch_ms'], r['avg_launch_ms_under_load'], d['detail']['bit_exact_vs_reference'], d['detail']['slot_files_bit_exact'])"
       done
       unset HOH_LIB ;;
+    abenv)
+      # bench.py A/B over environment settings ($AB_ENVS: "A=1,B=2 C=3 ..."; "-" = defaults)
+      B="--no-legs --no-pmc --no-cpu-baseline --no-config2"
+      for ev in ${AB_ENVS:--}; do
+        E=""; [ "$ev" != "-" ] && E=$(echo $ev | tr ',' ' ')
+        n=$(echo $ev | tr ',=' '__')
+        timeout -k 10 200 env $E python -u bench.py --steps 100 --warmup 5 $B > $O/abe_${n}.json 2> $O/ab_err || { tail $O/ab_err; exit 1; }
+        python3 -c "import json; d=json.loads(open('$O/abe_${n}.json').read().strip().splitlines()[-1]); r=d['roofline']; print('[$ev]', d['value'], r['avg_launch_ms'], r['avg_launch_ms_under_load'], d['detail']['bit_exact_vs_reference'], d['detail']['slot_files_bit_exact'])"
+      done ;;
     inflight)
       B="--no-legs --no-pmc --no-cpu-baseline --no-config2"
-      for dq in ${INFLIGHT:-"16:0 20:0 24:0 28:0 32:0 24:16 24:20 32:16 32:20"}; do
+      for dq in ${INFLIGHT:-16:0 20:0 24:0 28:0 32:0 40:0 24:24 28:28}; do
         d=${dq%:*}; q=${dq#*:}
         timeout -k 10 200 python -u bench.py --steps 100 --warmup 5 --inflight $d --hw-queues $q $B > $O/if_${d}_${q}.json 2> $O/if_err \
           || { tail $O/if_err; exit 1; }
         python3 -c "import json; d=json.load(open('$O/if_${d}_${q}.json')); print('inflight $d queues $q', d['value'], d['detail']['latency_ms_enc'], d['detail']['latency_ms_dec'])"
       done ;;
     noix)
-      for ev in ${NOIX_ENVS:-"-"}; do
+      for ev in ${NOIX_ENVS:--}; do
         E=""; [ "$ev" != "-" ] && E=$(echo $ev | tr ',' ' ')
         for kind in synth natural; do
           timeout -k 10 120 env $E python3 tools/scripts/noix_bench.py $kind 8192 5 > $O/noix.txt 2>&1 || { tail $O/noix.txt; exit 1; }
@@ -66,9 +76,9 @@ PY
         python3 -c "import json; d=json.loads(open('$O/noixb.json').read().strip().splitlines()[-1])['detail']; print('[$ev] pipeline', d.get('no_index_pipeline_MBps'), d.get('no_index_pipeline_lossless'), 'single', d.get('no_index_decode_MBps'))"
       done ;;
     natab)
-      for ev in ${NAT_ENVS:-"-"}; do
+      for ev in ${NAT_ENVS:--}; do
         E=""; [ "$ev" != "-" ] && E=$(echo $ev | tr ',' ' ')
-        for sp in ${NAT_SPEEDS:-"3 4"}; do
+        for sp in ${NAT_SPEEDS:-3 4}; do
           timeout -k 10 300 env $E python3 tools/scripts/natural_prof.py 8192 $sp 2 > $O/natab.txt 2>&1 || { tail $O/natab.txt; exit 1; }
           echo "[$ev] $(grep ^natural $O/natab.txt)"
         done
@@ -89,7 +99,7 @@ PY
       done
       python3 tools/scripts/pmc_summary2.py $O/pmc* > $O/pmc_summary.txt; cat $O/pmc_summary.txt ;;
     nat)
-      for sp in 1 2 3 4; do
+      for sp in ${NAT_PROF_SPEEDS:-1 2 3 4}; do
         (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/nat$sp -o run \
           -- python3 $GRAFT_REPO_ROOT/tools/scripts/natural_prof.py 8192 $sp 2) > $O/nat$sp.txt 2>&1 || { tail $O/nat$sp.txt; exit 1; }
         grep "^natural" $O/nat$sp.txt
