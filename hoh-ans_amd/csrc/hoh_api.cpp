@@ -64,7 +64,7 @@ struct hoh_ctx {
   Scratch scr;
   hipStream_t own = nullptr;
   SideStream side;              // -s>=1: the LZ screen beside the predictor search (created on first use)
-  Buf idx8, fpb, pinfo, lg;     // -s>=1 workspaces
+  Buf idx8, fpb, pinfo, lg;     // -s>=1 workspaces (fpb: fingerprints, then the tile-major pixels)
   Buf lzs;                      // -s>=2: LZ posting lists (k_lzsort): sorted positions + ping-pong (then the sorted fingerprints) + ranks
   uint32_t lg_key[4] = {0, 0, 0, 0};
   uint64_t lg_off[4] = {0, 0, 0, 0};
@@ -388,11 +388,12 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   int e = HOH_OK;
   if (speed) {
     if ((e = ensure(c->idx8, (size_t)ntiles * j.npix_cap))) return e;
-    if ((e = ensure(c->fpb, (size_t)ntiles * j.npix_cap * 4))) return e;
+    if ((e = ensure(c->fpb, (size_t)ntiles * j.npix_cap * 8))) return e;   // fingerprints + pixels
     if ((e = ensure(c->pinfo, (size_t)ntiles * HOH_NPLANE_S * sizeof(PlaneInfo)))) return e;
     if ((e = ensure_log2_tables(c, W, H, j))) return e;
     j.idx8 = (uint8_t*)c->idx8.p;
     j.fpb = (uint32_t*)c->fpb.p;
+    j.tpx = j.fpb + (size_t)ntiles * j.npix_cap;
     j.lzs = nullptr;
     j.lzrank = nullptr;
     // posting lists for the long LZ windows (-s2..-s4) of tiles whose positions fit 16 bits

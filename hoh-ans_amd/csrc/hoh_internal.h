@@ -177,6 +177,7 @@ struct EncodeJob {
   int32_t* ncol;          // [tile] distinct colours (<= 256) or -1 (k_colours)
   uint8_t* idx8;          // -s>=1: [tile][npix_cap] palette indices (the indexed plane's data)
   uint32_t* fpb;          // -s>=1: [tile][npix_cap] 4-pixel window fingerprints (LZ)
+  uint32_t* tpx;          // -s>=1: [tile][npix_cap] the tile's pixels as u32 in tile raster order (LZ)
   uint32_t* lzs;          // -s>=2, tiles <= 65536 px: [tile][npix_cap] positions grouped by hash16(fingerprint),
                           //   ascending inside a group: pos | hash << 16 (k_lzsort); null: no posting lists
   uint16_t* lzrank;       //   [tile][npix_cap] index of each position in lzs

@@ -610,14 +610,24 @@ __device__ __forceinline__ uint32_t fp4(uint32_t a, uint32_t b, uint32_t c, uint
 }
 
 // fingerprint of the 4-pixel window starting at every position (0: fewer than 4 pixels left)
+// Also the tile's pixels as u32 in tile raster order (tpx): k_lzscan's ring fills and run lengths
+// read them as contiguous words instead of three bytes behind a division by the tile width.
 __global__ __launch_bounds__(NT) void k_lzfp(EncodeJob j) {
+  __shared__ uint32_t px[NT + 3];
   const int t = blockIdx.y;
   const TileInfo ti = j.tiles[t];
-  const uint32_t npix = (uint32_t)ti.w * ti.h;
-  for (uint32_t q = blockIdx.x * NT + threadIdx.x; q < npix; q += gridDim.x * NT) {
-    uint32_t f = 0;
-    if (q + 3 < npix) f = fp4(tile_px(j, ti, q), tile_px(j, ti, q + 1), tile_px(j, ti, q + 2), tile_px(j, ti, q + 3));
-    j.fpb[(size_t)t * j.npix_cap + q] = f;
+  const uint32_t npix = (uint32_t)ti.w * ti.h, tid = threadIdx.x;
+  uint32_t* fo = j.fpb + (size_t)t * j.npix_cap;
+  uint32_t* po = j.tpx + (size_t)t * j.npix_cap;
+  for (uint32_t c0 = blockIdx.x * NT; c0 < npix; c0 += gridDim.x * NT) {
+    for (uint32_t k = tid; k < NT + 3; k += NT) px[k] = c0 + k < npix ? tile_px(j, ti, c0 + k) : 0u;
+    __syncthreads();
+    const uint32_t q = c0 + tid;
+    if (q < npix) {
+      po[q] = px[tid];
+      fo[q] = q + 3 < npix ? fp4(px[tid], px[tid + 1], px[tid + 2], px[tid + 3]) : 0u;
+    }
+    __syncthreads();
   }
 }
 
@@ -910,6 +920,7 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
   const uint32_t npix = (uint32_t)ti.w * ti.h, nwords = (npix + 63) / 64, w = ti.w;
   const uint64_t* bits = j.candbits + (size_t)t * (j.npix_cap / 64);
   const uint32_t* F = j.fpb + (size_t)t * j.npix_cap;
+  const uint32_t* TP = j.tpx + (size_t)t * j.npix_cap;
   uint32_t* mt = j.matches + (size_t)t * 3 * (j.lz_cap + 1);
   int bonus = 0;                                                      // choh.cpp:139-154
   if (ti.colours != -1) {
@@ -945,7 +956,7 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
     if (lo > wend) wend = lo & ~63u;
     while (wend < need) {
       const uint32_t p = wend + (uint32_t)lane;
-      const uint32_t v = tile_px(j, ti, min(p, npix - 1)), e = p & rmask;   // unconditional load
+      const uint32_t v = TP[min(p, npix - 1)], e = p & rmask;              // unconditional load
       const uint32_t x = p < npix ? v : 0xff000000u;
       pring[e] = x;
       if (e < 16) pring[e + rp] = x;                                 // the mirror of entries 0..15
@@ -977,21 +988,25 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
         if (run < 16 || L >= lim) break;
       }
     } else {
-      // backs beyond the ring (vertical ones past the window; every back at -s4 without a ring):
-      // the older side from the image, eight positions per round trip of loads
+      // backs beyond the ring (long ones, vertical ones past the window; every back without a
+      // ring): the older side from the tile's pixel words, sixteen positions per round trip
       while (L < lim) {
-        uint32_t a[8], c[8];
+        uint32_t a[16], c[16];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
+        for (int u = 0; u < 16; u++) {
           const uint32_t p = min(q + L + (uint32_t)u, npix - 1);
-          a[u] = rp ? pring[p & rmask] : tile_px(j, ti, p);
-          c[u] = tile_px(j, ti, p - b);
+          a[u] = rp ? pring[p & rmask] : TP[p];
+          c[u] = TP[p - b];
         }
-        uint32_t run = 8;
+        uint32_t r0 = 8, r1 = 16;
 #pragma unroll
-        for (int u = 7; u >= 0; u--) run = a[u] != c[u] ? (uint32_t)u : run;
+        for (int u = 7; u >= 0; u--) {
+          r1 = a[u + 8] != c[u + 8] ? (uint32_t)u + 8 : r1;
+          r0 = a[u] != c[u] ? (uint32_t)u : r0;
+        }
+        const uint32_t run = r0 < 8 ? r0 : r1;
         L = min(L + run, lim);
-        if (run < 8) break;
+        if (run < 16) break;
       }
     }
     return L;
