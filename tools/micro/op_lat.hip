@@ -36,7 +36,12 @@ __global__ void lat(uint32_t* out, uint64_t* cyc, uint32_t a) {
   if (OP == 12) { uint64_t t = ((uint64_t)y << 32) | x; asm volatile("v_lshrrev_b64 %0, 3, %0" : "+v"(t)); x = (uint32_t)t; y = (uint32_t)(t >> 32); } \
   if (OP == 13) asm volatile("v_rcp_f64 %0, %0" : "+v"(d)); \
   if (OP == 14) asm volatile("v_trunc_f64 %0, %0" : "+v"(d)); \
-  if (OP == 15) asm volatile("v_cvt_f32_u32 %0, %0" : "+v"(x));
+  if (OP == 15) asm volatile("v_cvt_f32_u32 %0, %0" : "+v"(x)); \
+  if (OP == 16) asm volatile("v_add_f64 %0, %0, %1" : "+v"(d) : "v"(one)); \
+  if (OP == 17) asm volatile("v_mad_i32_i24 %0, %0, %1, %1" : "+v"(x) : "v"(a)); \
+  if (OP == 18) { uint64_t e_; asm volatile("v_cmp_ge_u32_e64 %1, %0, %2\n\tv_cndmask_b32_e64 %0, %0, %2, %1" : "+v"(x), "=s"(e_) : "v"(y)); } \
+  if (OP == 19) asm volatile("v_or_b32 %0, 0x43300000, %0" : "+v"(x)); \
+  if (OP == 20) asm volatile("v_sub_u32 %0, %1, %0" : "+v"(x) : "v"(y));
   for (int it = 0; it < 4; ++it) {
     if (ILP == 1) { REP64(ONE(x0, y0, d0)) }
     if (ILP == 4) { REP16(ONE(x0, y0, d0) ONE(x1, y1, d1) ONE(x2, y2, d2) ONE(x3, y3, d3)) }
@@ -87,6 +92,11 @@ int main() {
   BOTH(13, "v_rcp_f64")
   BOTH(14, "v_trunc_f64")
   BOTH(15, "v_cvt_f32_u32")
+  BOTH(16, "v_add_f64")
+  BOTH(17, "v_mad_i32_i24")
+  BOTH(18, "v_cmp_e64+cndmask(sgpr)")
+  BOTH(19, "v_or_b32 literal")
+  BOTH(20, "v_sub_u32")
   uint64_t* d_clk; CK(hipMalloc(&d_clk, 2048 * 16));
   for (int nb : {1, 256, 1024}) {
     hipLaunchKernelGGL(clk, dim3(nb), dim3(64), 0, 0, d_clk, 3u, 20000);
