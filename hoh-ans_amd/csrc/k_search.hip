@@ -252,117 +252,6 @@ __device__ double cell_cost_one(const uint16_t* D, int w, int h, int depth, int 
   return cost;
 }
 
-// cell_cost for every full mask kMasks[4 .. 4 + nf) at once (nf <= 10).  best_pred depends only
-// on the pixel and its 16 predictions, never on the walk's state, so one pass computes them once
-// for all masks: with keys (|v - p_k| << 4) | k, the first least predictor over all sixteen is the
-// smallest key and over all but one index e the smallest key other than e's, i.e. the smallest or
-// the second smallest.  kMasks[4..13] are "all but e" for e = 6, 1, 2, 3, 4, 5, 7, 9, the pair
-// {0, 1} and all sixteen.  Per mask only the state differs: its best predictors of the row above
-// (LDS, [mask][column][lane] bytes) and of the left neighbour (a register), the two picks (from the
-// pixel's predictions staged in LDS, [pair][lane] words), the residual and its weight, summed in
-// f64 in raster order exactly as cell_cost sums each mask.  The weights are gathered one pixel
-// ahead of their additions.
-#define WM_N 10
-#define WM_COLS 42
-__device__ __forceinline__ uint32_t wm_best(int m, uint32_t k1, uint32_t k2, uint32_t kp) {
-  const uint32_t b1 = k1 & 15u, b2 = k2 & 15u;
-  switch (m) {
-    case 0: return b1 == 6 ? b2 : b1;
-    case 1: return kp & 15u;
-    case 2: return b1 == 1 ? b2 : b1;
-    case 3: return b1 == 2 ? b2 : b1;
-    case 4: return b1 == 3 ? b2 : b1;
-    case 5: return b1 == 4 ? b2 : b1;
-    case 6: return b1 == 5 ? b2 : b1;
-    case 7: return b1 == 7 ? b2 : b1;
-    case 8: return b1 == 9 ? b2 : b1;
-    default: return b1;
-  }
-}
-__device__ void cell_cost_multi(const uint16_t* D, int w, int h, int depth, int xt, int yt, int cx, int cy, int nf,
-                                const double* ent, uint16_t* top, uint8_t* bpr, uint32_t* pst, double* out) {
-  const int c = 1 << depth, half = c >> 1;
-  const int tw = (w + xt - 1) / xt, th = (h + yt - 1) / yt;
-  const int x0 = cx * tw, y0 = cy * th;
-  // bpr: this lane's byte of [m][column][64 lanes]; pst: this lane's word of [pair][64 lanes]
-  for (int i = 0; i < tw; i++) {
-    top[i] = cy ? D[(long)y0 * w + x0 + i - w] : (uint16_t)half;
-#pragma unroll
-    for (int m = 0; m < WM_N; m++)
-      if (m < nf) bpr[(m * WM_COLS + i) * 64] = 4;
-  }
-  double cost[WM_N], pend[WM_N];
-#pragma unroll
-  for (int m = 0; m < WM_N; m++) { cost[m] = 0.0; pend[m] = 0.0; }
-  bool have = false;
-  for (int ym = 0; ym < th && y0 + ym < h; ym++) {
-    uint32_t L, TL;
-    if (cx) {
-      L = D[(long)(y0 + ym) * w + x0 - 1];
-      TL = (ym || cy) ? D[(long)(y0 + ym - 1) * w + x0 - 1] : (uint32_t)half;
-    } else {
-      L = TL = half;
-    }
-    const uint16_t* row = D + (long)(y0 + ym) * w + x0;
-    const int vw = min(tw, w - x0);
-    uint32_t left[WM_N];
-#pragma unroll
-    for (int m = 0; m < WM_N; m++) left[m] = m < nf ? bpr[(m * WM_COLS + tw - 1) * 64] : 0u;
-    uint32_t vn = vw > 0 ? row[0] : 0u;
-    for (int xm = 0; xm < vw; xm++) {
-      const uint32_t v = vn;
-      if (xm + 1 < vw) vn = row[xm + 1];
-      const uint32_t T = top[xm];
-      const int xr = xm + 1 == tw ? 0 : xm + 1;
-      const uint32_t TR = top[xr];
-      Preds p;
-      preds16(L, T, TL, TR, false, p);
-      uint32_t k1 = 0xffffffffu, k2 = 0xffffffffu;
-#pragma unroll
-      for (int k = 0; k < 16; k++) {
-        const uint32_t key = ((uint32_t)abs((int)v - (int)p.v[k]) << 4) | (uint32_t)k;
-        k2 = min(k2, max(k1, key));
-        k1 = min(k1, key);
-      }
-      const uint32_t kp = min(((uint32_t)abs((int)v - (int)p.v[0]) << 4), ((uint32_t)abs((int)v - (int)p.v[1]) << 4) | 1u);
-#pragma unroll
-      for (int k = 0; k < 8; k++) pst[k * 64] = p.v[2 * k] | (p.v[2 * k + 1] << 16);
-      // the previous pixel's weights join their sums now (their loads had a pixel's work to land)
-      if (have) {
-#pragma unroll
-        for (int m = 0; m < WM_N; m++) cost[m] += pend[m];
-      }
-#pragma unroll
-      for (int m = 0; m < WM_N; m++) {
-        if (m < nf) {
-          uint8_t* bq = bpr + (m * WM_COLS + xm) * 64;
-          const uint32_t bA = *bq, bB = left[m];
-          // prediction k: half k & 1 of word k >> 1 (read as words: the stores above are words)
-          const uint32_t pa = (pst[(bA >> 1) * 64] >> ((bA & 1) * 16)) & 0xffffu;
-          const uint32_t pb = (pst[(bB >> 1) * 64] >> ((bB & 1) * 16)) & 0xffffu;
-          const uint32_t pr = midp(pa, pb);
-          const uint32_t r = ((uint32_t)((int)v - (int)pr + half + c)) & (uint32_t)(c - 1);
-          pend[m] = ent[r];
-          const uint32_t nb = wm_best(m, k1, k2, kp);
-          *bq = (uint8_t)nb;
-          left[m] = nb;
-        }
-      }
-      have = true;
-      TL = T;
-      top[xm] = (uint16_t)v;
-      L = v;
-    }
-  }
-  if (have) {
-#pragma unroll
-    for (int m = 0; m < WM_N; m++) cost[m] += pend[m];
-  }
-#pragma unroll
-  for (int m = 0; m < WM_N; m++)
-    if (m < nf) out[m] = cost[m];
-}
-
 // channelpredict_all (prediction.hpp:153-229) at one pixel, fully parallel: the best predictors
 // it needs (row above, left neighbour / end of the row above) are recomputed from the originals
 struct AllCtx {
@@ -410,29 +299,14 @@ __device__ __forceinline__ uint32_t resid_all(const AllCtx& a, int x, int y) {
 // slowest wave.  The full walk keeps the cell's top row and best predictors in LDS (8 KB per
 // wave: ~120 VGPRs, four waves per SIMD).  ncmax: cells of the largest plane (host, from the tile
 // size).
-// Task kinds: the four one-predictor masks, then (WALK_MULTI, two or more full masks: -s2..-s4)
-// one task per (plane, cell) for every full mask at once (cell_cost_multi: natural 8192^2 -s3
-// 102 -> 83 ms, -s4 109 -> 91 ms); otherwise a task per mask (cell_cost; -s1's one full mask walks
-// faster alone, 33 against 36 ms).  bp and bpr share their LDS: one launch uses one of them.
-#ifndef WALK_MULTI
-#define WALK_MULTI 1
-#endif
-__host__ __device__ inline bool walk_multi(int npred) { return WALK_MULTI && (npred == 10 || npred == 14); }
-__host__ __device__ inline int walk_kinds(int npred) { return walk_multi(npred) ? 5 : npred; }
-static inline size_t walk_lds(int npred) { return walk_multi(npred) ? WM_N * WM_COLS * 64 + 8 * 64 * 4 : 64 * 44; }
 __global__ __launch_bounds__(64) void k_search_walk(EncodeJob j, int npred, int ncmax) {
   __shared__ uint16_t top[64][42];
-  // dynamic LDS (walk_lds): cell_cost_multi's bpr + pst, or cell_cost's bp[64][44] (the small
-  // request keeps -s1's walk at its occupancy)
-  extern __shared__ __attribute__((aligned(16))) uint8_t wdyn[];
-  uint8_t* bpr = wdyn;
-  uint32_t* pst = (uint32_t*)(wdyn + WM_N * WM_COLS * 64);
-  uint8_t (*bp)[44] = (uint8_t (*)[44])wdyn;
+  __shared__ uint8_t bp[64][44];
   const int lane = threadIdx.x;
   const uint32_t npl = (uint32_t)j.ntiles * HOH_NPLANE_S;
   const uint64_t g = (uint64_t)blockIdx.x * 64 + lane;
   const uint32_t m = (uint32_t)(g / ((uint64_t)npl * ncmax));
-  if (m >= (uint32_t)walk_kinds(npred)) return;
+  if (m >= (uint32_t)npred) return;
   const uint32_t rem = (uint32_t)(g % ((uint64_t)npl * ncmax)), pl = rem / ncmax, cell = rem % ncmax;
   const int t = (int)(pl / HOH_NPLANE_S), p = (int)(pl % HOH_NPLANE_S);
   const TileInfo ti = j.tiles[t];
@@ -443,13 +317,6 @@ __global__ __launch_bounds__(64) void k_search_walk(EncodeJob j, int npred, int 
   const uint16_t* D = j.sym + fin_plane_off(j, t, p);
   double* ent = search_scr(j, (int)pl);
   const uint32_t mk = kMasks[m];
-  if (m == 4 && walk_multi(npred)) {
-    // (the mask count stays a run-time value: templated on it, the walk took 212 VGPRs and ran
-    // 10-15 % slower at half the occupancy)
-    cell_cost_multi(D, w, h, depth, xt, yt, (int)cell % xt, (int)cell / xt, npred - 4, ent, top[lane], bpr + lane,
-                    pst + lane, ent + 512 + cell * 14 + 4);
-    return;
-  }
   ent[512 + cell * 14 + m] =
       m < 4 ? cell_cost_one(D, w, h, depth, xt, yt, (int)cell % xt, (int)cell / xt, (uint32_t)__builtin_ctz(mk), ent)
             : cell_cost(D, w, h, depth, xt, yt, (int)cell % xt, (int)cell / xt, mk, ent, top[lane], bp[lane]);
@@ -1674,7 +1541,9 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, v
   // context's side stream beside it; k_nuke (which compacts the searched planes) joins the two.
   // The search scratch and the LZ map lie in disjoint parts of each tile's tab_gen region.
   // a failed fork runs the LZ kernels on s itself (ordered), never unordered on the side stream
-  const bool fork = side.s && side.fork && side.join && hipEventRecord(side.fork, s) == hipSuccess &&
+  // HOH_LZ_FORK=0: the LZ kernels on s itself (measurement)
+  static const int fork_ok = [] { const char* e = getenv("HOH_LZ_FORK"); return e ? atoi(e) : 1; }();
+  const bool fork = fork_ok && side.s && side.fork && side.join && hipEventRecord(side.fork, s) == hipSuccess &&
                     hipStreamWaitEvent(side.s, side.fork, 0) == hipSuccess;
   hipStream_t sl = fork ? side.s : s;
   {
@@ -1709,11 +1578,11 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, v
   {
     const int npred = j.speed * 5 < 14 ? j.speed * 5 : 14;
     const int ncmax = ((j.tw + 39) / 40) * ((j.th + 39) / 40);
-    const uint64_t ntask = (uint64_t)walk_kinds(npred) * j.ntiles * HOH_NPLANE_S * ncmax;
+    const uint64_t ntask = (uint64_t)npred * j.ntiles * HOH_NPLANE_S * ncmax;
     const dim3 gs(j.ntiles * HOH_NPLANE_S), gw((unsigned)((ntask + 63) / 64));
     hipLaunchKernelGGL(k_search, gs, dim3(NT), sizeof(SearchLds), s, j, 0, 0);
     for (int pass = 0; pass < (j.speed > 2 ? 2 : 1); pass++) {
-      hipLaunchKernelGGL(k_search_walk, gw, dim3(64), walk_lds(npred), s, j, npred, ncmax);
+      hipLaunchKernelGGL(k_search_walk, gw, dim3(64), 0, s, j, npred, ncmax);
       hipLaunchKernelGGL(k_search, gs, dim3(NT), sizeof(SearchLds), s, j, 1, pass);
     }
   }

@@ -144,3 +144,17 @@ def test_serial_decode_16384_natural(hoh):
     g = gs[0]
     serial_decode(hoh, hoh.natural_rgb_dev(16384, 16384, g["spec"]["seed"]), 16384, 16384, g["out"]["len"],
                   g["out"]["sha256"])
+
+
+@pytest.mark.parametrize("speed", [2, 3, 4])
+def test_natural_8192_repeatable(hoh, speed):
+    """The same image encoded again on the same context gives the same file (a race in the search
+    or LZ kernels shows up as run-to-run size differences; tools/scripts/rep_speed.py)."""
+    import torch
+    d = hoh.natural_rgb_dev(8192, 8192, 1)
+    shas = set()
+    for _ in range(4):
+        out, n, _ = hoh.encode_image(d, 8192, 8192, speed=speed)
+        torch.cuda.synchronize()
+        shas.add((n, sha(out, n)))
+    assert len(shas) == 1, shas
