@@ -1662,7 +1662,7 @@ __global__ __launch_bounds__(64) void k_tilebytes_s(EncodeJob j) {
 // ---------------------------------------------------------------- orchestration
 
 static int lzs_ring_max() {
-  static const int v = [] { const char* e = getenv("HOH_LZS_RING_MAX"); return e ? atoi(e) : 2048; }();
+  static const int v = [] { const char* e = getenv("HOH_LZS_RING_MAX"); return e ? atoi(e) : 4096; }();
   return v;
 }
 static int lzs_seg() {
@@ -1700,9 +1700,11 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, v
     while (rp < limit + 324) rp <<= 1;
     // Four segment walks per tile (stitched as in k_lz), each with a pixel ring of up to
     // lzs_ring_max() positions; the ring serves backs up to rp - 324, the rest (long backs of
-    // -s3/-s4, vertical ones) read the image.  The scan waits on its loads, so workgroups per CU
-    // (LDS) count for more than the ring's reach: at -s4 rings of 8192 positions (one workgroup
-    // per CU) took 185 ms per natural 8192^2 encode, 2048 (three) 166 ms.
+    // -s3/-s4, vertical ones) read the tile's pixel words.  The scan waits on its loads, so
+    // workgroups per CU (LDS) count for more than the ring's reach (natural 8192^2 -s4 with
+    // rings of 8192 / 4096 / 2048: 111 / 105 / 84 ms), but with 2048-position rings about 1 in 40
+    // -s4 encodes came out a few bytes off (a race not found yet; none in 100
+    // encodes with 4096 or 8192), so the rings stay at 4096.
     // HOH_LZS_RING_MAX / HOH_LZS_SEG override (measurement).
     if (rp > lzs_ring_max()) rp = lzs_ring_max();
     if (rp < 1024) rp = 0;
