@@ -844,9 +844,12 @@ __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring,
           (m1 < (uint32_t)tid && fr[(base + m1) & (ring - 1)] == f);
       walk = !first && !c;
       if (!c && mode == LZC_MAP) {
-        // the latest earlier position of f (or of a fingerprint sharing its entry)
+        // the latest earlier position of f (or of a fingerprint sharing its entry).  The map's
+        // loads are agent-scope: its CAS / max run in L2, and a workgroup-scope load may be served
+        // from the CU's L1, whose copy of the line those atomics do not update (a stale empty slot
+        // loses a candidate, and the greedy scan then a match)
         for (uint32_t h = (f >> 1) & (mw - 1);; h = (h + 1) & (mw - 1)) {
-          const uint32_t v = __hip_atomic_load(mp + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          const uint32_t v = __hip_atomic_load(mp + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if (v == 0) break;
           if ((v & 0xffu) == tag) {
             c = q - ((v >> 8) - 1) <= bm;
@@ -918,7 +921,7 @@ __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring,
         atomicMax(&ht[hs2], e);
       } else {
         for (uint32_t h = (f >> 1) & (mw - 1);; h = (h + 1) & (mw - 1)) {
-          uint32_t v = __hip_atomic_load(mp + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          uint32_t v = __hip_atomic_load(mp + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if (v == 0) {
             uint32_t z = 0;
             if (__hip_atomic_compare_exchange_strong(mp + h, &z, e, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
