@@ -658,10 +658,14 @@ __device__ __forceinline__ uint32_t lzc_h(uint32_t f, int k) {
 // tag, linear probing from (f >> 1), at most half full, in the tab_gen buffer (k_tables writes
 // it later).  Fingerprints whose slot chain and tag coincide share an entry holding the larger
 // position, so "latest position older than q - bm" stays an exact no and only candidates are
-// added.  One workgroup owns a tile's map: workgroup-scope atomic loads / CAS / max, ordered
-// between chunks by the barrier; the chunk's own positions come from the chunk tables (a walk of
+// added.  One workgroup owns a tile's map: workgroup-scope CAS / max (performed in L2) and
+// agent-scope loads, so no load is served from an L1 copy older than an atomic (a stale 0 or an
+// older position would be a false no, a lost match), ordered between chunks by the barrier; the chunk's own positions come from the chunk tables (a walk of
 // at most the chunk if they are unsure).
 enum { LZC_WALK = 0, LZC_TAB = 1, LZC_MAP = 2 };
+#ifndef LZC_MAP_LOAD_SCOPE
+#define LZC_MAP_LOAD_SCOPE __HIP_MEMORY_SCOPE_AGENT                    // the map's loads: from L2 (below)
+#endif
 __device__ __forceinline__ uint32_t* lzc_map(const EncodeJob& j, int t) {
   return (uint32_t*)((char*)j.tab_gen + (size_t)t * TAB_TILE_BYTES + LZC_MAP_OFF);
 }
@@ -708,7 +712,7 @@ __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring,
       if (!c && mode == LZC_MAP) {
         // the latest earlier position of f (or of a fingerprint sharing its entry)
         for (uint32_t h = (f >> 1) & (mw - 1);; h = (h + 1) & (mw - 1)) {
-          const uint32_t v = __hip_atomic_load(mp + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          const uint32_t v = __hip_atomic_load(mp + h, __ATOMIC_RELAXED, LZC_MAP_LOAD_SCOPE);
           if (v == 0) break;
           if ((v & 0xffu) == tag) {
             c = q - ((v >> 8) - 1) <= bm;
@@ -780,7 +784,7 @@ __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring,
         atomicMax(&ht[hs2], e);
       } else {
         for (uint32_t h = (f >> 1) & (mw - 1);; h = (h + 1) & (mw - 1)) {
-          uint32_t v = __hip_atomic_load(mp + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          uint32_t v = __hip_atomic_load(mp + h, __ATOMIC_RELAXED, LZC_MAP_LOAD_SCOPE);
           if (v == 0) {
             uint32_t z = 0;
             if (__hip_atomic_compare_exchange_strong(mp + h, &z, e, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
