@@ -398,11 +398,79 @@ def extra_legs(args, slots, W, H, D, status, torch, hoh_ans, hd):
         out["natural_s0_single_dec_ms"] = round(ms_d, 3)
         out["natural_s0_single_MBps"] = round(W * H * 3 / (ms_e + ms_d) / 1e3, 1)
         out["natural_s0_single_lossless"] = bool(torch.equal(s0.dec, nat[0]))
-        del nat
     except Exception as e:
         out["natural_s0_error"] = repr(e)[:300]
+        nat = None
+    if nat is not None and args.speed_legs:
+        out.update(speed_legs(args, slots, nat, W, H, D, status, torch, hoh_ans, hd))
+    del nat
     out["legs_note"] = ("%d images in flight, one set-up pass per slot, then %d timed steps each; inputs resident "
                         "in HBM" % (D, K))
+    return out
+
+
+def speed_legs(args, slots, nat, W, H, D, status, torch, hoh_ans, hd):
+    """BASELINE configs[4] at the search speeds: the natural-statistic image (seed --seed in every
+    slot) encoded at choh -s1..-s4 (full predictor search, layer_encode.hpp:122-319, and the
+    seek-distance LZ, lz.hpp:32-95 at 10..14), D images in flight, encode only (-s>=1 layers are
+    undecodable by construction), one set-up pass per slot, then --speed-leg-steps
+    timed steps.  EVERY slot's last file is SHA-compared with the reference choh's
+    (golden_natural.json); one image at a time: the best of 3 synchronous encodes on slot 0."""
+    out = {}
+    K = max(1, args.speed_leg_steps)
+    for speed in [int(x) for x in args.speed_legs.split(",") if x.strip()]:
+        key = "natural_s%d" % speed
+        try:
+            def enq(k, i):
+                s = slots[k]
+                with torch.cuda.stream(s.stream):
+                    hoh_ans.encode_image_async(nat[k], W, H, s.out, status[i, 0:2], ctx=s.ctx, speed=speed)
+
+            def chk(total):
+                st = status[:total].cpu().numpy()
+                for i in range(total):
+                    hoh_ans.check_status(st[i, 0:2], "%s encode (step %d)" % (key, i))
+                return st
+
+            hd.run_pipeline(D, D, enq, lambda k, i: None)
+            torch.cuda.synchronize()
+            chk(D)
+            steps, el = 0, 0.0
+            for c in range(0, K, status.shape[0]):
+                n = min(status.shape[0], K - c)
+                torch.cuda.synchronize()
+                t = time.perf_counter()
+                hd.run_pipeline(D, n, enq, lambda k, i: None)
+                torch.cuda.synchronize()
+                el += time.perf_counter() - t
+                st = chk(n)
+                steps = n
+            g = golden_natural_sha(W, H, args.seed, speed)
+            match, checked = 0, 0
+            for k in range(min(D, steps)):
+                n_k = int(st[k + ((steps - 1 - k) // D) * D, 1])
+                checked += 1
+                match += g is not None and \
+                    hashlib.sha256(slots[k].out[:n_k].cpu().numpy().tobytes()).hexdigest() == g
+            te = []
+            for r in range(4):
+                torch.cuda.synchronize()
+                t = time.perf_counter()
+                _, n1, _ = hoh_ans.encode_image(nat[0], W, H, out_dev=slots[0].out, ctx=slots[0].ctx, speed=speed)
+                torch.cuda.synchronize()
+                te.append(time.perf_counter() - t)
+            single_ok = g is not None and hashlib.sha256(slots[0].out[:n1].cpu().numpy().tobytes()).hexdigest() == g
+            out[key + "_MBps"] = round(W * H * 3 * K / el / 1e6, 1)
+            out[key + "_ms_per_step"] = round(el / K * 1e3, 3)
+            out[key + "_file_bytes"] = n1
+            out[key + "_slot_files_bit_exact"] = "%d of %d" % (match + single_ok, checked + 1)
+            out[key + "_bit_exact_vs_reference"] = (match == checked and single_ok) if g else None
+            out[key + "_single_enc_ms"] = round(min(te[1:]) * 1e3, 3)
+        except Exception as e:      # reported, never silently replaced
+            out[key + "_error"] = repr(e)[:300]
+    out["speed_legs_note"] = ("configs[4] natural 8192^2 image, choh -sN encode only (Q14: -s>=1 layers are "
+                              "undecodable), %d images in flight, %d timed steps per speed; every slot's file "
+                              "SHA-checked against the reference choh's (golden_natural.json)" % (D, K))
     return out
 
 
@@ -594,6 +662,9 @@ def main():
     ap.add_argument("--no-legs", action="store_true",
                     help="skip the detail legs (no-index pipeline, natural-statistic pipeline)")
     ap.add_argument("--leg-steps", type=int, default=40, help="timed steps of each detail leg")
+    ap.add_argument("--speed-legs", default="1,2,3,4",
+                    help="choh -sN speeds of the natural-image encode legs (configs[4]); empty: none")
+    ap.add_argument("--speed-leg-steps", type=int, default=40, help="timed steps of each -sN leg")
     ap.add_argument("--pmc-probe", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.size <= 0:

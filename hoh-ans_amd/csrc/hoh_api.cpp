@@ -236,7 +236,9 @@ extern "C" int hoh_debug_read(hoh_ctx* c, int which, void* dst, size_t bytes) {
     return hipMemcpy(dst, (const uint8_t*)c->dec.bufs[15] + c->dec.sizes[15] - bytes, bytes, hipMemcpyDeviceToHost) == hipSuccess
                ? HOH_OK : HOH_E_HIP;
   }
-  const Buf& b = which == 0 ? c->matches : c->lzspec;
+  // 3: k_lzsort's posting lists of the last -s2..-s4 encode (sorted keys, sorted fingerprints,
+  // u16 ranks: tools/scripts/lzsort_check.py); 4: the fingerprints + tile pixel words (k_lzfp)
+  const Buf& b = which == 0 ? c->matches : which == 3 ? c->lzs : which == 4 ? c->fpb : c->lzspec;
   if (bytes > b.n || !b.p) return HOH_E_ARG;
   return hipMemcpy(dst, b.p, bytes, hipMemcpyDeviceToHost) == hipSuccess ? HOH_OK : HOH_E_HIP;
 }

@@ -880,15 +880,24 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
         base[tid] = run;
       }
       __syncthreads();
+      const uint32_t o = valid ? cnt[wv][d] + wr : 0u;
+#ifdef LZSORT_DELAY_TEST
+      // adversarial schedule (tools/scripts/lzsort_race.sh, never in the product build): the last
+      // wave clears late, so every other wave's next chunk runs ahead of it
+      if (wv == LZSORT_T / 64 - 1)
+        for (int z = 0; z < 4; z++) __builtin_amdgcn_s_sleep(127);
+#endif
+      // each wave clears only its own row, after its own reads (LDS operations of one wave are
+      // performed in order): the row is written next by this wave's next chunk and read by the
+      // per-digit scan only behind that chunk's first barrier.  (Clearing every row by digit
+      // owner after a barrier raced with a faster wave's next-chunk count store: a lost count
+      // gave two positions one slot, a wrong posting list and a different file per run.)
+#pragma unroll
+      for (int k = 0; k < 4; k++) cnt[wv][lane + 64 * k] = 0;
       if (valid) {
-        const uint32_t o = cnt[wv][d] + wr;
         out[o] = key;
         if (pass) R[key & 0xffffu] = (uint16_t)o;
       }
-      __syncthreads();
-      if (tid < 256)
-#pragma unroll
-        for (int w = 0; w < LZSORT_T / 64; w++) cnt[w][tid] = 0;
     }
     __syncthreads();
   }
