@@ -252,6 +252,131 @@ __device__ double cell_cost_one(const uint16_t* D, int w, int h, int depth, int 
   return cost;
 }
 
+// cell_cost for every mask at once (-s2..-s4): the one-predictor masks kMasks[0..3] (cell_cost_one's
+// rule) and the full masks kMasks[4 .. 4 + nf) (nf <= 10); out[m] = the cost of kMasks[m].
+// best_pred depends only on the pixel and its 16 predictions, never on the walk's state, so one
+// pass computes them once for all masks: with keys (|v - p_k| << 4) | k, the first least
+// predictor over all sixteen is the smallest key and over all but one index e the smallest key
+// other than e's, i.e. the smallest or the second smallest.  kMasks[4..13] are "all but e" for
+// e = 6, 1, 2, 3, 4, 5, 7, 9, the pair {0, 1} and all sixteen.  Per mask only the state differs:
+// its best predictors of the row above and of the left neighbour, the two picks, the residual
+// and its weight, summed in f64 in raster order exactly as cell_cost sums each mask (the weights
+// gathered one pixel ahead of their additions).  The walk's LDS state is dwords only: a version
+// with byte / u16 LDS stores (ds_write_b8 / b16, each lane's own bytes) changed files from run to
+// run (1 encode in 4 to 1 in 48 at -s3); with every LDS access a lane's whole dword, 172 encodes
+// at -s2..-s4 were identical (tools/scripts/rep_speed.py).
+#define WM_N 10
+__device__ __forceinline__ uint32_t wm_best(int m, uint32_t k1, uint32_t k2, uint32_t kp) {
+  const uint32_t b1 = k1 & 15u, b2 = k2 & 15u;
+  switch (m) {
+    case 0: return b1 == 6 ? b2 : b1;
+    case 1: return kp & 15u;
+    case 2: return b1 == 1 ? b2 : b1;
+    case 3: return b1 == 2 ? b2 : b1;
+    case 4: return b1 == 3 ? b2 : b1;
+    case 5: return b1 == 4 ? b2 : b1;
+    case 6: return b1 == 5 ? b2 : b1;
+    case 7: return b1 == 7 ? b2 : b1;
+    case 8: return b1 == 9 ? b2 : b1;
+    default: return b1;
+  }
+}
+__device__ void cell_cost_multi(const uint16_t* D, int w, int h, int depth, int xt, int yt, int cx, int cy, int nf,
+                                const double* ent, uint32_t* top, uint32_t* bst, double* out) {
+  // top: this lane's word per column, [col][64 lanes]; bst: this lane's best predictors, eight
+  // 4-bit columns per word, [mask][col / 8][64 lanes] (dword accesses only)
+  const int c = 1 << depth, half = c >> 1;
+  const int tw = (w + xt - 1) / xt, th = (h + yt - 1) / yt;
+  const int x0 = cx * tw, y0 = cy * th;
+  for (int i = 0; i < tw; i++) top[i * 64] = cy ? D[(long)y0 * w + x0 + i - w] : (uint32_t)half;
+  for (int m = 0; m < WM_N; m++)
+    if (m < nf)
+      for (int g = 0; g < (tw + 7) / 8; g++) bst[(m * 6 + g) * 64] = 0x44444444u;
+  double cost[WM_N], pend[WM_N], cost1[4], pend1[4];
+#pragma unroll
+  for (int m = 0; m < WM_N; m++) { cost[m] = 0.0; pend[m] = 0.0; }
+#pragma unroll
+  for (int m = 0; m < 4; m++) { cost1[m] = 0.0; pend1[m] = 0.0; }
+  bool have = false;
+  for (int ym = 0; ym < th && y0 + ym < h; ym++) {
+    uint32_t L, TL;
+    if (cx) {
+      L = D[(long)(y0 + ym) * w + x0 - 1];
+      TL = (ym || cy) ? D[(long)(y0 + ym - 1) * w + x0 - 1] : (uint32_t)half;
+    } else {
+      L = TL = half;
+    }
+    const uint16_t* row = D + (long)(y0 + ym) * w + x0;
+    const int vw = min(tw, w - x0);
+    uint32_t left[WM_N];
+#pragma unroll
+    for (int m = 0; m < WM_N; m++)
+      left[m] = m < nf ? (bst[(m * 6 + ((tw - 1) >> 3)) * 64] >> (((tw - 1) & 7) * 4)) & 15u : 0u;
+    const bool a4 = ym == 0, b4first = !(ym > 0 && vw == tw);
+    uint32_t vn = vw > 0 ? row[0] : 0u;
+    for (int xm = 0; xm < vw; xm++) {
+      const uint32_t v = vn;
+      if (xm + 1 < vw) vn = row[xm + 1];
+      const uint32_t T = top[xm * 64];
+      const int xr = xm + 1 == tw ? 0 : xm + 1;
+      const uint32_t TR = top[xr * 64];
+      Preds p;
+      preds16(L, T, TL, TR, false, p);
+      uint32_t k1 = 0xffffffffu, k2 = 0xffffffffu;
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        const uint32_t key = ((uint32_t)abs((int)v - (int)p.v[k]) << 4) | (uint32_t)k;
+        k2 = min(k2, max(k1, key));
+        k1 = min(k1, key);
+      }
+      const uint32_t kp = min(((uint32_t)abs((int)v - (int)p.v[0]) << 4), ((uint32_t)abs((int)v - (int)p.v[1]) << 4) | 1u);
+      if (have) {
+#pragma unroll
+        for (int m = 0; m < WM_N; m++) cost[m] += pend[m];
+#pragma unroll
+        for (int m = 0; m < 4; m++) cost1[m] += pend1[m];
+      }
+#pragma unroll
+      for (int m = 0; m < 4; m++) {
+        const uint32_t pkm = p.v[m == 0 ? 0 : m == 1 ? 1 : m == 2 ? 5 : 4];
+        const uint32_t pa = a4 ? p.v[4] : pkm, pb = (xm == 0 && b4first) ? p.v[4] : pkm;
+        const uint32_t r = ((uint32_t)((int)v - (int)midp(pa, pb) + half + c)) & (uint32_t)(c - 1);
+        pend1[m] = ent[r];
+      }
+      const uint32_t sh = (uint32_t)(xm & 7) * 4;
+#pragma unroll
+      for (int m = 0; m < WM_N; m++) {
+        if (m < nf) {
+          uint32_t* bw = bst + (m * 6 + (xm >> 3)) * 64;
+          const uint32_t wd = *bw;
+          const uint32_t bA = (wd >> sh) & 15u, bB = left[m];
+          const uint32_t pr = midp(pick(p, bA), pick(p, bB));
+          const uint32_t r = ((uint32_t)((int)v - (int)pr + half + c)) & (uint32_t)(c - 1);
+          pend[m] = ent[r];
+          const uint32_t nb = wm_best(m, k1, k2, kp);
+          *bw = (wd & ~(15u << sh)) | (nb << sh);
+          left[m] = nb;
+        }
+      }
+      have = true;
+      TL = T;
+      top[xm * 64] = v;
+      L = v;
+    }
+  }
+  if (have) {
+#pragma unroll
+    for (int m = 0; m < WM_N; m++) cost[m] += pend[m];
+#pragma unroll
+    for (int m = 0; m < 4; m++) cost1[m] += pend1[m];
+  }
+#pragma unroll
+  for (int m = 0; m < 4; m++) out[m] = cost1[m];
+#pragma unroll
+  for (int m = 0; m < WM_N; m++)
+    if (m < nf) out[4 + m] = cost[m];
+}
+
 // channelpredict_all (prediction.hpp:153-229) at one pixel, fully parallel: the best predictors
 // it needs (row above, left neighbour / end of the row above) are recomputed from the originals
 struct AllCtx {
@@ -299,14 +424,22 @@ __device__ __forceinline__ uint32_t resid_all(const AllCtx& a, int x, int y) {
 // slowest wave.  The full walk keeps the cell's top row and best predictors in LDS (8 KB per
 // wave: ~120 VGPRs, four waves per SIMD).  ncmax: cells of the largest plane (host, from the tile
 // size).
+// Task kinds: at -s2..-s4 one task per (plane, cell) walks every mask at once (cell_cost_multi:
+// natural 8192^2 -s3 101 -> 71 ms, -s4 109 -> 84 ms); at -s1, whose one full mask walks faster
+// alone (33 against 36 ms), a task per mask (cell_cost_one / cell_cost).  The multi walk's state
+// is in dynamic LDS (walk_lds), so -s1's walk keeps its occupancy.
+__host__ __device__ inline bool walk_multi(int npred) { return npred == 10 || npred == 14; }
+__host__ __device__ inline int walk_kinds(int npred) { return walk_multi(npred) ? 1 : npred; }
+static inline size_t walk_lds(int npred) { return walk_multi(npred) ? (42 + WM_N * 6) * 64 * 4 : 0; }
 __global__ __launch_bounds__(64) void k_search_walk(EncodeJob j, int npred, int ncmax) {
   __shared__ uint16_t top[64][42];
   __shared__ uint8_t bp[64][44];
+  extern __shared__ uint32_t wdyn[];                                  // cell_cost_multi: [42 + 60][64 lanes]
   const int lane = threadIdx.x;
   const uint32_t npl = (uint32_t)j.ntiles * HOH_NPLANE_S;
   const uint64_t g = (uint64_t)blockIdx.x * 64 + lane;
   const uint32_t m = (uint32_t)(g / ((uint64_t)npl * ncmax));
-  if (m >= (uint32_t)npred) return;
+  if (m >= (uint32_t)walk_kinds(npred)) return;
   const uint32_t rem = (uint32_t)(g % ((uint64_t)npl * ncmax)), pl = rem / ncmax, cell = rem % ncmax;
   const int t = (int)(pl / HOH_NPLANE_S), p = (int)(pl % HOH_NPLANE_S);
   const TileInfo ti = j.tiles[t];
@@ -316,6 +449,11 @@ __global__ __launch_bounds__(64) void k_search_walk(EncodeJob j, int npred, int 
   if (!(xt > 1 || yt > 1) || (int)cell >= xt * yt) return;
   const uint16_t* D = j.sym + fin_plane_off(j, t, p);
   double* ent = search_scr(j, (int)pl);
+  if (walk_multi(npred)) {
+    cell_cost_multi(D, w, h, depth, xt, yt, (int)cell % xt, (int)cell / xt, npred - 4, ent, wdyn + lane,
+                    wdyn + 42 * 64 + lane, ent + 512 + cell * 14);
+    return;
+  }
   const uint32_t mk = kMasks[m];
   ent[512 + cell * 14 + m] =
       m < 4 ? cell_cost_one(D, w, h, depth, xt, yt, (int)cell % xt, (int)cell / xt, (uint32_t)__builtin_ctz(mk), ent)
@@ -1591,11 +1729,11 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, v
   {
     const int npred = j.speed * 5 < 14 ? j.speed * 5 : 14;
     const int ncmax = ((j.tw + 39) / 40) * ((j.th + 39) / 40);
-    const uint64_t ntask = (uint64_t)npred * j.ntiles * HOH_NPLANE_S * ncmax;
+    const uint64_t ntask = (uint64_t)walk_kinds(npred) * j.ntiles * HOH_NPLANE_S * ncmax;
     const dim3 gs(j.ntiles * HOH_NPLANE_S), gw((unsigned)((ntask + 63) / 64));
     hipLaunchKernelGGL(k_search, gs, dim3(NT), sizeof(SearchLds), s, j, 0, 0);
     for (int pass = 0; pass < (j.speed > 2 ? 2 : 1); pass++) {
-      hipLaunchKernelGGL(k_search_walk, gw, dim3(64), 0, s, j, npred, ncmax);
+      hipLaunchKernelGGL(k_search_walk, gw, dim3(64), walk_lds(npred), s, j, npred, ncmax);
       hipLaunchKernelGGL(k_search, gs, dim3(NT), sizeof(SearchLds), s, j, 1, pass);
     }
   }
