@@ -2,15 +2,17 @@
 
 oracle/ref/Makefile `dropin` compiles the reference's callers UNCHANGED -- simple_entropy_encoder.cpp
 (:26-33, encode_entropy(bytes, n, 256, out, 12, 1)), simple_entropy_decoder.cpp (:28-34,
-decode_entropy_8bit) and layer_roundtrip_test.cpp (:7-59, layer_encode cruncher 2 -> decode_layer)
--- against include/hoh/*.hpp, linked to libhohgpu.so, into oracle/_ref/dropin/.  These tests run
+decode_entropy_8bit), layer_roundtrip_test.cpp (:7-59, layer_encode cruncher 2 -> decode_layer) and
+the encoder itself, choh.cpp (:394-527, encode_tile -> layer_encode / encode_entropy per tile) --
+against include/hoh/*.hpp, linked to libhohgpu.so, into oracle/_ref/dropin/.  These tests run
 the flow of entropy_roundtrip_test.sh:1-11 and the layer round trip with those binaries:
   * the drop-in encoder's stream must equal the reference encoder's (oracle/_ref, the reference
     binary built from the same source without the drop-ins) byte for byte;
   * the drop-in decoder must restore the input (cmp), from its own stream and the reference's;
   * the reference decoder must read the drop-in's stream back too (one stream: Q1 does not bite),
     except the single-symbol table it cannot read (Q6);
-  * layer_roundtrip_test must print "Layer roundtrip: OK" and exit 0 through the GPU.
+  * layer_roundtrip_test must print "Layer roundtrip: OK" and exit 0 through the GPU;
+  * choh's files and printed sizes must equal the reference binary's, tiled at -s0..-s2.
 The inputs are repository files (the reference encodes its own source text; that file is not
 kept here), plus byte patterns that reach the stored fallback and a single-symbol table (Q6)."""
 import os
@@ -84,3 +86,34 @@ def test_layer_roundtrip_flow():
     assert "Layer roundtrip: OK" in r.stdout
     r = _run([_bin(REF, "layer_roundtrip_test")])
     assert r.returncode == 0 and "Layer roundtrip: OK" in r.stdout
+
+
+def _choh_cases():
+    # (name, W, H, speed): tiled images (768x512: 3x2 tiles of 256; 1024^2: 4x4) at -s0 and -s1,
+    # plus an untiled one (header only)
+    return [("synth", 768, 512, 0), ("synth", 768, 512, 1), ("natural", 1024, 1024, 0),
+            ("natural", 1024, 1024, 1), ("synth", 768, 512, 2), ("synth", 320, 200, 0)]
+
+
+@pytest.mark.parametrize("case", _choh_cases(), ids=lambda c: "%s-%dx%d-s%d" % c)
+def test_choh_through_dropins(tmp_path, case):
+    """The reference's own encoder main (choh.cpp:394-527: header, tiling, encode_tile per tile,
+    which calls layer_encode (layer_encode.hpp:11-20) per plane and encode_entropy for the LZ and
+    palette streams) compiled unchanged against the drop-ins and run on the GPU: its file and
+    printed size must equal the reference binary's (oracle/_ref/choh, same source, no drop-ins)."""
+    import hoh_ans.natural as nat
+    from hoh_ans import synth
+    kind, W, H, speed = case
+    img = synth.synth_rgb(W, H, seed=3, noise=4) if kind == "synth" else nat.natural_rgb(W, H, 1)
+    src = tmp_path / "in.rgb"
+    src.write_bytes(np.ascontiguousarray(img, dtype=np.uint8).tobytes())
+    outs = {}
+    for tag, exe in (("dropin", _bin(DROP, "choh")), ("ref", _bin(REF, "choh"))):
+        o = tmp_path / ("%s.hoh" % tag)
+        r = subprocess.run([exe, str(src), str(o), str(W), str(H), "-s%d" % speed], capture_output=True,
+                           text=True, timeout=600)
+        assert r.returncode == 0, (tag, r.stdout + r.stderr)
+        outs[tag] = (o.read_bytes(), r.stdout.strip().splitlines()[-1])
+    assert outs["dropin"][1] == outs["ref"][1], "printed sizes differ"
+    assert outs["dropin"][0] == outs["ref"][0], "files differ (%d vs %d bytes)" % (len(outs["dropin"][0]),
+                                                                                   len(outs["ref"][0]))
