@@ -14,7 +14,6 @@
 #include <stdio.h>
 #include <string>
 #include <atomic>
-#include <atomic>
 
 void launch_synth(uint8_t* rgb, int W, int H, int y0, uint64_t seed, int noise, hipStream_t s);
 void launch_natural(uint8_t* rgb, int W, int rows, int y0, uint64_t seed, hipStream_t s);
@@ -72,6 +71,7 @@ struct hoh_ctx {
   DecWork dec;                  // decoder workspaces (k_decode.hip)
   uint64_t* pinned = nullptr;   // small host staging (status words, sizes)
   int profiling = 0;
+  int noix = HOH_NOIX_ADAPTIVE;  // HOH_OPT_NOIX_DECODER
   std::vector<std::string> knames;      // names of the marks recorded by the current call
   std::vector<hipEvent_t> kev;          // event pool, kev[0..nmark) recorded by the current call
   size_t nmark = 0;
@@ -174,11 +174,8 @@ int hoh_ctx_create(hoh_ctx** out, int device) {
   return HOH_OK;
 }
 
-// HOH_LZ_POSTING=0: -s2..-s4 LZ scans walk every back distance (the round-3 scan, for comparison)
-static int lz_posting() {
-  static const int v = [] { const char* e = getenv("HOH_LZ_POSTING"); return e ? atoi(e) : 1; }();
-  return v;
-}
+// knob LZ_POSTING=0: -s2..-s4 LZ scans walk every back distance (the round-3 scan, for comparison)
+static int lz_posting() { return HOH_KNOB(LZ_POSTING, 1); }
 
 static void freebuf(Buf& b) { if (b.p) (void)hipFree(b.p); b.p = nullptr; b.n = 0; }
 
@@ -200,6 +197,17 @@ void hoh_ctx_destroy(hoh_ctx* c) {
 }
 
 void hoh_set_profiling(hoh_ctx* c, int on) { if (c) c->profiling = on; }
+
+int hoh_ctx_set_option(hoh_ctx* c, int option, int64_t value) {
+  if (!c) return HOH_E_ARG;
+  switch (option) {
+    case HOH_OPT_NOIX_DECODER:
+      if (value < HOH_NOIX_ADAPTIVE || value > HOH_NOIX_WAVE) return HOH_E_ARG;
+      c->noix = (int)value;
+      return HOH_OK;
+  }
+  return HOH_E_ARG;
+}
 
 int hoh_get_kernel_ms(hoh_ctx* c, const char** names, float* ms, int max) {
   if (!c || c->nmark < 2) return 0;
@@ -822,4 +830,5 @@ hipStream_t ctx_stream(hoh_ctx* c, void* s) { return pick(c, s); }
 uint64_t* ctx_pinned(hoh_ctx* c) { return c->pinned; }
 int ctx_device(hoh_ctx* c) { return c->device; }
 int ctx_cus(hoh_ctx* c) { return c->cus; }
+int ctx_noix(hoh_ctx* c) { return c->noix; }
 void ctx_mark(hoh_ctx* c, hipStream_t s, const char* name, bool reset) { prof_mark(c, s, name, reset); }

@@ -55,6 +55,7 @@ hipStream_t ctx_stream(hoh_ctx* c, void* s);
 uint64_t* ctx_pinned(hoh_ctx* c);
 int ctx_device(hoh_ctx* c);
 int ctx_cus(hoh_ctx* c);
+int ctx_noix(hoh_ctx* c);                  // HOH_OPT_NOIX_DECODER (include/hoh_ans.h)
 void ctx_mark(hoh_ctx* c, hipStream_t s, const char* name, bool reset);
 
 // Per-context device scratch for the host-buffer entry points (encode_entropy, decode_entropy,

@@ -4,6 +4,17 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stddef.h>
+#include <stdlib.h>
+
+// Measurement knobs (A/B runs of tools/scripts only).  The product library has one schedule: a
+// knob is its compile-time default.  A library built with -DHOH_KNOBS (`make KNOBS=1`, or
+// tools/scripts/mkvar.sh ... -DHOH_KNOBS) reads HOH_<name> from the environment once per site.
+#ifdef HOH_KNOBS
+static inline int hoh_knob_env(const char* name, int def) { const char* e = getenv(name); return e ? atoi(e) : def; }
+#define HOH_KNOB(name, def) ([] { static const int v_ = hoh_knob_env("HOH_" #name, (def)); return v_; }())
+#else
+#define HOH_KNOB(name, def) (def)
+#endif
 
 #define HOH_WAVE 64
 #define HOH_HDR_CAP 1600          // bytes reserved per stream for varints + meta + table

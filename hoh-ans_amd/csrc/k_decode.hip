@@ -14,6 +14,7 @@
 //             subtract-green, one wave per tile, anti-diagonal wavefront over 64-row bands.
 //  k_dunpred_lz: tiles with LZ copies, serial raster walk.
 #include "hoh_dec.h"
+#include "../../include/hoh_ans.h"
 #include <string.h>
 #include <stdlib.h>
 #include <algorithm>
@@ -2449,28 +2450,16 @@ int decode_tiles_async_impl(hoh_ctx* c, const uint8_t* d_blob, size_t size, int 
   return decode_run(c, j, idx, s, &as);
 }
 
-// HOH_LZ_XROW: copies reading the row above that make an LZ tile a chain tile (measurement knob)
-static uint32_t lz_xrow() {
-  static const uint32_t v = [] { const char* e = getenv("HOH_LZ_XROW"); return e ? (uint32_t)atoi(e) : (uint32_t)LZ_XROW; }();
-  return v;
-}
+// copies reading the row above that make an LZ tile a chain tile (knob LZ_XROW)
+static uint32_t lz_xrow() { return (uint32_t)HOH_KNOB(LZ_XROW, LZ_XROW); }
 
-// HOH_NOIX_WAVE=1: no-index decodes with k_drans_wave alone (the round-2 decoder, for comparison)
-static int noix_wave() {
-  static const int v = [] { const char* e = getenv("HOH_NOIX_WAVE"); return e ? atoi(e) : 0; }();
-  return v;
-}
-
-// No-index chain kernel choice.  k_drans_multi (12 chains per CU, full tables) has the shorter
-// step (~260 cycles against k_drans_lanes' ~400) but holds a whole CU per 12 chains; k_drans_lanes
-// packs up to 64 chains per workgroup into compact tables and fills the device when several
-// decodes run at once.  So a decode that has the device to itself takes k_drans_multi, one that
-// finds another context's no-index chain kernel still in flight takes k_drans_lanes.
-// HOH_NOIX_MULTI=1 / 0 pins the choice (k_drans_multi / k_drans_lanes); unset: adaptive.
-static int noix_multi() {
-  static const int v = [] { const char* e = getenv("HOH_NOIX_MULTI"); return e ? atoi(e) : -1; }();
-  return v;
-}
+// No-index chain kernel choice (hoh_ctx_set_option HOH_OPT_NOIX_DECODER, default adaptive).
+// k_drans_multi (12 chains per CU, full tables) has the shorter step (~260 cycles against
+// k_drans_lanes' ~400) but holds a whole CU per 12 chains; k_drans_lanes packs up to 64 chains per
+// workgroup into compact tables and fills the device when several decodes run at once.  So an
+// adaptive decode that has the device to itself takes k_drans_multi, one that finds another
+// context's no-index chain kernel still in flight takes k_drans_lanes.  HOH_NOIX_WAVE: one wave
+// per stream (k_drans_wave, the round-2 decoder).
 
 // Contexts' completion events per device, to count the no-index decodes in flight beside this one.
 static std::mutex g_noix_mu;
@@ -2487,13 +2476,10 @@ void noix_release(DecWork& w) {
   w.noix_dev = -1;
 }
 
-// HOH_NOIX_WINDOW_MS: another context's no-index decode issued this recently counts as
+// Another context's no-index decode issued this recently (knob NOIX_WINDOW_MS) counts as
 // concurrent traffic even when its chain kernel has finished (a pipeline's decodes leave gaps
 // between kernels; one k_drans_multi among them takes every CU's LDS for its 7 ms)
-static int64_t noix_window_us() {
-  static const int64_t v = [] { const char* e = getenv("HOH_NOIX_WINDOW_MS"); return (int64_t)(e ? atof(e) * 1000 : 20000); }();
-  return v;
-}
+static int64_t noix_window_us() { return (int64_t)HOH_KNOB(NOIX_WINDOW_MS, 20) * 1000; }
 
 // 1 if another context on this device issued a no-index decode within the window or its chain
 // kernel has not finished (hipEventQuery only: nothing waits); registers w on first use and stamps
@@ -2514,20 +2500,13 @@ static int noix_busy(DecWork& w, int dev) {
         (now - o->noix_t < noix_window_us() || hipEventQuery(o->noix_ev) == hipErrorNotReady)) return 1;
   return 0;
 }
-// k_drans_lanes: LDS table budget per workgroup (HOH_DL_BUDGET_KB, >= the 5.1 KB worst-case table)
-// and workgroups per CU (HOH_DL_WG)
+// k_drans_lanes: LDS table budget per workgroup (knob DL_BUDGET_KB, >= the 5.1 KB worst-case
+// table) and workgroups per CU (knob DL_WG)
 static uint32_t dl_budget() {
-  static const uint32_t v = [] {
-    const char* e = getenv("HOH_DL_BUDGET_KB");
-    const uint32_t kb = e ? (uint32_t)atoi(e) : 20u;
-    return std::max<uint32_t>(std::min<uint32_t>(kb, 150u) * 1024u, dl_bytes(15, 512));
-  }();
-  return v;
+  const uint32_t kb = (uint32_t)HOH_KNOB(DL_BUDGET_KB, 20);
+  return std::max<uint32_t>(std::min<uint32_t>(kb, 150u) * 1024u, dl_bytes(15, 512));
 }
-static int dl_wg_per_cu() {
-  static const int v = [] { const char* e = getenv("HOH_DL_WG"); return e ? std::max(1, atoi(e)) : 4; }();
-  return v;
-}
+static int dl_wg_per_cu() { return std::max(1, HOH_KNOB(DL_WG, 4)); }
 
 static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s, const AsyncDec* as) {
   j.npix_cap = (uint32_t)(((size_t)j.tw * j.th + 63) / 64 * 64);
@@ -2574,7 +2553,7 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   if (indexed) {
     hipLaunchKernelGGL(k_dmatch, dim3((S + 255) / 256), dim3(256), 0, s, j, S);
     hipLaunchKernelGGL(k_drans, dim3(S), dim3(DR_T), DR_SMEM, s, j, S);
-  } else if (noix_wave()) {                                   // the one-wave-per-stream decoder alone
+  } else if (ctx_noix(c) == HOH_NOIX_WAVE) {                  // the one-wave-per-stream decoder alone
     hipLaunchKernelGGL(k_drans_wave, dim3(S), dim3(64), DL_SMEM, s, j, S, 0);
   } else {
     // every plane / LZ stream: a chain lane of k_drans_multi or k_drans_lanes (noix_multi above);
@@ -2585,8 +2564,8 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
     uint32_t* tbytes = mlist + S;
     uint32_t* rounds = tbytes + S;                           // S + 1 words
     hipLaunchKernelGGL(k_dmlist, dim3((S + 255) / 256), dim3(256), 0, s, j, S, mlist);
-    const int pin = noix_multi();
-    const bool multi = pin >= 0 ? pin != 0 : !noix_busy(w, ctx_device(c));
+    const int pin = ctx_noix(c);
+    const bool multi = pin == HOH_NOIX_MULTI || (pin != HOH_NOIX_LANES && !noix_busy(w, ctx_device(c)));
     if (multi) {
       // one workgroup per CU (its LDS is a whole CU's), rounds of DM_MS streams per workgroup
       const int nmax = std::min(S, 6 * j.ntiles);

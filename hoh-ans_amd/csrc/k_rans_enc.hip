@@ -362,15 +362,12 @@ __global__ __launch_bounds__(64) void k_rans_gen(EncodeJob j, int nstreams, SidM
 
 static std::atomic<unsigned> g_rot{0};
 
-// LDS requested per chain workgroup (isolation: at most 160 / this many chains per CU); the
-// HOH_CHAIN_LDS_KB environment variable overrides it for measurement
+// LDS requested per chain workgroup (isolation: at most 160 / this many chains per CU; knob
+// CHAIN_LDS_KB), never less than the lanes' output windows (WIN_PITCH dwords per lane)
 static size_t chain_lds() {
-  static const size_t v = [] {
-    const char* e = getenv("HOH_CHAIN_LDS_KB");
-    const int kb = e ? atoi(e) : 56;
-    return (size_t)(kb < 8 ? 8 : kb > 160 ? 160 : kb) * 1024;
-  }();
-  return v;
+  const int kb = HOH_KNOB(CHAIN_LDS_KB, 56);
+  const size_t want = (size_t)(kb > 160 ? 160 : kb) * 1024, win = (size_t)WIN_PITCH * 4 * 64;
+  return want < win ? win : want;
 }
 
 void launch_rans_fast01(const EncodeJob& j, hipStream_t s, int np0, SidMap a0, int na0, SidMap b0, int np1, SidMap a1,

@@ -1673,14 +1673,8 @@ __global__ __launch_bounds__(64) void k_tilebytes_s(EncodeJob j) {
 
 // ---------------------------------------------------------------- orchestration
 
-static int lzs_ring_max() {
-  static const int v = [] { const char* e = getenv("HOH_LZS_RING_MAX"); return e ? atoi(e) : 2048; }();
-  return v;
-}
-static int lzs_seg() {
-  static const int v = [] { const char* e = getenv("HOH_LZS_SEG"); const int n = e ? atoi(e) : LZS_SEG; return n < 1 ? 1 : n > LZS_SEG ? LZS_SEG : n; }();
-  return v;
-}
+static int lzs_ring_max() { return HOH_KNOB(LZS_RING_MAX, 2048); }
+static int lzs_seg() { const int n = HOH_KNOB(LZS_SEG, LZS_SEG); return n < 1 ? 1 : n > LZS_SEG ? LZS_SEG : n; }
 
 void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, void (*mark)(void*, const char*), void* mc) {
   const int dist = j.speed == 1 ? 10 : j.speed == 2 ? 11 : j.speed == 3 ? 12 : 14;   // choh.cpp:125-137
@@ -1692,8 +1686,8 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, v
   // context's side stream beside it; k_nuke (which compacts the searched planes) joins the two.
   // The search scratch and the LZ map lie in disjoint parts of each tile's tab_gen region.
   // a failed fork runs the LZ kernels on s itself (ordered), never unordered on the side stream
-  // HOH_LZ_FORK=0: the LZ kernels on s itself (measurement)
-  static const int fork_ok = [] { const char* e = getenv("HOH_LZ_FORK"); return e ? atoi(e) : 1; }();
+  // knob LZ_FORK=0: the LZ kernels on s itself (measurement)
+  const int fork_ok = HOH_KNOB(LZ_FORK, 1);
   const bool fork = fork_ok && side.s && side.fork && side.join && hipEventRecord(side.fork, s) == hipSuccess &&
                     hipStreamWaitEvent(side.s, side.fork, 0) == hipSuccess;
   hipStream_t sl = fork ? side.s : s;
@@ -1715,7 +1709,7 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, v
     // -s3/-s4, vertical ones) read the image.  The scan waits on its loads, so workgroups per CU
     // (LDS) count for more than the ring's reach: at -s4 rings of 8192 positions (one workgroup
     // per CU) took 185 ms per natural 8192^2 encode, 2048 (three) 166 ms.
-    // HOH_LZS_RING_MAX / HOH_LZS_SEG override (measurement).
+    // knobs LZS_RING_MAX / LZS_SEG (measurement).
     if (rp > lzs_ring_max()) rp = lzs_ring_max();
     if (rp < 1024) rp = 0;
     const int nseg = rp ? lzs_seg() : 1;

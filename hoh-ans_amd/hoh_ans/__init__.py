@@ -61,6 +61,7 @@ def lib():
                                            C.POINTER(C.c_uint64), C.c_int]
         L.hoh_reset_kernel_stats.argtypes = [vp]
         L.hoh_reset_kernel_stats.restype = None
+        L.hoh_ctx_set_option.argtypes = [vp, C.c_int, C.c_int64]
         L.hoh_encode_bound.restype = sz
         L.hoh_encode_bound.argtypes = [C.c_int, C.c_int]
         L.hoh_encode_image.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, vp, sz, szp, szp, vp]
@@ -170,6 +171,15 @@ class Context:
 
     def reset_stats(self):
         lib().hoh_reset_kernel_stats(self.h)
+
+    def set_option(self, option, value):
+        """hoh_ctx_set_option: e.g. set_option(OPT_NOIX_DECODER, NOIX_LANES)."""
+        check(lib().hoh_ctx_set_option(self.h, option, value), "hoh_ctx_set_option")
+
+
+# hoh_ctx_set_option (include/hoh_ans.h)
+OPT_NOIX_DECODER = 1
+NOIX_ADAPTIVE, NOIX_LANES, NOIX_MULTI, NOIX_WAVE = -1, 0, 1, 2
 
 
 _CTX = None

@@ -57,6 +57,20 @@ int hoh_get_kernel_ms(hoh_ctx* ctx, const char** names, float* ms, int max);
 int hoh_get_kernel_stats(hoh_ctx* ctx, const char** names, double* total_ms, uint64_t* count, int max);
 void hoh_reset_kernel_stats(hoh_ctx* ctx);
 
+/* Per-context options (HOH_E_ARG for an unknown option or value).
+ * HOH_OPT_NOIX_DECODER picks the rANS chain kernel of decodes WITHOUT a side index (any foreign
+ * .hoh, dhoh.cpp:297-396; every stream one serial chain): HOH_NOIX_ADAPTIVE (default: one lane per
+ * chain with full tables while the decode has the device to itself, compact-table lanes beside
+ * other no-index decodes), HOH_NOIX_LANES (compact tables, up to 64 chains per workgroup),
+ * HOH_NOIX_MULTI (full tables, 12 chains per CU) or HOH_NOIX_WAVE (one wave per stream).  Every
+ * choice gives the same bytes; the library reads no environment variables for it. */
+#define HOH_OPT_NOIX_DECODER 1
+#define HOH_NOIX_ADAPTIVE (-1)
+#define HOH_NOIX_LANES 0
+#define HOH_NOIX_MULTI 1
+#define HOH_NOIX_WAVE 2
+int hoh_ctx_set_option(hoh_ctx* ctx, int option, int64_t value);
+
 /* ---- image level: `choh in out W H -sN` / `dhoh in out` -------------------------------- */
 
 /* Worst-case .hoh size for a W x H image (stored planes + LZ streams + framing). */

@@ -160,3 +160,34 @@ def test_natural_8192_repeatable(hoh, speed):
         torch.cuda.synchronize()
         shas.add((n, sha(out, n)))
     assert len(shas) == 1, shas
+
+
+@pytest.mark.parametrize("mode", ["lanes", "multi", "wave", "adaptive"])
+def test_no_index_decoders(hoh, golden, mode):
+    """Every no-index chain kernel (hoh_ctx_set_option HOH_OPT_NOIX_DECODER; dhoh.cpp:297-396 reads
+    the file alone, entropy_decoding.hpp:268-276 per stream) decodes losslessly, pinned per
+    context rather than left to the adaptive choice: the synthetic 8192^2 bench file (reference
+    SHA), the natural 1024^2 -s0 file (LZ streams, reference SHA), and a high-noise 2048^2 image
+    (triangular noise k = 40) whose wide residual tables put more than three symbol starts into
+    many 64-slot buckets (k_drans_lanes' walk past its three-entry window)."""
+    import torch
+    ctx = hoh.Context(0)
+    ctx.set_option(hoh.OPT_NOIX_DECODER, {"lanes": hoh.NOIX_LANES, "multi": hoh.NOIX_MULTI,
+                                          "wave": hoh.NOIX_WAVE, "adaptive": hoh.NOIX_ADAPTIVE}[mode])
+    f = [c for c in golden["choh_s0"] if c["spec"]["W"] == 8192][0]
+    g = [x for x in natural_goldens() if (x["spec"]["W"], x["spec"]["speed"]) == (1024, 0)][0]
+    cases = [(hoh.synth_rgb_dev(8192, 8192, f["spec"]["seed"], f["spec"]["noise"], ctx=ctx), 8192, f["out"]),
+             (hoh.natural_rgb_dev(1024, 1024, g["spec"]["seed"], ctx=ctx), 1024, g["out"]),
+             (hoh.synth_rgb_dev(2048, 2048, 7, 40, ctx=ctx), 2048, None)]
+    for d, W, want in cases:
+        out, n, _ = hoh.encode_image(d, W, W, ctx=ctx)
+        torch.cuda.synchronize()
+        if want is not None:
+            assert n == want["len"] and sha(out, n) == want["sha256"]
+        f2 = out[:n].clone()
+        rgb, w, h = hoh.decode_image(f2, n, ctx=ctx, index=None)
+        torch.cuda.synchronize()
+        assert (w, h) == (W, W) and torch.equal(rgb, d), (mode, W)
+    with pytest.raises(hoh.HohError):
+        ctx.set_option(hoh.OPT_NOIX_DECODER, 3)
+    ctx.close()
