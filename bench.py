@@ -5,24 +5,27 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-One step = one pass of the hot path over the workload, inputs resident in HBM:
-  N = 1: choh -s0 of an 8192x8192 image (BASELINE.json configs[2]: 1024 tiles of 256x256, 3072
-         tile-plane rANS streams) into HBM (hoh_encode_image_async, which also records the decode
-         side index), then dhoh of that file back into HBM (hoh_decode_image_async).
+One step = one pass of the hot path over one batch of the workload, inputs resident in HBM:
+  N = 1: choh -s0 of a batch of B = --batch (default 8) 8192x8192 images (BASELINE.json
+         configs[2]: 1024 tiles of 256x256 each, 3072 tile-plane rANS streams) into HBM
+         (hoh_encode_images_async: every kernel covers the B images' tiles; it also records the
+         decode side index), then dhoh of the B files back into HBM (hoh_decode_images_async).
+         --batch 1: one image per step through hoh_encode_image_async / hoh_decode_image_async.
   N > 1: weak scaling (default) -- the image is 8192 x (8192*N) and rank r owns a band of tile
          rows (8192^2 pixels per GPU).  --strong: configs[3], one 16384x16384 image sharded over
          the N GPUs.  A step is: encode the shard's tiles (hoh_encode_tiles_async), gather every
          shard to rank 0 over RCCL (all-gather of the tile sizes, point-to-point blobs straight
          into rank 0's file behind the header + tile table: byte-identical to a 1-GPU encode),
          and decode the shard (hoh_decode_tiles_async, tile sizes read on the device).
-value = raw RGB bytes of the whole image x K / max-over-ranks(time of the K steps) / 1e6.
+value = raw RGB bytes of the step's images x K / max-over-ranks(time of the K steps) / 1e6.
 
-Images in flight (--inflight, default 20): each GPU keeps D images in flight, each slot with its
-own library context (HIP stream, workspaces), hardware queue and its OWN input image (seeds
-1..D, so no slot's input is a cache hit of another's).  One host thread per rank deals the steps
-round-robin to the slots through enqueue-only calls; at N > 1 the gathers are issued in step
-order on one process group (hoh_ans.dist.run_pipeline).  Warmup: max(W, D) steps run (every slot
-sizes its workspaces on its first step); the line reports the number that ran.
+Slots in flight (--inflight): at N = 1 D = 4 slots of B = 8 images (32 images in flight), each
+slot with its own library context (HIP stream, workspaces) and its OWN input images (seeds 1..32,
+so no image is a cache hit of another's), at HIP's default of 4 hardware queues (nothing set); the
+N > 1 path and --batch 1 keep 20 single-image slots on up to 20 queues.  One host thread per rank
+deals the steps round-robin to the slots through enqueue-only calls; at N > 1 the gathers are
+issued in step order on one process group (hoh_ans.dist.run_pipeline).  A set-up pass of one
+step per slot (workspaces sized outside the timed region), then W warmup steps, then K timed.
 
 Outside the timed region: every slot's decoded image is compared with its input (lossless), and
 at N = 1 slot 0's file (seed 1) with the sha256 golden of the compiled reference (tests/golden).
@@ -321,9 +324,41 @@ def golden_natural_sha(W, H, seed, speed=0):
     return None
 
 
-def extra_legs(args, slots, W, H, D, status, torch, hoh_ans, hd):
-    """N = 1 detail legs on the bench's own slots (contexts, streams, buffers), D images in flight,
-    one set-up pass per slot, then --leg-steps timed steps, lossless-checked afterwards:
+class SlotIO:
+    """The detail legs' calls on a slot: its B images per step through the batched calls
+    (hoh_*_images_async) when B > 1, else the single-image calls; status row i holds {code, size}
+    of every image's encode, then of every image's decode."""
+
+    def __init__(self, hoh_ans, W, H, B, stride):
+        self.h, self.W, self.H, self.B, self.stride = hoh_ans, W, H, B, stride
+
+    def encode(self, s, inp, row, index=None, speed=0):
+        if self.B > 1:
+            self.h.encode_images_async(inp, self.B, self.W, self.H, s.out, self.stride, row[:2 * self.B], ctx=s.ctx,
+                                       index=index, speed=speed)
+        else:
+            self.h.encode_image_async(inp, self.W, self.H, s.out, row[0:2], ctx=s.ctx, index=index, speed=speed)
+
+    def decode(self, s, row, index=None):
+        if self.B > 1:
+            self.h.decode_images_async(s.out, self.B, self.stride, self.W, self.H, s.dec, row[2 * self.B:4 * self.B],
+                                       ctx=s.ctx, index=index)
+        else:
+            self.h.decode_image_async(s.out, s.out.numel(), self.W, self.H, s.dec, row[2:4], ctx=s.ctx, index=index)
+
+    def check(self, st, total, what, decode=True):
+        for i in range(total):
+            for b in range(self.B):
+                self.h.check_status(st[i, 2 * b:2 * b + 2], "%s encode (step %d image %d)" % (what, i, b))
+                if decode:
+                    self.h.check_status(st[i, 2 * self.B + 2 * b:2 * self.B + 2 * b + 2],
+                                        "%s decode (step %d image %d)" % (what, i, b))
+
+
+def extra_legs(args, slots, W, H, D, B, stride, status, torch, hoh_ans, hd):
+    """N = 1 detail legs on the bench's own slots (contexts, streams, buffers), D slots of B images
+    in flight (the headline's calls), one set-up pass per slot, then --leg-steps timed steps,
+    lossless-checked afterwards:
       no_index_pipeline: the same synthetic images, encoded without recording a side index and
         decoded from the file alone (what a foreign .hoh gets: every stream one serial chain);
       natural_s0_pipeline: configs[4]'s natural-statistic image (seed --seed, generated into every
@@ -332,6 +367,8 @@ def extra_legs(args, slots, W, H, D, status, torch, hoh_ans, hd):
         choh's SHA."""
     out = {}
     K = max(1, args.leg_steps)
+    io = SlotIO(hoh_ans, W, H, B, stride)
+    img = W * H * 3
 
     def leg(inputs, use_index):
         idx = [hoh_ans.Index() if use_index else None for _ in range(D)]
@@ -339,14 +376,11 @@ def extra_legs(args, slots, W, H, D, status, torch, hoh_ans, hd):
         def enq(k, i):
             s = slots[k]
             with torch.cuda.stream(s.stream):
-                hoh_ans.encode_image_async(inputs[k], W, H, s.out, status[i, 0:2], ctx=s.ctx, index=idx[k])
-                hoh_ans.decode_image_async(s.out, s.out.numel(), W, H, s.dec, status[i, 2:4], ctx=s.ctx, index=idx[k])
+                io.encode(s, inputs[k], status[i], index=idx[k])
+                io.decode(s, status[i], index=idx[k])
 
         def chk(total):
-            st = status[:total].cpu().numpy()
-            for i in range(total):
-                hoh_ans.check_status(st[i, 0:2], "leg encode (step %d)" % i)
-                hoh_ans.check_status(st[i, 2:4], "leg decode (step %d)" % i)
+            io.check(status[:total].cpu().numpy(), total, "leg")
 
         hd.run_pipeline(D, D, enq, lambda k, i: None)
         torch.cuda.synchronize()
@@ -360,7 +394,7 @@ def extra_legs(args, slots, W, H, D, status, torch, hoh_ans, hd):
         el = time.perf_counter() - t
         ok = all(bool(torch.equal(slots[k].dec, inputs[k])) for k in range(D))
         n0 = int(status[min(status.shape[0], K) - 1 - ((min(status.shape[0], K) - 1) % D), 1].item())
-        return W * H * 3 * K / el / 1e6, ok, el / K * 1e3, n0
+        return img * B * K / el / 1e6, ok, el / K * 1e3, n0
 
     try:
         v, ok, ms, _ = leg([s.rgb for s in slots], False)
@@ -369,8 +403,11 @@ def extra_legs(args, slots, W, H, D, status, torch, hoh_ans, hd):
         out["no_index_pipeline_lossless"] = ok
     except Exception as e:      # reported, never silently replaced
         out["no_index_pipeline_error"] = repr(e)[:300]
+    nat = None
     try:
-        nat = [hoh_ans.natural_rgb_dev(W, H, args.seed, ctx=slots[k].ctx) for k in range(D)]
+        one = hoh_ans.natural_rgb_dev(W, H, args.seed, ctx=slots[0].ctx)
+        nat = [one.repeat(B) for _ in range(D)]
+        del one
         torch.cuda.synchronize()
         v, ok, ms, n0 = leg(nat, True)
         sha = hashlib.sha256(slots[0].out[:n0].cpu().numpy().tobytes()).hexdigest()
@@ -386,50 +423,52 @@ def extra_legs(args, slots, W, H, D, status, torch, hoh_ans, hd):
         for r in range(4):
             torch.cuda.synchronize()
             t = time.perf_counter()
-            _, n1, _ = hoh_ans.encode_image(nat[0], W, H, out_dev=s0.out, ctx=s0.ctx, index=ix)
+            _, n1, _ = hoh_ans.encode_image(nat[0][:img], W, H, out_dev=s0.out0, ctx=s0.ctx, index=ix)
             torch.cuda.synchronize()
             te.append(time.perf_counter() - t)
             t = time.perf_counter()
-            hoh_ans.decode_image(s0.out, n1, out_dev=s0.dec, ctx=s0.ctx, index=ix)
+            hoh_ans.decode_image(s0.out0, n1, out_dev=s0.dec0, ctx=s0.ctx, index=ix)
             torch.cuda.synchronize()
             tdl.append(time.perf_counter() - t)
         ms_e, ms_d = min(te[1:]) * 1e3, min(tdl[1:]) * 1e3
         out["natural_s0_single_enc_ms"] = round(ms_e, 3)
         out["natural_s0_single_dec_ms"] = round(ms_d, 3)
         out["natural_s0_single_MBps"] = round(W * H * 3 / (ms_e + ms_d) / 1e3, 1)
-        out["natural_s0_single_lossless"] = bool(torch.equal(s0.dec, nat[0]))
+        out["natural_s0_single_lossless"] = bool(torch.equal(s0.dec0, nat[0][:img]))
     except Exception as e:
         out["natural_s0_error"] = repr(e)[:300]
         nat = None
     if nat is not None and args.speed_legs:
-        out.update(speed_legs(args, slots, nat, W, H, D, status, torch, hoh_ans, hd))
+        out.update(speed_legs(args, slots, nat, W, H, D, B, stride, status, torch, hoh_ans, hd))
     del nat
-    out["legs_note"] = ("%d images in flight, one set-up pass per slot, then %d timed steps each; inputs resident "
-                        "in HBM" % (D, K))
+    out["legs_note"] = ("%d slots x %d image(s) in flight, one set-up pass per slot, then %d timed steps each; inputs "
+                        "resident in HBM" % (D, B, K))
     return out
 
 
-def speed_legs(args, slots, nat, W, H, D, status, torch, hoh_ans, hd):
+def speed_legs(args, slots, nat, W, H, D, B, stride, status, torch, hoh_ans, hd):
     """BASELINE configs[4] at the search speeds: the natural-statistic image (seed --seed in every
     slot) encoded at choh -s1..-s4 (full predictor search, layer_encode.hpp:122-319, and the
-    seek-distance LZ, lz.hpp:32-95 at 10..14), D images in flight, encode only (-s>=1 layers are
-    undecodable by construction), one set-up pass per slot, then --speed-leg-steps
-    timed steps.  EVERY slot's last file is SHA-compared with the reference choh's
-    (golden_natural.json); one image at a time: the best of 3 synchronous encodes on slot 0."""
+    seek-distance LZ, lz.hpp:32-95 at 10..14), D slots of B images in flight (a slot's B images run
+    one after another at -s>=1: hoh_encode_images_async batches -s0 only), encode only (-s>=1
+    layers are undecodable by construction), one set-up pass per slot, then
+    --speed-leg-steps timed steps.  EVERY image's last file is SHA-compared with the reference
+    choh's (golden_natural.json); one image at a time: the best of 3 synchronous encodes on slot 0."""
     out = {}
     K = max(1, args.speed_leg_steps)
+    io = SlotIO(hoh_ans, W, H, B, stride)
+    img = W * H * 3
     for speed in [int(x) for x in args.speed_legs.split(",") if x.strip()]:
         key = "natural_s%d" % speed
         try:
             def enq(k, i):
                 s = slots[k]
                 with torch.cuda.stream(s.stream):
-                    hoh_ans.encode_image_async(nat[k], W, H, s.out, status[i, 0:2], ctx=s.ctx, speed=speed)
+                    io.encode(s, nat[k], status[i], speed=speed)
 
             def chk(total):
                 st = status[:total].cpu().numpy()
-                for i in range(total):
-                    hoh_ans.check_status(st[i, 0:2], "%s encode (step %d)" % (key, i))
+                io.check(st, total, key, decode=False)
                 return st
 
             hd.run_pipeline(D, D, enq, lambda k, i: None)
@@ -448,19 +487,21 @@ def speed_legs(args, slots, nat, W, H, D, status, torch, hoh_ans, hd):
             g = golden_natural_sha(W, H, args.seed, speed)
             match, checked = 0, 0
             for k in range(min(D, steps)):
-                n_k = int(st[k + ((steps - 1 - k) // D) * D, 1])
-                checked += 1
-                match += g is not None and \
-                    hashlib.sha256(slots[k].out[:n_k].cpu().numpy().tobytes()).hexdigest() == g
+                row = k + ((steps - 1 - k) // D) * D
+                for b in range(B):
+                    n_k = int(st[row, 2 * b + 1])
+                    checked += 1
+                    o = slots[k].out[b * stride:b * stride + n_k]
+                    match += g is not None and hashlib.sha256(o.cpu().numpy().tobytes()).hexdigest() == g
             te = []
             for r in range(4):
                 torch.cuda.synchronize()
                 t = time.perf_counter()
-                _, n1, _ = hoh_ans.encode_image(nat[0], W, H, out_dev=slots[0].out, ctx=slots[0].ctx, speed=speed)
+                _, n1, _ = hoh_ans.encode_image(nat[0][:img], W, H, out_dev=slots[0].out0, ctx=slots[0].ctx, speed=speed)
                 torch.cuda.synchronize()
                 te.append(time.perf_counter() - t)
-            single_ok = g is not None and hashlib.sha256(slots[0].out[:n1].cpu().numpy().tobytes()).hexdigest() == g
-            out[key + "_MBps"] = round(W * H * 3 * K / el / 1e6, 1)
+            single_ok = g is not None and hashlib.sha256(slots[0].out0[:n1].cpu().numpy().tobytes()).hexdigest() == g
+            out[key + "_MBps"] = round(img * B * K / el / 1e6, 1)
             out[key + "_ms_per_step"] = round(el / K * 1e3, 3)
             out[key + "_file_bytes"] = n1
             out[key + "_slot_files_bit_exact"] = "%d of %d" % (match + single_ok, checked + 1)
@@ -469,8 +510,9 @@ def speed_legs(args, slots, nat, W, H, D, status, torch, hoh_ans, hd):
         except Exception as e:      # reported, never silently replaced
             out[key + "_error"] = repr(e)[:300]
     out["speed_legs_note"] = ("configs[4] natural 8192^2 image, choh -sN encode only (Q14: -s>=1 layers are "
-                              "undecodable), %d images in flight, %d timed steps per speed; every slot's file "
-                              "SHA-checked against the reference choh's (golden_natural.json)" % (D, K))
+                              "undecodable), %d slots x %d image(s) in flight, %d timed steps per speed; every "
+                              "image's file SHA-checked against the reference choh's (golden_natural.json)"
+                              % (D, B, K))
     return out
 
 
@@ -621,6 +663,12 @@ STRONG_SIDE, STRONG_SEED = 16384, 2     # configs[3]; seed 2 is the reference ch
 
 
 HW_QUEUE_CAP = 20
+DEFAULT_SLOTS, DEFAULT_BATCH = 4, 8       # N = 1: 4 streams x 8 images (r05 sweep)
+
+
+def hw_queue_note():
+    q = os.environ.get("GPU_MAX_HW_QUEUES")
+    return q if q else "4 (HIP default, GPU_MAX_HW_QUEUES unset)"
 
 
 def hw_queues_for(d):
@@ -643,10 +691,15 @@ def main():
     ap.add_argument("--strong", action="store_true", help="configs[3]: one size x size image sharded over N GPUs")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--noise", type=int, default=4)
-    ap.add_argument("--inflight", type=int, default=20, help="images in flight per GPU (1 = one at a time)")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="slots in flight per GPU (default: 4 at N = 1, each a batch of --batch images; 20 "
+                         "single images per GPU on the N > 1 path)")
     ap.add_argument("--hw-queues", type=int, default=0,
                     help="GPU_MAX_HW_QUEUES for this process (default: hw_queues_for(--inflight), at most 20)")
     ap.add_argument("--strong-inflight", type=int, default=8, help="images in flight per GPU in the 16384^2 leg")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="N = 1: images per slot and step (default %d) through the batched calls "
+                         "(hoh_*_images_async); 1: the single-image calls" % DEFAULT_BATCH)
     ap.add_argument("--no-index", action="store_true", help="decode without the side index (serial rANS)")
     ap.add_argument("--cpu-tiles", type=int, default=512)
     ap.add_argument("--cpu-procs", type=int, default=0,
@@ -665,6 +718,8 @@ def main():
     ap.add_argument("--speed-legs", default="1,2,3,4",
                     help="choh -sN speeds of the natural-image encode legs (configs[4]); empty: none")
     ap.add_argument("--speed-leg-steps", type=int, default=40, help="timed steps of each -sN leg")
+    ap.add_argument("--batch-only", action="store_true",
+                    help="N = 1: the timed batched leg alone (no one-in-flight / no-index / roofline detail)")
     ap.add_argument("--pmc-probe", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.size <= 0:
@@ -672,6 +727,11 @@ def main():
     if args.pmc_probe:
         pmc_probe(args)
         return
+    sharded0 = int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.sharded
+    if args.batch <= 0:
+        args.batch = 1 if sharded0 else DEFAULT_BATCH
+    if args.inflight <= 0:
+        args.inflight = 20 if (sharded0 or args.batch == 1) else DEFAULT_SLOTS
     D = max(1, args.inflight)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -688,12 +748,13 @@ def main():
         else:
             pmc, pmc_note = pmc_traffic_live(args)
 
-    # hardware queues (HIP reads this at runtime init): one per in-flight image up to HW_QUEUE_CAP;
-    # past that the images share queues evenly ("in-flight sweep": more than ~20 queues
-    # per process cost 15-30% of the throughput, however many images they carry)
+    # hardware queues (HIP reads GPU_MAX_HW_QUEUES at runtime init).  The batched N = 1 path runs
+    # at HIP's default (4 queues: nothing is set); the single-image paths (--batch 1, and the N > 1
+    # path) keep one queue per in-flight image up to HW_QUEUE_CAP, past that shared evenly
+    # ("in-flight sweep": more than ~20 queues per process cost 15-30%)
     if args.hw_queues > 0:
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, args.hw_queues))
-    else:
+    elif sharded0 or args.batch == 1:
         os.environ["GPU_MAX_HW_QUEUES"] = str(hw_queues_for(D))
 
     import torch
@@ -704,18 +765,21 @@ def main():
     dev = torch.device("cuda", local)
     if sharded:
         sharded_main(args, D, world, rank, dev, torch, hoh_ans, hd)
+    elif args.batch > 1 and args.batch_only:
+        batch_main(args, D, args.batch, dev, torch, hoh_ans, hd)
     else:
         single_main(args, D, dev, torch, hoh_ans, hd, pmc, pmc_note)
 
 
-def roofline_obj(kms, kavg, ratio, rows_raw, raw_total, K, el, pmc):
+def roofline_obj(kms, kavg, ratio, rows_raw, raw_total, K, el, pmc, B=1):
     """SURVEY 8(d)'s encode-side algorithmic bytes charged to one launch of the dominant kernel
-    (one launch = one image's or shard's encode): 3 B/px read + 3r B/px written = (1 + r) raw; the
-    design's own bytes (u16 residuals in + payload out) beside it as design_bytes."""
+    (one launch = one image's or shard's encode, as measured one image in flight): 3 B/px read +
+    3r B/px written = (1 + r) raw; the design's own bytes (u16 residuals in + payload out) beside
+    it as design_bytes.  The pipeline figure counts the B images of every step."""
     alg = int(round((1 + ratio) * rows_raw))
     design = 2 * rows_raw + int(round(ratio * rows_raw))
     achieved = alg / (kms * 1e-3) / 1e9 if kms else None
-    pipeline_gbs = 2 * (1 + ratio) * raw_total * K / el / 1e9
+    pipeline_gbs = 2 * (1 + ratio) * raw_total * B * K / el / 1e9
     traffic = pmc.get(DOM, {}).get("hbm_bytes") if pmc else None
     return {"bound": "hbm", "kernel": "k_rans_fast01 (" + DOM + ")",
             "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -729,6 +793,7 @@ def roofline_obj(kms, kavg, ratio, rows_raw, raw_total, K, el, pmc):
             "avg_launch_ms": round(kms, 4) if kms else None,
             "avg_launch_ms_source": "HIP events on the encoder's stream, one image in flight, 5 launches",
             "avg_launch_ms_under_load": round(kavg[DOM], 4) if DOM in kavg else None,
+            "images_per_launch_under_load": B,
             "pipeline_achieved": round(pipeline_gbs, 2), "pipeline_frac": round(pipeline_gbs / HBM_PEAK_GBS, 5),
             "pipeline_bytes_per_image": round(2 * (1 + ratio) * raw_total)}
 
@@ -829,27 +894,145 @@ def sharded_main(args, D, world, rank, dev, torch, hoh_ans, hd):
         sys.exit(3)
 
 
+def batch_main(args, D, B, dev, torch, hoh_ans, hd):
+    """N = 1 with --batch B > 1: D slots, each step one batch of B images (seeds args.seed + k*B ..,
+    contiguous in HBM) through hoh_encode_images_async + hoh_decode_images_async, whose kernels
+    cover the B images' tiles per launch (choh.cpp:464-500's tile loop over the batch): fewer,
+    larger launches on fewer streams, so the device fills without many hardware queues.  Every
+    image's file of each slot's last step is SHA-checked against the reference's
+    (golden_bench.json) and every image's decode against its input."""
+    L = hoh_ans.lib()
+    W = H = args.size
+    img = W * H * 3
+    stride = L.hoh_encode_bound(W, H)
+    K, warm = args.steps, args.warmup
+    status = torch.zeros((max(K, warm, D), 4 * B), dtype=torch.int64, device=dev)
+
+    class Slot:
+        def __init__(self, k):
+            self.seeds = [args.seed + k * B + b for b in range(B)]
+            self.ctx = hoh_ans.Context(dev.index)
+            self.stream = torch.cuda.Stream(device=dev)
+            self.rgb = torch.empty(B * img, dtype=torch.uint8, device=dev)
+            for b, sd in enumerate(self.seeds):
+                self.rgb[b * img:(b + 1) * img] = hoh_ans.synth_rgb_dev(W, H, sd, args.noise, ctx=self.ctx)
+            self.index = None if args.no_index else hoh_ans.Index()
+            self.out = torch.empty(B * stride, dtype=torch.uint8, device=dev)
+            self.dec = torch.empty(B * img, dtype=torch.uint8, device=dev)
+
+    slots = [Slot(k) for k in range(D)]
+    torch.cuda.synchronize()
+
+    def enqueue(k, i):
+        s = slots[k]
+        with torch.cuda.stream(s.stream):
+            hoh_ans.encode_images_async(s.rgb, B, W, H, s.out, stride, status[i, :2 * B], ctx=s.ctx, index=s.index)
+            hoh_ans.decode_images_async(s.out, B, stride, W, H, s.dec, status[i, 2 * B:], ctx=s.ctx, index=s.index)
+
+    def run(total):
+        hd.run_pipeline(D, total, enqueue, lambda k, i: None)
+
+    def check_status(total):
+        st = status[:total].cpu().numpy()
+        for i in range(total):
+            for b in range(B):
+                hoh_ans.check_status(st[i, 2 * b:2 * b + 2], "encode (step %d image %d)" % (i, b))
+                hoh_ans.check_status(st[i, 2 * B + 2 * b:2 * B + 2 * b + 2], "decode (step %d image %d)" % (i, b))
+        return st
+
+    run(D)
+    torch.cuda.synchronize()
+    check_status(D)
+    if warm:
+        run(warm)
+        torch.cuda.synchronize()
+        check_status(warm)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    run(K)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t
+    st = check_status(K)
+    bad_dec = [(k, b) for k, s in enumerate(slots) for b in range(B)
+               if not bool(torch.equal(s.dec[b * img:(b + 1) * img], s.rgb[b * img:(b + 1) * img]))]
+    lossless = not bad_dec
+    gb = golden_bench_shas(W, H, args.noise)
+    match, checked, nogold, comp, bad_sha = 0, 0, [], None, []
+    for k, s in enumerate(slots):
+        if k >= K:
+            continue
+        row = k + ((K - 1 - k) // D) * D
+        for b, sd in enumerate(s.seeds):
+            n_b = int(st[row, 2 * b + 1])
+            if comp is None:
+                comp = n_b
+            want = gb.get(sd)
+            if want is None:
+                nogold.append(sd)
+                continue
+            checked += 1
+            ok = hashlib.sha256(s.out[b * stride:b * stride + n_b].cpu().numpy().tobytes()).hexdigest() == want
+            match += ok
+            if not ok:
+                bad_sha.append((k, b, sd, n_b))
+    if bad_dec or bad_sha:
+        print("batch_main: lossless failures (slot, image) %s; SHA mismatches (slot, image, seed, size) %s"
+              % (bad_dec, bad_sha), file=sys.stderr)
+    value = B * img * K / el / 1e6
+    res = {
+        "metric": metric_name(), "value": round(value, 2), "unit": "MB/s", "n_gpus": 1, "steps": K, "warmup": warm,
+        "ms_per_step": round(el / K * 1e3, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u8", "data": "synthetic",
+        "config": {"workload": ("%dx%d synthetic RGB (gradient + triangular noise k=%d, seeds %d..%d), 256x256 tiles, "
+                                "choh -s0 encode + dhoh decode, %s, %d slot(s) x a batch of %d images per step "
+                                "(hoh_encode_images_async / hoh_decode_images_async)"
+                                % (W, H, args.noise, args.seed, args.seed + D * B - 1,
+                                   "side index" if not args.no_index else "serial decode", D, B)),
+                   "W": W, "H": H, "tiles": (W // 256) * (H // 256), "batch": B, "parallelism": "1 GPU"},
+        "detail": {"inflight_slots": D, "batch": B, "images_in_flight": D * B,
+                   "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0),
+                   "lossless": lossless, "compressed_bytes": comp,
+                   "slot_files_bit_exact": "%d of %d" % (match, checked),
+                   "slot_files_bit_exact_all": (match == checked and not nogold) if checked else None,
+                   "slot_files_no_golden_seeds": nogold},
+    }
+    print(json.dumps(res), flush=True)
+    if not lossless or match != checked:
+        sys.exit(3)
+
+
 def single_main(args, D, dev, torch, hoh_ans, hd, pmc, pmc_note):
-    """N = 1: D whole-image slots, enqueue-only encode + decode, no host round trip per step."""
+    """N = 1: D slots of B = --batch images each (B * D images in flight), enqueue-only encode +
+    decode, no host round trip per step.  B > 1: one step encodes and decodes the slot's B images
+    through the batched calls (hoh_encode_images_async / hoh_decode_images_async: every kernel
+    covers the B images' tiles); B = 1: the single-image calls."""
     L = hoh_ans.lib()
     W = H = args.size
     rows = H
     K = args.steps
     warm = args.warmup
-    status = torch.zeros((max(K, warm, D), 4), dtype=torch.int64, device=dev)
+    B = max(1, args.batch)
+    img = W * rows * 3
+    stride = L.hoh_encode_bound(W, rows)
+    status = torch.zeros((max(K, warm, D), 4 * B), dtype=torch.int64, device=dev)
 
     class Slot:
-        """One in-flight image: its own input (seed args.seed + k), library context (HIP stream +
-        workspaces), side index and output buffers."""
+        """B in-flight images (seeds args.seed + k*B .. + B-1, contiguous in HBM), one library
+        context (HIP stream + workspaces), side index and output buffers; rgb0 / out0 / dec0 are
+        the first image's views (one-in-flight measurements and the detail legs)."""
 
         def __init__(self, k):
-            self.seed = args.seed + k
+            self.seeds = [args.seed + k * B + b for b in range(B)]
+            self.seed = self.seeds[0]
             self.ctx = hoh_ans.Context(dev.index)
             self.stream = torch.cuda.Stream(device=dev)
-            self.rgb = hoh_ans.synth_rgb_dev(W, rows, self.seed, args.noise, ctx=self.ctx)
+            self.rgb = torch.empty(B * img, dtype=torch.uint8, device=dev)
+            for b, sd in enumerate(self.seeds):
+                self.rgb[b * img:(b + 1) * img] = hoh_ans.synth_rgb_dev(W, rows, sd, args.noise, ctx=self.ctx)
             self.index = None if args.no_index else hoh_ans.Index()
-            self.out = torch.empty(L.hoh_encode_bound(W, rows), dtype=torch.uint8, device=dev)
-            self.dec = torch.empty(W * rows * 3, dtype=torch.uint8, device=dev)
+            self.out = torch.empty(B * stride, dtype=torch.uint8, device=dev)
+            self.dec = torch.empty(B * img, dtype=torch.uint8, device=dev)
+            self.rgb0, self.out0, self.dec0 = self.rgb[:img], self.out[:stride], self.dec[:img]
             self.events = []
 
     slots = [Slot(k) for k in range(D)]
@@ -860,9 +1043,15 @@ def single_main(args, D, dev, torch, hoh_ans, hd, pmc, pmc_note):
         with torch.cuda.stream(s.stream):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            hoh_ans.encode_image_async(s.rgb, W, H, s.out, status[i, 0:2], ctx=s.ctx, index=s.index)
+            if B > 1:
+                hoh_ans.encode_images_async(s.rgb, B, W, H, s.out, stride, status[i, :2 * B], ctx=s.ctx, index=s.index)
+            else:
+                hoh_ans.encode_image_async(s.rgb, W, H, s.out, status[i, 0:2], ctx=s.ctx, index=s.index)
             e1.record()
-            hoh_ans.decode_image_async(s.out, s.out.numel(), W, H, s.dec, status[i, 2:4], ctx=s.ctx, index=s.index)
+            if B > 1:
+                hoh_ans.decode_images_async(s.out, B, stride, W, H, s.dec, status[i, 2 * B:], ctx=s.ctx, index=s.index)
+            else:
+                hoh_ans.decode_image_async(s.out, s.out.numel(), W, H, s.dec, status[i, 2:4], ctx=s.ctx, index=s.index)
             e2 = torch.cuda.Event(enable_timing=True)
             e2.record()
             s.events.append((e0, e1, e2))
@@ -873,8 +1062,9 @@ def single_main(args, D, dev, torch, hoh_ans, hd, pmc, pmc_note):
     def check_status(total):
         st = status[:total].cpu().numpy()
         for i in range(total):
-            hoh_ans.check_status(st[i, 0:2], "encode (step %d)" % i)
-            hoh_ans.check_status(st[i, 2:4], "decode (step %d)" % i)
+            for b in range(B):
+                hoh_ans.check_status(st[i, 2 * b:2 * b + 2], "encode (step %d image %d)" % (i, b))
+                hoh_ans.check_status(st[i, 2 * B + 2 * b:2 * B + 2 * b + 2], "decode (step %d image %d)" % (i, b))
         return int(st[total - 1, 1])
 
     for s in slots:
@@ -920,57 +1110,57 @@ def single_main(args, D, dev, torch, hoh_ans, hd, pmc, pmc_note):
         for _ in range(5):
             torch.cuda.synchronize()
             ta = time.perf_counter()
-            _, n0, _ = hoh_ans.encode_image(s0.rgb, W, H, out_dev=s0.out, ctx=s0.ctx, index=s0.index)
-            hoh_ans.decode_image(s0.out, n0, out_dev=s0.dec, ctx=s0.ctx, index=s0.index)
+            _, n0, _ = hoh_ans.encode_image(s0.rgb0, W, H, out_dev=s0.out0, ctx=s0.ctx, index=s0.index)
+            hoh_ans.decode_image(s0.out0, n0, out_dev=s0.dec0, ctx=s0.ctx, index=s0.index)
             s0.stream.synchronize()
             times.append(time.perf_counter() - ta)
         iso = {k: v[0] / v[1] for k, v in s0.ctx.kernel_stats().items() if v[1]}
         s0.ctx.profiling(False)
         single_ms = sorted(times)[len(times) // 2] * 1e3
         if not args.no_index:
-            noix = torch.empty_like(s0.dec)
+            noix = torch.empty_like(s0.dec0)
             times = []
             for _ in range(3):
                 s0.stream.synchronize()
                 ta = time.perf_counter()
-                hoh_ans.decode_image(s0.out, n0, out_dev=noix, ctx=s0.ctx, index=None)
+                hoh_ans.decode_image(s0.out0, n0, out_dev=noix, ctx=s0.ctx, index=None)
                 s0.stream.synchronize()
                 times.append(time.perf_counter() - ta)
             noix_ms = min(times) * 1e3
-            noix_ok = bool(torch.equal(noix, s0.rgb))
+            noix_ok = bool(torch.equal(noix, s0.rgb0))
             del noix
 
     # checks outside the timed region: every slot lossless, and EVERY slot's file (its last
     # timed step's) against the reference choh's sha256 for that slot's seed
     # (tests/golden/golden_bench.json, made by tests/golden/make_golden_bench.py)
     lossless = all(bool(torch.equal(s.dec, s.rgb)) for s in slots)
-    sha = hashlib.sha256(s0.out[:n0].cpu().numpy().tobytes()).hexdigest()
+    sha = hashlib.sha256(s0.out0[:n0].cpu().numpy().tobytes()).hexdigest()
     gb = golden_bench_shas(W, H, args.noise)
     st = status[:K].cpu().numpy()
     slot_match, slot_checked, slot_nogolden = 0, 0, []
     for k, s in enumerate(slots):
-        if k == 0:
-            n_k = n0                      # slot 0 was re-encoded by the one-in-flight leg (same image)
-        elif k < K:
-            n_k = int(st[k + ((K - 1 - k) // D) * D, 1])
-        else:
+        if k >= K:
             continue
-        want = gb.get(s.seed)
-        if want is None:
-            slot_nogolden.append(s.seed)
-            continue
-        slot_checked += 1
-        slot_match += hashlib.sha256(s.out[:n_k].cpu().numpy().tobytes()).hexdigest() == want
+        row = k + ((K - 1 - k) // D) * D          # the slot's last timed step
+        for b, sd in enumerate(s.seeds):
+            # image 0 of slot 0 was re-encoded by the one-in-flight leg (same image)
+            n_k = n0 if (k == 0 and b == 0) else int(st[row, 2 * b + 1])
+            want = gb.get(sd)
+            if want is None:
+                slot_nogolden.append(sd)
+                continue
+            slot_checked += 1
+            slot_match += hashlib.sha256(s.out[b * stride:b * stride + n_k].cpu().numpy().tobytes()).hexdigest() == want
     comp_total = n0
     raw_total = W * H * 3
-    value = raw_total * K / el / 1e6
+    value = raw_total * B * K / el / 1e6
     legs = {}
     if not args.no_legs:      # after the checks: the legs reuse the slots' buffers
-        legs = extra_legs(args, slots, W, H, D, status, torch, hoh_ans, hd)
+        legs = extra_legs(args, slots, W, H, D, B, stride, status, torch, hoh_ans, hd)
 
     kavg = {k: v[0] / v[1] for k, v in stats.items() if v[1]}
     ratio = comp_total / raw_total
-    roof = roofline_obj(iso.get(DOM) or None, kavg, ratio, W * rows * 3, raw_total, K, el, pmc)
+    roof = roofline_obj(iso.get(DOM) or None, kavg, ratio, W * rows * 3, raw_total, K, el, pmc, B)
     golden = golden_sha(W, H, args.seed, args.noise)
     res = {
         "metric": metric_name(),
@@ -986,16 +1176,22 @@ def single_main(args, D, dev, torch, hoh_ans, hd, pmc, pmc_note):
         "dtype": "u8",
         "data": "synthetic",
         "config": {
-            "workload": ("%dx%d synthetic RGB (gradient + triangular noise k=%d, seeds %d..%d: one image per "
-                         "slot), 256x256 tiles, choh -s0 encode + dhoh decode, %s, %d image(s) in flight per GPU"
-                         % (W, H, args.noise, args.seed, args.seed + D - 1,
-                            "side index" if not args.no_index else "serial decode", D)),
-            "W": W, "H": H, "tiles": (W // 256) * (H // 256), "per_gpu": "%dx%d" % (W, rows),
+            "workload": ("%dx%d synthetic RGB (gradient + triangular noise k=%d, seeds %d..%d: one image each), "
+                         "256x256 tiles, choh -s0 encode + dhoh decode, %s, %d slot(s) x %d image(s) per step "
+                         "(%s) = %d images in flight per GPU, %s hardware queues"
+                         % (W, H, args.noise, args.seed, args.seed + D * B - 1,
+                            "side index" if not args.no_index else "serial decode", D, B,
+                            "batched calls hoh_encode_images_async / hoh_decode_images_async" if B > 1 else
+                            "hoh_encode_image_async / hoh_decode_image_async", D * B, hw_queue_note())),
+            "W": W, "H": H, "tiles": (W // 256) * (H // 256), "per_gpu": "%dx%d" % (W, rows), "batch": B,
             "parallelism": "1 GPU",
         },
         "roofline": roof,
         "detail": {
-            "inflight": D,
+            "inflight": D * B,
+            "slots": D,
+            "batch": B,
+            "hw_queues": hw_queue_note(),
             "warmup_requested": args.warmup,
             "latency_ms_enc": round(t_enc / K * 1e3, 3),
             "latency_ms_dec": round(t_dec / K * 1e3, 3),
@@ -1026,7 +1222,7 @@ def single_main(args, D, dev, torch, hoh_ans, hd, pmc, pmc_note):
             res["detail"]["config2_single_stream"] = {"error": repr(e)[:300]}
     if not args.no_cpu_baseline:
         try:
-            res["cpu_baseline"] = cpu_baseline(s0.rgb.cpu().numpy(), W, H, args)
+            res["cpu_baseline"] = cpu_baseline(s0.rgb0.cpu().numpy(), W, H, args)
         except Exception as e:      # reported, never silently replaced
             res["cpu_baseline"] = {"value": None, "error": repr(e)[:300]}
     print(json.dumps(res), flush=True)

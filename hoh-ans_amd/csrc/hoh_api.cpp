@@ -17,8 +17,10 @@
 
 void launch_synth(uint8_t* rgb, int W, int H, int y0, uint64_t seed, int noise, hipStream_t s);
 void launch_natural(uint8_t* rgb, int W, int rows, int y0, uint64_t seed, hipStream_t s);
-void launch_put_bytes(uint8_t* dst, const uint8_t* b, int n, hipStream_t s);
+void launch_put_bytes(uint8_t* dst, const uint8_t* b, int n, hipStream_t s, int copies = 1, uint64_t stride = 0);
 void launch_status_enc(const uint32_t* gerr, const uint64_t* total, uint64_t cap, uint64_t* out, hipStream_t s);
+void launch_status_enc_batch(const uint32_t* gerr, const uint64_t* img_total, const uint32_t* img_err,
+                             uint64_t stride, uint64_t* out, int n, hipStream_t s);
 
 std::atomic<uint64_t> g_device_allocs{0};     // every hipMalloc this library makes
 
@@ -50,6 +52,8 @@ struct hoh_index {
   Buf streams;                  // IndexStream[]
   int nstreams = 0;
   size_t ck_count = 0;
+  int nimg = 1;                 // a batch's index: its image count and file stride (payload
+  uint64_t stride = 0;          //   offsets are absolute in the batch buffer)
 };
 
 struct Scratch {                // see ScratchFrame (hoh_dec.h)
@@ -363,7 +367,8 @@ static int ensure_log2_tables(hoh_ctx* c, int W, int H, EncodeJob& j) {
 static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int t0, int ntiles,
                              uint8_t* d_out, size_t cap, uint64_t prefix, int write_table,
                              uint32_t* d_tile_sizes, uint64_t* total_out, hoh_index* idx,
-                             hipStream_t s, int speed = 0, uint64_t* d_status = nullptr) {
+                             hipStream_t s, int speed = 0, uint64_t* d_status = nullptr, int nimg = 1,
+                             uint64_t out_stride = 0) {
   const bool async = d_status != nullptr;
   int xt, yt, tw, th;
   hoh_tiling(W, H, &xt, &yt, &tw, &th);
@@ -427,7 +432,7 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   if ((e = ensure(c->tab_fast, S * HOH_FAST_RANGE * sizeof(EncFast)))) return e;
   if ((e = ensure(c->tab_gen, S * 512 * sizeof(EncGen)))) return e;
   if ((e = ensure(c->slabs, nslab * 4))) return e;
-  if ((e = ensure(c->misc, 64))) return e;
+  if ((e = ensure(c->misc, 64 + (size_t)nimg * 16))) return e;   // gerr, total | batch: img_total[n], img_err[n]
   j.sym = (uint16_t*)c->sym.p;
   j.hist = (uint32_t*)c->hist.p;
   j.candbits = (uint64_t*)c->candbits.p;
@@ -456,10 +461,15 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   j.cap = cap;
   j.prefix = prefix;
   j.write_table = write_table;
+  j.nimg = nimg;
+  j.img_tiles = ntiles / nimg;
+  j.out_stride = out_stride;
+  j.img_total = (uint64_t*)((uint8_t*)c->misc.p + 64);
+  j.img_err = (uint32_t*)(j.img_total + nimg);
   // at -s0 k_front writes every candidate word of every tile (k_lz reads no others)
   if (speed &&
       hipMemsetAsync(j.candbits, 0, (size_t)ntiles * (j.npix_cap / 64) * 8, s) != hipSuccess) return HOH_E_HIP;
-  if (hipMemsetAsync(c->misc.p, 0, 64, s) != hipSuccess) return HOH_E_HIP;
+  if (hipMemsetAsync(c->misc.p, 0, 64 + (size_t)nimg * 16, s) != hipSuccess) return HOH_E_HIP;
   prof.mark("memset");
   launch_front(j, s);            prof.mark("front");
   launch_palette(j, s);          prof.mark("palette");
@@ -499,7 +509,8 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
     prof.mark("index");
   }
   if (async) {
-    launch_status_enc(j.gerr, j.total, cap, d_status, s);
+    if (nimg > 1) launch_status_enc_batch(j.gerr, j.img_total, j.img_err, out_stride, d_status, nimg, s);
+    else launch_status_enc(j.gerr, j.total, cap, d_status, s);
     return hipGetLastError() == hipSuccess ? HOH_OK : HOH_E_HIP;
   }
   if (hipMemcpyAsync(c->pinned, c->misc.p, 16, hipMemcpyDeviceToHost, s) != hipSuccess) return HOH_E_HIP;
@@ -609,6 +620,37 @@ int hoh_encode_image_async(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int s
   uint64_t total = 0;
   return encode_tiles_impl(c, d_rgb, W, H, 0, xt * yt, d_out, cap, hl, 1, nullptr, &total, speed ? nullptr : idx, s,
                            speed, d_status);
+}
+
+int hoh_encode_images_async(hoh_ctx* c, int n, const uint8_t* d_rgb, int W, int H, int speed, uint8_t* d_out,
+                            size_t stride, hoh_index* idx, uint64_t* d_status, void* stream) {
+  if (!c || n <= 0 || !d_rgb || !d_out || !d_status || W <= 0 || H <= 0 || speed < 0 || speed > 4) return HOH_E_ARG;
+  int xt, yt, tw, th;
+  if (!hoh_tiling(W, H, &xt, &yt, &tw, &th)) return HOH_E_UNSUPPORTED;
+  const size_t img_bytes = (size_t)W * H * 3;
+  if (n == 1 || speed || !batch_stacks(W, H)) {
+    // one image after another on the stream (same bytes); a side index holds one image only
+    if (idx && n > 1) return HOH_E_UNSUPPORTED;
+    for (int i = 0; i < n; i++) {
+      const int r = hoh_encode_image_async(c, d_rgb + i * img_bytes, W, H, speed, d_out + i * stride, stride, idx,
+                                           d_status + 2 * i, stream);
+      if (r) return r;
+    }
+    return HOH_OK;
+  }
+  if ((int64_t)H * n > (1ll << 30) || (int64_t)xt * yt * n > (1 << 24)) return HOH_E_ARG;
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick(c, stream);
+  uint8_t hb[32];
+  size_t hl = header_fixed(W, H, hb);
+  hb[hl++] = (uint8_t)(xt - 1);
+  hb[hl++] = (uint8_t)(yt - 1);
+  if (stride < hl) return HOH_E_CAP;
+  launch_put_bytes(d_out, hb, (int)hl, s, n, stride);
+  uint64_t total = 0;
+  const int r = encode_tiles_impl(c, d_rgb, W, H * n, 0, xt * yt * n, d_out, stride, hl, 1, nullptr, &total, idx, s,
+                                  0, d_status, n, stride);
+  return r;
 }
 
 int hoh_encode_image(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int speed, uint8_t* d_out, size_t cap,
@@ -818,11 +860,14 @@ int index_capture(hoh_index* idx, const EncodeJob& j, hipStream_t s) {
   if ((e = index_reserve(idx, (size_t)S, (size_t)S * per))) return e;
   idx->nstreams = S;
   idx->ck_count = (size_t)S * per;
+  idx->nimg = j.nimg > 1 ? j.nimg : 1;
+  idx->stride = j.nimg > 1 ? j.out_stride : 0;
   launch_index_capture(j, (IndexStream*)idx->streams.p, per, s);
   return hipGetLastError() == hipSuccess ? HOH_OK : HOH_E_HIP;
 }
 
 const IndexStream* index_streams(const hoh_index* idx) { return idx ? (const IndexStream*)idx->streams.p : nullptr; }
+int index_batch(const hoh_index* idx, uint64_t* stride) { if (stride) *stride = idx ? idx->stride : 0; return idx ? idx->nimg : 1; }
 const Checkpoint* index_ckpts(const hoh_index* idx) { return idx ? (const Checkpoint*)idx->ck.p : nullptr; }
 int index_nstreams(const hoh_index* idx) { return idx ? idx->nstreams : 0; }
 DecWork& ctx_dec(hoh_ctx* c) { return c->dec; }

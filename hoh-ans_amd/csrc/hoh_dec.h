@@ -50,6 +50,7 @@ void launch_index_capture(const EncodeJob& j, IndexStream* is, size_t per, hipSt
 const IndexStream* index_streams(const hoh_index* idx);
 const Checkpoint* index_ckpts(const hoh_index* idx);
 int index_nstreams(const hoh_index* idx);
+int index_batch(const hoh_index* idx, uint64_t* stride);    // images and file stride the index was recorded for
 DecWork& ctx_dec(hoh_ctx* c);
 hipStream_t ctx_stream(hoh_ctx* c, void* s);
 uint64_t* ctx_pinned(hoh_ctx* c);

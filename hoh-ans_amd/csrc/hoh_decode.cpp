@@ -10,6 +10,8 @@ int decode_image_impl(hoh_ctx* c, const uint8_t* d_in, size_t size, uint8_t* d_r
                       const hoh_index* idx, hipStream_t s);
 int decode_image_async_impl(hoh_ctx* c, const uint8_t* d_in, size_t size, int W, int H, uint8_t* d_rgb, size_t cap,
                             const hoh_index* idx, uint64_t* d_status, hipStream_t s);
+int decode_images_async_impl(hoh_ctx* c, int n, const uint8_t* d_in, size_t stride, int W, int H, uint8_t* d_rgb,
+                             const hoh_index* idx, uint64_t* d_status, hipStream_t s);
 int decode_tiles_impl(hoh_ctx* c, const uint8_t* d_blob, size_t size, int W, int H, int t0, int ntiles,
                       const uint32_t* h_sizes, uint8_t* d_rgb, const hoh_index* idx, hipStream_t s);
 int decode_tiles_async_impl(hoh_ctx* c, const uint8_t* d_blob, size_t size, int W, int H, int t0, int ntiles,
@@ -67,6 +69,13 @@ int hoh_decode_image_async(hoh_ctx* c, const uint8_t* d_hoh, size_t size, int W,
   if (!c || !d_hoh || !d_rgb || !d_status || W <= 0 || H <= 0) return HOH_E_ARG;
   (void)hipSetDevice(ctx_device(c));
   return decode_image_async_impl(c, d_hoh, size, W, H, d_rgb, cap, idx, d_status, ctx_stream(c, stream));
+}
+
+int hoh_decode_images_async(hoh_ctx* c, int n, const uint8_t* d_hoh, size_t stride, int W, int H, uint8_t* d_rgb,
+                            const hoh_index* idx, uint64_t* d_status, void* stream) {
+  if (!c || n <= 0 || !d_hoh || !d_rgb || !d_status || W <= 0 || H <= 0 || stride == 0) return HOH_E_ARG;
+  (void)hipSetDevice(ctx_device(c));
+  return decode_images_async_impl(c, n, d_hoh, stride, W, H, d_rgb, idx, d_status, ctx_stream(c, stream));
 }
 
 int hoh_decode_tiles(hoh_ctx* c, const uint8_t* d_blob, size_t size, int W, int H, int t0, int ntiles,

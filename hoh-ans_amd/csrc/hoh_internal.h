@@ -213,7 +213,22 @@ struct EncodeJob {
   uint64_t cap;
   uint64_t prefix;        // bytes before the tile size table (file header, written by the host)
   int write_table;        // write the n-1 tile size varints (a whole .hoh); 0 for a shard blob
+  // batch of images (hoh_encode_images_async): the job's image is the stack of nimg images of one
+  // shape (their tile rows follow each other), and each image's tiles form a file of their own
+  int nimg;               // images (1: one image or shard)
+  int img_tiles;          // tiles per image
+  uint64_t out_stride;    // bytes from one image's file to the next in out
+  uint64_t* img_total;    // [nimg] each file's bytes (nimg > 1; else *total)
+  uint32_t* img_err;      // [nimg] TF_* flags of each image's tiles (nimg > 1; else in gerr)
 };
+
+// A batch stacks when the image is tiled (choh.cpp:454-461) with tile rows of exactly 256: then
+// n images one after another in memory are the tiles of the n*H image (whose tiling is the same
+// 256-row grid), tile row for tile row.
+inline int batch_stacks(int W, int H) { return (W >= 512 || H >= 512) && W >= 256 && H >= 256 && H % 256 == 0; }
+
+// the image of tile t and the base of its file in out
+__host__ __device__ inline int tile_img(const EncodeJob& j, int t) { return j.nimg > 1 ? t / j.img_tiles : 0; }
 
 // arena offsets (elements / words): [tile][3] planes, [tile][3] LZ streams, [tile] indexed plane
 __host__ __device__ inline size_t idx_plane_off(const EncodeJob& j, int t) {

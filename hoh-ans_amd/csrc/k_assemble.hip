@@ -42,17 +42,21 @@ __device__ uint64_t block_excl_scan(uint64_t v, uint64_t* part, int tid) {
   return incl - v;
 }
 
+// One workgroup per file: blockIdx.x = the image of a batch (its tiles [tb, te), its file at
+// img * out_stride), else the one file / shard blob.
 __global__ __launch_bounds__(1024) void k_layout(EncodeJob j) {
   __shared__ uint64_t part[1024];
   __shared__ uint64_t tot_size, tot_vlen;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, img = blockIdx.x;
+  const int tb = j.nimg > 1 ? img * j.img_tiles : 0, te = j.nimg > 1 ? tb + j.img_tiles : j.ntiles;
+  const uint64_t fbase = j.nimg > 1 ? (uint64_t)img * j.out_stride : 0;
   if (tid == 0) { tot_size = 0; tot_vlen = 0; }
   __syncthreads();
   // pass 1: tile sizes and the table length
-  for (int base = 0; base < j.ntiles; base += 1024) {
+  for (int base = tb; base < te; base += 1024) {
     const int t = base + tid;
     uint64_t sz = 0, vl = 0;
-    if (t < j.ntiles) {
+    if (t < te) {
       TileInfo ti = j.tiles[t];
       const StreamInfo* st = j.streams + (size_t)t * j.spt;
       uint32_t bad = ti.flags & (TF_UNREPRODUCIBLE | TF_UNSUPPORTED | TF_OVERFLOW);
@@ -75,13 +79,13 @@ __global__ __launch_bounds__(1024) void k_layout(EncodeJob j) {
         if (ti.mode == 128) s64 += 1 + hoh_varint_len(L1) + hoh_varint_len(L2) + L1 + L2 + L3;   // :352-363
         else s64 += L1;                                                  // :335-338
       }
-      if (bad) atomicOr(j.gerr, (uint32_t)bad << 8);
+      if (bad) atomicOr(j.nimg > 1 ? j.img_err + img : j.gerr, j.nimg > 1 ? bad : (uint32_t)bad << 8);
       ti.lz_bytes = lzb;
       ti.size = (uint32_t)s64;
       j.tiles[t] = ti;
       sz = s64;
       if (j.tile_sizes) j.tile_sizes[t] = (uint32_t)s64;
-      if (j.write_table && t + 1 < j.ntiles) vl = hoh_varint_len(s64);
+      if (j.write_table && t + 1 < te) vl = hoh_varint_len(s64);
     }
     if (sz) atomicAdd((unsigned long long*)&tot_size, (unsigned long long)sz);
     if (vl) atomicAdd((unsigned long long*)&tot_vlen, (unsigned long long)vl);
@@ -90,12 +94,12 @@ __global__ __launch_bounds__(1024) void k_layout(EncodeJob j) {
   const uint64_t first = j.prefix + tot_vlen;
   // pass 2: offsets
   uint64_t carry_s = 0, carry_v = 0;
-  for (int base = 0; base < j.ntiles; base += 1024) {
+  for (int base = tb; base < te; base += 1024) {
     const int t = base + tid;
     uint64_t sz = 0, vl = 0;
-    if (t < j.ntiles) {
+    if (t < te) {
       sz = j.tiles[t].size;
-      if (j.write_table && t + 1 < j.ntiles) vl = hoh_varint_len(sz);
+      if (j.write_table && t + 1 < te) vl = hoh_varint_len(sz);
     }
     const uint64_t es = block_excl_scan(sz, part, tid);
     const uint64_t chunk_s = part[1023];
@@ -103,10 +107,10 @@ __global__ __launch_bounds__(1024) void k_layout(EncodeJob j) {
     const uint64_t ev = block_excl_scan(vl, part, tid);
     const uint64_t chunk_v = part[1023];
     __syncthreads();
-    if (t < j.ntiles) {
+    if (t < te) {
       TileInfo ti = j.tiles[t];
-      ti.off = first + carry_s + es;
-      ti.pad = (uint32_t)(j.prefix + carry_v + ev);     // where this tile's size varint goes
+      ti.off = fbase + first + carry_s + es;
+      ti.pad = (uint32_t)(j.prefix + carry_v + ev);     // where this tile's size varint goes (in its file)
       j.tiles[t] = ti;
       StreamInfo* st = j.streams + (size_t)t * j.spt;
       uint64_t o = ti.off + 3 + 1;
@@ -125,19 +129,33 @@ __global__ __launch_bounds__(1024) void k_layout(EncodeJob j) {
     carry_s += chunk_s;
     carry_v += chunk_v;
   }
-  if (tid == 0) *j.total = first + tot_size;
+  if (tid == 0) {
+    if (j.nimg > 1) j.img_total[img] = first + tot_size;
+    else *j.total = first + tot_size;
+  }
+}
+
+// a batch image's file is written only when it fits its stride and none of its tiles failed
+__device__ __forceinline__ bool file_ok(const EncodeJob& j, int t) {
+  if (*j.gerr) return false;
+  if (j.nimg <= 1) return *j.total <= j.cap;
+  const int img = tile_img(j, t);
+  return j.img_total[img] <= j.out_stride && !j.img_err[img];
 }
 
 __global__ __launch_bounds__(64) void k_tilebytes(EncodeJob j) {
   const int t = blockIdx.x * 64 + threadIdx.x;
-  if (t >= j.ntiles || *j.total > j.cap || *j.gerr) return;
+  if (t >= j.ntiles || !file_ok(j, t)) return;
   const TileInfo ti = j.tiles[t];
   const StreamInfo* st = j.streams + (size_t)t * j.spt;
   uint8_t* o = j.out + ti.off;
   o[0] = 0; o[1] = 0;                                  // 1x1 inner tiling (choh.cpp:115-116)
   o[2] = (uint8_t)ti.mode;                             // internal colour mode (:328)
   o[3] = 0x03;                                         // LZ flags (lz.hpp:98)
-  if (j.write_table && t + 1 < j.ntiles) hoh_write_varint(j.out, ti.pad, ti.size);   // choh.cpp:496-498
+  const int img = tile_img(j, t);
+  const bool last = j.nimg > 1 ? (t + 1) % j.img_tiles == 0 : t + 1 == j.ntiles;
+  if (j.write_table && !last)                          // choh.cpp:496-498
+    hoh_write_varint(j.out + (j.nimg > 1 ? (uint64_t)img * j.out_stride : 0), ti.pad, ti.size);
   if (ti.mode == 127) {                                // indexed layer header (layer_encode.hpp:57, :320-325)
     uint8_t* q = o + 3 + ti.lz_bytes;
     q[0] = 0x10; q[1] = 0; q[2] = 0; q[3] = 0x00; q[4] = 0x10;
@@ -157,7 +175,7 @@ __global__ __launch_bounds__(64) void k_tilebytes(EncodeJob j) {
 
 __global__ __launch_bounds__(256) void k_streambytes(EncodeJob j) {
   const int s = blockIdx.x, tid = threadIdx.x;
-  if (*j.total > j.cap || *j.gerr) return;
+  if (!file_ok(j, s / j.spt)) return;
   const StreamInfo st = j.streams[s];
   if (st.range == 0 || st.drop) return;
   uint8_t* o = j.out + st.out_off;
@@ -221,7 +239,7 @@ void launch_finalize(const EncodeJob& j, int nstreams, hipStream_t s, SidMap m) 
 }
 
 void launch_layout(const EncodeJob& j, hipStream_t s) {
-  hipLaunchKernelGGL(k_layout, dim3(1), dim3(1024), 0, s, j);
+  hipLaunchKernelGGL(k_layout, dim3(j.nimg > 1 ? j.nimg : 1), dim3(1024), 0, s, j);
 }
 
 void launch_assemble(const EncodeJob& j, int nstreams, hipStream_t s) {

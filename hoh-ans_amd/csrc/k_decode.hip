@@ -59,6 +59,8 @@ struct DecJob {
   int t0;                       // global index of the first tile (shard decode)
   const uint32_t* tsizes;       // shard decode: tile byte sizes instead of the file's table
   int blk_ok;                   // plane_cap holds the blocked layout of a 256-wide tile
+  int nimg, img_tiles;          // batch (hoh_decode_images_async): nimg files of img_tiles tiles, the
+  uint64_t in_stride;           //   image their stack, file i at in + i * in_stride (nimg <= 1: one file)
 };
 
 __device__ __forceinline__ uint64_t rd_varint(const uint8_t* b, uint64_t& p) {
@@ -111,40 +113,48 @@ __device__ __forceinline__ bool dec_abort(const DecJob& j) {
   return g_abort != 0;
 }
 
-// the .hoh prefix the caller's W, H imply (async decode): magic .. tiling bytes, <= 16 bytes
+// the .hoh prefix the caller's W, H imply (async decode): magic .. tiling bytes, <= 16 bytes;
+// a batch: every file's (one workgroup each)
 __global__ void k_dhdr(DecJob j, uint64_t lo, uint64_t hi, int n) {
   const int i = threadIdx.x;
   if (i >= n) return;
+  const uint64_t b = (uint64_t)blockIdx.x * j.in_stride + i;
   const uint8_t want = (uint8_t)((i < 8 ? lo >> (8 * i) : hi >> (8 * (i - 8))) & 255);
-  if ((uint64_t)i >= j.size || j.in[i] != want) atomicOr(j.gerr, 1u);
+  if (b >= j.size || j.in[b] != want) atomicOr(j.gerr, 1u);
 }
 
 // Tile table (dhoh.cpp:42-65): n-1 varints after the header give tile sizes.  Parallel parse:
 // a varint ends at a byte < 0x80, unless a run of >= 3 bytes >= 0x80 occurs (varint.hpp reads a
 // third byte whole), in which case thread 0 re-parses serially.  Shard decode (tsizes set)
 // takes the sizes from the caller instead.  Sizes are parked in tiles[i+1].off, then scanned.
+// One workgroup per file: a batch's file blockIdx.x holds tiles [ib, ib + nt) at in_stride * it.
 __global__ __launch_bounds__(1024) void k_dtable(DecJob j) {
   if (dec_abort(j)) return;
   __shared__ uint64_t wsum[17];
   __shared__ uint64_t tend;
   __shared__ int serial;
   const int tid = threadIdx.x;
-  const int nt = j.ntiles, nv = nt - 1;
+  const bool batch = j.nimg > 1;
+  const int ib = batch ? blockIdx.x * j.img_tiles : 0;
+  const int nt = batch ? j.img_tiles : j.ntiles, nv = nt - 1;
+  const uint64_t fb = batch ? (uint64_t)blockIdx.x * j.in_stride : 0;
+  const uint64_t fend = batch ? min((uint64_t)j.size, fb + j.in_stride) : (uint64_t)j.size;
+  DecTile* tiles = j.tiles + ib;
   for (int i = tid; i < nt; i += 1024) {
     DecTile t;
-    const int g = j.t0 + i;
+    const int g = j.t0 + ib + i;
     const int xo = (g % j.xt) * j.tw, yo = (g / j.xt) * j.th;
     t.x0 = xo; t.y0 = yo;
     t.w = min(j.tw, j.W - xo); t.h = min(j.th, j.H - yo);
     t.off = i == 0 ? 0 : (j.tsizes ? j.tsizes[i - 1] : 0);
     t.mode = 0; t.nmatch = 0; t.err = 0; t.pad = 0;
-    j.tiles[i] = t;
+    tiles[i] = t;
   }
-  if (tid == 0) { tend = j.prefix; serial = 0; }
+  if (tid == 0) { tend = fb + j.prefix; serial = 0; }
   __syncthreads();
   if (!j.tsizes && nv > 0) {
-    const uint64_t p0 = j.prefix;
-    const uint64_t end = min((uint64_t)j.size, p0 + 3ull * nv);
+    const uint64_t p0 = fb + j.prefix;
+    const uint64_t end = min(fend, p0 + 3ull * nv);
     uint64_t cnt = 0;
     for (uint64_t base = p0; base < end && cnt < (uint64_t)nv; base += 1024) {
       const uint64_t pos = base + tid;
@@ -161,7 +171,7 @@ __global__ __launch_bounds__(1024) void k_dtable(DecJob j) {
         uint64_t v = b;
         if (b2) v = ((uint64_t)(j.in[pos - 2] & 0x7f) << 14) + ((uint64_t)(j.in[pos - 1] & 0x7f) << 7) + b;
         else if (b1) v = ((uint64_t)(j.in[pos - 1] & 0x7f) << 7) + b;
-        j.tiles[idx + 1].off = v;
+        tiles[idx + 1].off = v;
         if (idx == (uint64_t)nv - 1) tend = pos + 1;
       }
       cnt += tot;
@@ -173,8 +183,8 @@ __global__ __launch_bounds__(1024) void k_dtable(DecJob j) {
       uint64_t p = p0;
       bool ok = true;
       for (int i = 0; i < nv; i++) {
-        if (p + 3 > j.size) { ok = false; break; }
-        j.tiles[i + 1].off = rd_varint(j.in, p);
+        if (p + 3 > fend) { ok = false; break; }
+        tiles[i + 1].off = rd_varint(j.in, p);
       }
       tend = p;
       if (!ok) atomicOr(j.gerr, 1u);
@@ -185,14 +195,14 @@ __global__ __launch_bounds__(1024) void k_dtable(DecJob j) {
   uint64_t carry = tend;
   for (int i0 = 0; i0 < nt; i0 += 1024) {
     const int i = i0 + tid;
-    const uint64_t v = i < nt ? j.tiles[i].off : 0;
+    const uint64_t v = i < nt ? tiles[i].off : 0;
     uint64_t tot;
     const uint64_t incl = block_scan_1024(v, wsum, &tot);
-    if (i < nt) j.tiles[i].off = carry + incl;     // tiles[0].off holds 0
+    if (i < nt) tiles[i].off = carry + incl;     // tiles[0].off holds 0
     carry += tot;
   }
   __syncthreads();
-  if (tid == 0 && j.tiles[nt - 1].off >= j.size) atomicOr(j.gerr, 1u);
+  if (tid == 0 && tiles[nt - 1].off >= fend) atomicOr(j.gerr, 1u);
 }
 
 // parse one entropy stream starting at byte p (all lanes, uniform control flow)
@@ -2320,7 +2330,7 @@ struct AsyncDec {              // enqueue-only decode: expected header bytes and
   uint64_t bytes;               // the status size word on success
 };
 static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s, const AsyncDec* as = nullptr);
-void launch_status_dec(const uint32_t* gerr, uint64_t bytes, uint64_t* out, hipStream_t s);
+void launch_status_dec(const uint32_t* gerr, uint64_t bytes, uint64_t* out, hipStream_t s, int n = 1);
 
 int decode_image_impl(hoh_ctx* c, const uint8_t* d_in, size_t size, uint8_t* d_rgb, size_t cap, int* Wp, int* Hp,
                       const hoh_index* idx, hipStream_t s) {
@@ -2387,6 +2397,51 @@ int decode_image_async_impl(hoh_ctx* c, const uint8_t* d_in, size_t size, int W,
   j.ntiles = j.xt * j.yt;
   j.in = d_in;
   j.size = size;
+  j.rgb = d_rgb;
+  return decode_run(c, j, idx, s, &as);
+}
+
+// enqueue-only decode of n W x H files at d_in + i * stride into n contiguous images (their stack:
+// one job, every kernel over all n files' tiles); {status, W*H*3} per image in d_status
+int decode_images_async_impl(hoh_ctx* c, int n, const uint8_t* d_in, size_t stride, int W, int H, uint8_t* d_rgb,
+                             const hoh_index* idx, uint64_t* d_status, hipStream_t s) {
+  if (!((W >= 512 || H >= 512) && W >= 256 && H >= 256)) return 6;
+  const size_t img = (size_t)W * H * 3;
+  if (n == 1 || !batch_stacks(W, H)) {
+    if (idx && n > 1) return 6;
+    for (int i = 0; i < n; i++) {
+      const int r = decode_image_async_impl(c, d_in + i * stride, stride, W, H, d_rgb + i * img, img, idx,
+                                            d_status + 2 * i, s);
+      if (r) return r;
+    }
+    return 0;
+  }
+  if ((int64_t)H * n > (1ll << 30)) return 1;
+  DecJob j;
+  memset(&j, 0, sizeof(j));
+  j.xt = W / 256; j.yt = H / 256;
+  j.tw = (W + j.xt - 1) / j.xt; j.th = (H + j.yt - 1) / j.yt;
+  uint8_t hb[16];
+  int p = 0;
+  hb[p++] = 153; hb[p++] = 72; hb[p++] = 79; hb[p++] = 72; hb[p++] = 2; hb[p++] = 8;   // choh.cpp:437-446
+  for (uint32_t v : {(uint32_t)W - 1, (uint32_t)H - 1}) p = (int)hoh_write_varint(hb, (uint32_t)p, v);
+  hb[p++] = (uint8_t)(j.xt - 1);
+  hb[p++] = (uint8_t)(j.yt - 1);
+  AsyncDec as;
+  as.hdr[0] = as.hdr[1] = 0;
+  for (int i = 0; i < p; i++) as.hdr[i / 8] |= (uint64_t)hb[i] << (8 * (i % 8));
+  as.hl = p;
+  as.status = d_status;
+  as.bytes = (uint64_t)img;
+  j.W = W; j.H = H * n;                           // the stack
+  j.yt *= n;
+  j.prefix = (uint64_t)p;
+  j.ntiles = j.xt * j.yt;
+  j.nimg = n;
+  j.img_tiles = j.ntiles / n;
+  j.in_stride = stride;
+  j.in = d_in;
+  j.size = (uint64_t)n * stride;
   j.rgb = d_rgb;
   return decode_run(c, j, idx, s, &as);
 }
@@ -2538,6 +2593,11 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   if ((e = dbuf(w, 15, (size_t)j.ntiles * j.th * ((j.tw + 15) & ~15) + 16, &q))) return e; j.bmap = (uint8_t*)q;
 #endif
   j.lz_xrow = lz_xrow();
+  if (idx) {                                   // a batch's index serves that batch's layout only
+    uint64_t st = 0;
+    const int ni = index_batch(idx, &st);
+    if (ni != (j.nimg > 1 ? j.nimg : 1) || (ni > 1 && st != j.in_stride)) return 1;
+  }
   j.ix = index_streams(idx);
   j.ck = index_ckpts(idx);
   j.nix = index_nstreams(idx);
@@ -2545,8 +2605,9 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   if (hipMemsetAsync(j.gerr, 0, 64, s) != hipSuccess) return 3;
   if (hipMemsetAsync(j.streams, 0, (size_t)S * sizeof(DecStream), s) != hipSuccess) return 3;
   ctx_mark(c, s, "start", as == nullptr);
-  if (as && as->hl) hipLaunchKernelGGL(k_dhdr, dim3(1), dim3(64), 0, s, j, as->hdr[0], as->hdr[1], as->hl);
-  hipLaunchKernelGGL(k_dtable, dim3(1), dim3(1024), 0, s, j);
+  const int nfile = j.nimg > 1 ? j.nimg : 1;
+  if (as && as->hl) hipLaunchKernelGGL(k_dhdr, dim3(nfile), dim3(64), 0, s, j, as->hdr[0], as->hdr[1], as->hl);
+  hipLaunchKernelGGL(k_dtable, dim3(nfile), dim3(1024), 0, s, j);
   ctx_mark(c, s, "dtable", false);
   hipLaunchKernelGGL(k_dparse, dim3(j.ntiles), dim3(64), 0, s, j);
   ctx_mark(c, s, "dparse", false);
@@ -2622,7 +2683,7 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
   ctx_mark(c, s, "dunpred", false);
   if (hipGetLastError() != hipSuccess) return 3;
   if (as) {
-    launch_status_dec(j.gerr, as->bytes, as->status, s);
+    launch_status_dec(j.gerr, as->bytes, as->status, s, j.nimg > 1 ? j.nimg : 1);
     return hipGetLastError() == hipSuccess ? 0 : 3;
   }
   uint64_t* pin = ctx_pinned(c);

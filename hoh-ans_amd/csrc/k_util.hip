@@ -34,10 +34,11 @@ void launch_synth(uint8_t* rgb, int W, int H, int y0, uint64_t seed, int noise, 
 
 // ---- enqueue-only API support (hoh_*_async): results are written by the stream, not read back
 
-// up to 16 bytes from kernel arguments into device memory (the .hoh header of an async encode)
-__global__ void k_put_bytes(uint8_t* dst, uint64_t lo, uint64_t hi, int n) {
+// up to 16 bytes from kernel arguments into device memory (the .hoh header of an async encode;
+// a batch: one copy per file, blockIdx.x * stride apart)
+__global__ void k_put_bytes(uint8_t* dst, uint64_t lo, uint64_t hi, int n, uint64_t stride) {
   const int i = threadIdx.x;
-  if (i < n) dst[i] = (uint8_t)((i < 8 ? lo >> (8 * i) : hi >> (8 * (i - 8))) & 255);
+  if (i < n) dst[blockIdx.x * stride + i] = (uint8_t)((i < 8 ? lo >> (8 * i) : hi >> (8 * (i - 8))) & 255);
 }
 
 // encoder status word -> {HOH status code, file bytes}: the mapping of encode_tiles_impl's
@@ -57,26 +58,49 @@ __global__ void k_status_enc(const uint32_t* gerr, const uint64_t* total, uint64
   out[1] = t;
 }
 
-// decoder error word -> {HOH status code, decoded bytes} (decode_run's epilogue)
-__global__ void k_status_dec(const uint32_t* gerr, uint64_t bytes, uint64_t* out) {
-  if (threadIdx.x) return;
-  const uint32_t g = gerr[0];
-  out[0] = g ? ((g & 2) ? 6 : 7) : 0;
-  out[1] = g ? 0 : bytes;
+// a batch: {code, file bytes} per image; the job's error word fails every image, an image's
+// tile flags and its stride only its own
+__global__ void k_status_enc_batch(const uint32_t* gerr, const uint64_t* img_total, const uint32_t* img_err,
+                                   uint64_t stride, uint64_t* out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t g = gerr[0], tf = img_err[i];
+  const uint64_t t = img_total[i];
+  uint64_t code = 0;
+  if (g) code = (g & 2) ? 4 : 3;
+  else if (tf) code = (tf & TF_UNREPRODUCIBLE) ? 5 : (tf & TF_UNSUPPORTED) ? 6 : 3;
+  else if (t > stride) code = 2;
+  out[2 * i] = code;
+  out[2 * i + 1] = t;
 }
 
-void launch_put_bytes(uint8_t* dst, const uint8_t* b, int n, hipStream_t s) {
+// decoder error word -> {HOH status code, decoded bytes} (decode_run's epilogue)
+// (a batch of n decodes: one {code, bytes} per image, the job's error word for all)
+__global__ void k_status_dec(const uint32_t* gerr, uint64_t bytes, uint64_t* out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t g = gerr[0];
+  out[2 * i] = g ? ((g & 2) ? 6 : 7) : 0;
+  out[2 * i + 1] = g ? 0 : bytes;
+}
+
+void launch_put_bytes(uint8_t* dst, const uint8_t* b, int n, hipStream_t s, int copies, uint64_t stride) {
   uint64_t w[2] = {0, 0};
   for (int i = 0; i < n && i < 16; i++) w[i / 8] |= (uint64_t)b[i] << (8 * (i % 8));
-  hipLaunchKernelGGL(k_put_bytes, dim3(1), dim3(64), 0, s, dst, w[0], w[1], n);
+  hipLaunchKernelGGL(k_put_bytes, dim3(copies), dim3(64), 0, s, dst, w[0], w[1], n, stride);
+}
+
+void launch_status_enc_batch(const uint32_t* gerr, const uint64_t* img_total, const uint32_t* img_err,
+                             uint64_t stride, uint64_t* out, int n, hipStream_t s) {
+  hipLaunchKernelGGL(k_status_enc_batch, dim3((n + 63) / 64), dim3(64), 0, s, gerr, img_total, img_err, stride, out, n);
 }
 
 void launch_status_enc(const uint32_t* gerr, const uint64_t* total, uint64_t cap, uint64_t* out, hipStream_t s) {
   hipLaunchKernelGGL(k_status_enc, dim3(1), dim3(64), 0, s, gerr, total, cap, out);
 }
 
-void launch_status_dec(const uint32_t* gerr, uint64_t bytes, uint64_t* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_status_dec, dim3(1), dim3(64), 0, s, gerr, bytes, out);
+void launch_status_dec(const uint32_t* gerr, uint64_t bytes, uint64_t* out, hipStream_t s, int n) {
+  hipLaunchKernelGGL(k_status_dec, dim3((n + 63) / 64), dim3(64), 0, s, gerr, bytes, out, n);
 }
 
 // ---- natural-statistic synthetic RGB (hoh_ans/natural.py, the same integer formula) ----------

@@ -87,6 +87,8 @@ def lib():
             ("hoh_decode_image_ix", [vp, vp, sz, vp, sz, ip, ip, vp, vp]),
             ("hoh_encode_image_async", [vp, vp, C.c_int, C.c_int, C.c_int, vp, sz, vp, vp, vp]),
             ("hoh_decode_image_async", [vp, vp, sz, C.c_int, C.c_int, vp, sz, vp, vp, vp]),
+            ("hoh_encode_images_async", [vp, C.c_int, vp, C.c_int, C.c_int, C.c_int, vp, sz, vp, vp, vp]),
+            ("hoh_decode_images_async", [vp, C.c_int, vp, sz, C.c_int, C.c_int, vp, vp, vp, vp]),
             ("hoh_encode_tiles_async", [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, sz, vp, vp, vp,
                                         vp]),
             ("hoh_decode_tiles_async", [vp, vp, sz, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, vp]),
@@ -201,7 +203,19 @@ def tiling(W, H):
 # ------------------------------------------------------------------ device-resident (torch) API
 
 def _stream_ptr(torch):
-    return vp(torch.cuda.current_stream().cuda_stream)
+    """torch's current stream as the call's stream.  torch's default stream is handle 0, which the
+    C ABI reads as "the context's own stream" (include/hoh_ans.h), a stream torch does not order
+    against: on it, torch's pending work is drained first (the call then sees the buffers torch
+    filled), and _after_call drains the library's work (torch then sees what the call wrote)."""
+    h = torch.cuda.current_stream().cuda_stream
+    if not h:
+        torch.cuda.synchronize()
+    return vp(h)
+
+
+def _after_call(torch):
+    if not torch.cuda.current_stream().cuda_stream:
+        torch.cuda.synchronize()
 
 
 class Index:
@@ -234,6 +248,7 @@ def encode_image(rgb_dev, W, H, out_dev=None, ctx=None, index=None, speed=0):
                                   out_dev.numel(), C.byref(n), C.byref(printed),
                                   index.h if index is not None else None, _stream_ptr(torch))
     check(r, "hoh_encode_image")
+    _after_call(torch)
     return out_dev, n.value, printed.value
 
 
@@ -250,6 +265,7 @@ def decode_image(hoh_dev, size, out_dev=None, ctx=None, index=None):
                                   out_dev.numel(), C.byref(w), C.byref(h),
                                   index.h if index is not None else None, _stream_ptr(torch))
     check(r, "hoh_decode_image")
+    _after_call(torch)
     return out_dev, w.value, h.value
 
 
@@ -263,6 +279,7 @@ def encode_image_async(rgb_dev, W, H, out_dev, status_dev, ctx=None, index=None,
                                      out_dev.numel(), index.h if index is not None else None,
                                      vp(status_dev.data_ptr()), _stream_ptr(torch))
     check(r, "hoh_encode_image_async")
+    _after_call(torch)
 
 
 def decode_image_async(hoh_dev, size, W, H, out_dev, status_dev, ctx=None, index=None):
@@ -274,6 +291,33 @@ def decode_image_async(hoh_dev, size, W, H, out_dev, status_dev, ctx=None, index
                                      out_dev.numel(), index.h if index is not None else None,
                                      vp(status_dev.data_ptr()), _stream_ptr(torch))
     check(r, "hoh_decode_image_async")
+    _after_call(torch)
+
+
+def encode_images_async(rgb_dev, n, W, H, out_dev, stride, status_dev, ctx=None, index=None, speed=0):
+    """Enqueue-only encode of a batch: n contiguous W x H images (rgb_dev, n*W*H*3 bytes) into n
+    files at out_dev + i*stride; status_dev: int64 tensor of 2n ({code, size} per image).  The
+    kernels cover the whole batch per launch (hoh_encode_images_async)."""
+    import torch
+    ctx = ctx or default_ctx()
+    assert out_dev.numel() >= n * stride and rgb_dev.numel() >= n * W * H * 3 and status_dev.numel() >= 2 * n
+    r = lib().hoh_encode_images_async(ctx.h, n, vp(rgb_dev.data_ptr()), W, H, speed, vp(out_dev.data_ptr()), stride,
+                                      index.h if index is not None else None, vp(status_dev.data_ptr()),
+                                      _stream_ptr(torch))
+    check(r, "hoh_encode_images_async")
+    _after_call(torch)
+
+
+def decode_images_async(hoh_dev, n, stride, W, H, out_dev, status_dev, ctx=None, index=None):
+    """Enqueue-only decode of n files at hoh_dev + i*stride into n contiguous images (out_dev)."""
+    import torch
+    ctx = ctx or default_ctx()
+    assert hoh_dev.numel() >= n * stride and out_dev.numel() >= n * W * H * 3 and status_dev.numel() >= 2 * n
+    r = lib().hoh_decode_images_async(ctx.h, n, vp(hoh_dev.data_ptr()), stride, W, H, vp(out_dev.data_ptr()),
+                                      index.h if index is not None else None, vp(status_dev.data_ptr()),
+                                      _stream_ptr(torch))
+    check(r, "hoh_decode_images_async")
+    _after_call(torch)
 
 
 def check_status(status, what):
@@ -296,6 +340,7 @@ def encode_tiles(rgb_dev, W, H, t0, ntiles, out_dev, sizes_dev, ctx=None, index=
                                      out_dev.numel(), vp(sizes_dev.data_ptr()), C.byref(n),
                                      index.h if index is not None else None, _stream_ptr(torch))
     check(r, "hoh_encode_tiles")
+    _after_call(torch)
     return n.value
 
 
@@ -308,6 +353,7 @@ def decode_tiles(blob_dev, size, W, H, t0, tile_sizes, out_dev, ctx=None, index=
     r = lib().hoh_decode_tiles(ctx.h, vp(blob_dev.data_ptr()), size, W, H, t0, ts.size, _p(ts), vp(base),
                                index.h if index is not None else None, _stream_ptr(torch))
     check(r, "hoh_decode_tiles")
+    _after_call(torch)
 
 
 def encode_tiles_async(rgb_dev, W, H, t0, ntiles, out_dev, sizes_dev, status_dev, ctx=None, index=None, row0=0,
@@ -321,6 +367,7 @@ def encode_tiles_async(rgb_dev, W, H, t0, ntiles, out_dev, sizes_dev, status_dev
                                      out_dev.numel(), vp(sizes_dev.data_ptr()), index.h if index is not None else None,
                                      vp(status_dev.data_ptr()), _stream_ptr(torch))
     check(r, "hoh_encode_tiles_async")
+    _after_call(torch)
 
 
 def decode_tiles_async(blob_dev, size, W, H, t0, ntiles, sizes_dev, out_dev, status_dev, ctx=None, index=None, row0=0):
@@ -333,6 +380,7 @@ def decode_tiles_async(blob_dev, size, W, H, t0, ntiles, sizes_dev, out_dev, sta
                                      vp(base), index.h if index is not None else None, vp(status_dev.data_ptr()),
                                      _stream_ptr(torch))
     check(r, "hoh_decode_tiles_async")
+    _after_call(torch)
 
 
 def file_prefix(W, H, tile_sizes):
@@ -359,6 +407,7 @@ def synth_rgb_dev(W, H, seed=1, noise=4, ctx=None, device="cuda", row0=0):
     t = torch.empty(W * H * 3, dtype=torch.uint8, device=device)
     check(lib().hoh_synth_rgb_rows(ctx.h, vp(t.data_ptr()), W, row0, H, seed, noise, _stream_ptr(torch)),
           "hoh_synth_rgb_rows")
+    _after_call(torch)
     return t
 
 
@@ -370,6 +419,7 @@ def natural_rgb_dev(W, H, seed=1, ctx=None, device="cuda", row0=0):
     t = torch.empty(W * H * 3, dtype=torch.uint8, device=device)
     check(lib().hoh_natural_rgb_rows(ctx.h, vp(t.data_ptr()), W, row0, H, seed, _stream_ptr(torch)),
           "hoh_natural_rgb_rows")
+    _after_call(torch)
     return t
 
 

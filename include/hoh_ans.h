@@ -122,6 +122,25 @@ int hoh_encode_image_async(hoh_ctx* ctx, const uint8_t* d_rgb, int W, int H, int
 int hoh_decode_image_async(hoh_ctx* ctx, const uint8_t* d_hoh, size_t size, int W, int H, uint8_t* d_rgb,
                            size_t cap, const hoh_index* idx, uint64_t* d_status, void* stream);
 
+/* ---- batched enqueue-only image path ------------------------------------------------------
+ * n images of one shape per call: each kernel of the image path covers the tiles of all n images
+ * in one launch (choh.cpp:464-500's tile loop, run over the batch), so a few streams -- and the
+ * few hardware queues HIP gives a process by default -- keep the device busy.  Images are
+ * contiguous (image i at d_rgb + i*W*H*3); file i is written at / read from d_hoh + i*stride
+ * (stride >= each file's size, e.g. hoh_encode_bound(W, H)).  d_status holds 2n u64, {status,
+ * size} per image as in the single-image calls: an image's own failures (HOH_E_CAP past its
+ * stride, HOH_E_UNREPRODUCIBLE, ...) mark only its slot; a failure of the job marks every slot.
+ * Files are byte-identical to the single-image calls'.  One side index serves the whole batch
+ * (payload positions are absolute in the batch buffer), so a decode with it needs the same n and
+ * stride (else HOH_E_ARG).  The batch runs as one job when its tiles stack -- H a multiple of 256,
+ * so the n images are the 256-row tile grid of one n*H image -- at -s0;
+ * otherwise the images run one after another on the stream (without a side index when n > 1:
+ * HOH_E_UNSUPPORTED). */
+int hoh_encode_images_async(hoh_ctx* ctx, int n, const uint8_t* d_rgb, int W, int H, int speed, uint8_t* d_out,
+                            size_t stride, hoh_index* idx, uint64_t* d_status, void* stream);
+int hoh_decode_images_async(hoh_ctx* ctx, int n, const uint8_t* d_hoh, size_t stride, int W, int H, uint8_t* d_rgb,
+                            const hoh_index* idx, uint64_t* d_status, void* stream);
+
 /* Host-side header parse: W, H and tiling of a .hoh (dhoh.cpp:320-366). */
 int hoh_peek_header(const uint8_t* hoh, size_t size, int* W, int* H, int* x_tiles, int* y_tiles);
 

@@ -1,6 +1,6 @@
 """Golden SHA-256 of every bench slot's file: the reference's own choh -s0 (compiled in place by
 oracle/ref/Makefile) on the deterministic 8192^2 synthetic image of each seed bench.py puts in
-flight (seeds 1..20, noise 4; slot k holds seed 1 + k).  bench.py compares every slot's file
+flight (seeds 1..40, noise 4: slot k holds seed 1 + k, or seeds 1 + k*B .. with --batch B).  bench.py compares every slot's file
 with these after the timed region.  ~7 s per seed on one core (run in parallel here).
 
     python tests/golden/make_golden_bench.py [--size S] [--seeds A B] [--jobs J]   (needs /root/reference)
