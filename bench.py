@@ -241,7 +241,11 @@ def cpu_baseline(rgb_host, W, H, args):
                     "tiles_skipped": sum(d.get("tiles_skipped", 0) for d in ds),
                     "wall_clock_MBps": round(raw / wall / 1e6, 3),
                     "wall_clock_note": "process start, band read and the LZ locate of ref_bench included",
-                    "ref_decode_mismatch_excl_last_row": bad})
+                    "ref_decode_mismatch_excl_last_row": bad,
+                    "ref_decode_note": "each tile decoded by the reference's decode_entropy + unpredict_all with its real "
+                                       "LZ back-reference map (oracle/ref/ref_bench.cpp lz_backref, outside the clock); "
+                                       "mismatch = decoded bytes that differ from the input, the last row excluded "
+                                       "(the reference decodes it with its non-MED edge rule, SURVEY Q9)"})
         # one thread on a bounded sample
         nt1 = min(args.cpu_tiles, ntiles)
         r = subprocess.run([exe, path, str(W), str(H), str(nt1), "0"], capture_output=True, text=True, timeout=600,

@@ -5,7 +5,10 @@
 // (entropy_decoding.hpp:134, unprediction.hpp:6) -- dhoh itself cannot be timed: it crashes on
 // every tiled file.  Prints one JSON line.  Single thread, like the reference; the
 // optional 5th argument (first tile) lets bench.py run one process per core on disjoint tile
-// ranges for the all-cores leg.  t_enc / t_dec cover encode_tile and the decode calls only: the
+// ranges for the all-cores leg.  The decode gets each tile's real back-reference map (lz_backref
+// below), so copied pixels decode as in dhoh.cpp:143-266 and the output is checked against the
+// input (mismatch_excl_last_row: the reference's unpredict_all decodes the last row with the
+// non-MED edge rule).  t_enc / t_dec cover encode_tile and the decode calls only: the
 // LZ locate below (find_lz_rgb, which finds where the planes start because the reference's
 // decode_entropy cannot skip a stream) is outside both clocks.  Only tiles whose
 // encode AND decode were timed (sub-green tiles) count in raw_bytes / t_enc / t_dec.
@@ -23,6 +26,29 @@
 #include "unprediction.hpp"
 
 static double now() { timespec t; clock_gettime(CLOCK_MONOTONIC, &t); return t.tv_sec + t.tv_nsec * 1e-9; }
+
+// The per-pixel back distance map the reference's decoder feeds unpredict_all (LEMPEL_BACKREF,
+// un_lz.hpp:150-170: 0 for predicted pixels, the copy's back distance for copied ones), rebuilt
+// from the same greedy walk as find_lz_rgb (lz.hpp:32-95 at seek distance 6: backs 1..64, no
+// vertical search), because the reference's own un_lz cannot read a tile's LZ streams back
+// (SURVEY Q1).  Outside the clocks, like the plane locate.
+static void lz_backref(const uint8_t* s, size_t size, int distance, int bonus, uint16_t* br) {
+  const int lim = 1 << distance;
+  for (size_t i = 0; i < size; i += 3) {
+    int longest = 0, best = -1;
+    for (int back = 1; back <= lim && (long)i - back * 3 >= 0; back++) {
+      int off = 0;
+      while (i + off * 3 + 2 < size && s[i + off * 3] == s[i - back * 3 + off * 3] &&
+             s[i + off * 3 + 1] == s[i - back * 3 + off * 3 + 1] && s[i + off * 3 + 2] == s[i - back * 3 + off * 3 + 2] &&
+             off < 259)
+        off++;
+      if (off > longest) { longest = off; best = back; if (off == 259) back = lim; }
+    }
+    if (longest < 4 + bonus) { br[i / 3] = 0; continue; }
+    for (int k = 0; k < longest; k++) br[i / 3 + k] = (uint16_t)best;
+    i += (size_t)(longest - 1) * 3;
+  }
+}
 
 int main(int argc, char** argv) {
   if (argc < 5) { fprintf(stderr, "usage: ref_bench in.rgb W H max_tiles [first_tile]\n"); return 1; }
@@ -76,6 +102,9 @@ int main(int argc, char** argv) {
       int depth[3] = {8, 9, 9};
       uint16_t* planes[3];
       uint16_t* br = new uint16_t[np]; memset(br, 0, np * 2);
+      const double c0 = now();
+      lz_backref(t, np * 3, 6, bonus, br);
+      c += now() - c0;                 // (kept out of the decode clock)
       for (int k = 0; k < 3; k++) {
         size_t bp = starts[k] + 5, cnt = 0;
         uint16_t* sym = decode_entropy(out, n, &bp, &cnt, 0);
