@@ -471,8 +471,12 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
       hipMemsetAsync(j.candbits, 0, (size_t)ntiles * (j.npix_cap / 64) * 8, s) != hipSuccess) return HOH_E_HIP;
   if (hipMemsetAsync(c->misc.p, 0, 64 + (size_t)nimg * 16, s) != hipSuccess) return HOH_E_HIP;
   prof.mark("memset");
+  // knob ENC_STOP = k (measurement, -s0): the encode stops after stage k (1 front, 2 palette, 3 LZ
+  // + nuke, 4 tables, 5 chains, 6 rANS generic + finalize, 7 layout + assembly); output invalid
+  const int stop = HOH_KNOB(ENC_STOP, 0);
   launch_front(j, s);            prof.mark("front");
-  launch_palette(j, s);          prof.mark("palette");
+  if (stop != 1) launch_palette(j, s);
+  prof.mark("palette");
   if (speed) {
     if (!c->side.s) {           // all three or none: a partial set is destroyed, never kept
       SideStream t;
@@ -490,17 +494,22 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
     if (hipGetLastError() != hipSuccess) return HOH_E_HIP;
     idx = nullptr;
   } else {
-    launch_lz(j, s);
-    launch_nuke(j, s);             prof.mark("lz");
-    launch_tables(j, (int)S, s);   prof.mark("tables");
+    if (!stop || stop > 2) { launch_lz(j, s); launch_nuke(j, s); }
+    prof.mark("lz");
+    if (!stop || stop > 3) launch_tables(j, (int)S, s);
+    prof.mark("tables");
     // the plane chains and the LZ streams (prob_bits 10) in one launch
-    launch_rans_fast01(j, s, ntiles * 4, SidMap{3, SK_G}, ntiles * 3, SidMap{1, SK_I}, ntiles * 3, SidMap{3, 0}, ntiles * 3,
-                       SidMap{0, 0});
+    if (!stop || stop > 4)
+      launch_rans_fast01(j, s, ntiles * 4, SidMap{3, SK_G}, ntiles * 3, SidMap{1, SK_I}, ntiles * 3, SidMap{3, 0},
+                         ntiles * 3, SidMap{0, 0});
     prof.mark("rans_enc_fast");
-    launch_rans_gen(j, (int)S, s); prof.mark("rans_enc_gen");
-    launch_finalize(j, (int)S, s); prof.mark("finalize");
-    launch_layout(j, s);           prof.mark("layout");
-    launch_assemble(j, (int)S, s); prof.mark("assemble");
+    if (!stop || stop > 5) { launch_rans_gen(j, (int)S, s); launch_finalize(j, (int)S, s); }
+    prof.mark("rans_enc_gen");
+    prof.mark("finalize");
+    if (!stop || stop > 6) { launch_layout(j, s); launch_assemble(j, (int)S, s); }
+    prof.mark("layout");
+    prof.mark("assemble");
+    if (stop) idx = nullptr;
   }
   if (hipGetLastError() != hipSuccess) return HOH_E_HIP;
   if (idx) {
