@@ -67,6 +67,7 @@ struct hoh_ctx {
   Scratch scr;
   hipStream_t own = nullptr;
   SideStream side;              // -s>=1: the LZ screen beside the predictor search (created on first use)
+  Buf dbg;                      // measurement builds (HOH_DEBUG_READ): per-tile kernel counters
   Buf idx8, fpb, pinfo, lg;     // -s>=1 workspaces (fpb: fingerprints, then the tile-major pixels)
   Buf lzs;                      // -s>=2: LZ posting lists (k_lzsort): sorted positions + ping-pong (then the sorted fingerprints) + ranks
   uint32_t lg_key[4] = {0, 0, 0, 0};
@@ -186,7 +187,7 @@ static void freebuf(Buf& b) { if (b.p) (void)hipFree(b.p); b.p = nullptr; b.n = 
 void hoh_ctx_destroy(hoh_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  Buf* all[] = {&c->idx8, &c->fpb, &c->lzs, &c->pinfo, &c->lg, &c->sym, &c->hist, &c->candbits, &c->matches, &c->lzspec, &c->pal, &c->streams, &c->tiles, &c->hdr,
+  Buf* all[] = {&c->dbg, &c->idx8, &c->fpb, &c->lzs, &c->pinfo, &c->lg, &c->sym, &c->hist, &c->candbits, &c->matches, &c->lzspec, &c->pal, &c->streams, &c->tiles, &c->hdr,
                 &c->tab_fast, &c->tab_gen, &c->slabs, &c->ckpt, &c->misc, &c->tsizes};
   for (Buf* b : all) freebuf(*b);
   for (Buf& b : c->scr.chunks) freebuf(b);
@@ -250,7 +251,8 @@ extern "C" int hoh_debug_read(hoh_ctx* c, int which, void* dst, size_t bytes) {
   }
   // 3: k_lzsort's posting lists of the last -s2..-s4 encode (sorted keys, sorted fingerprints,
   // u16 ranks: tools/scripts/lzsort_check.py); 4: the fingerprints + tile pixel words (k_lzfp)
-  const Buf& b = which == 0 ? c->matches : which == 3 ? c->lzs : which == 4 ? c->fpb : c->lzspec;
+  // 5: the per-tile kernel counters of the last encode (EncodeJob::dbg, [tile][64] u32)
+  const Buf& b = which == 0 ? c->matches : which == 3 ? c->lzs : which == 4 ? c->fpb : which == 5 ? c->dbg : c->lzspec;
   if (bytes > b.n || !b.p) return HOH_E_ARG;
   return hipMemcpy(dst, b.p, bytes, hipMemcpyDeviceToHost) == hipSuccess ? HOH_OK : HOH_E_HIP;
 }
@@ -403,12 +405,13 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   int e = HOH_OK;
   if (speed) {
     if ((e = ensure(c->idx8, (size_t)ntiles * j.npix_cap))) return e;
-    if ((e = ensure(c->fpb, (size_t)ntiles * j.npix_cap * 8))) return e;   // fingerprints + pixels
+    if ((e = ensure(c->fpb, (size_t)ntiles * j.npix_cap * 9))) return e;   // fingerprints + pixels + runs
     if ((e = ensure(c->pinfo, (size_t)ntiles * HOH_NPLANE_S * sizeof(PlaneInfo)))) return e;
     if ((e = ensure_log2_tables(c, W, H, j))) return e;
     j.idx8 = (uint8_t*)c->idx8.p;
     j.fpb = (uint32_t*)c->fpb.p;
     j.tpx = j.fpb + (size_t)ntiles * j.npix_cap;
+    j.run8 = (uint8_t*)(j.fpb + 2 * (size_t)ntiles * j.npix_cap);
     j.lzs = nullptr;
     j.lzrank = nullptr;
     // posting lists for the long LZ windows (-s2..-s4) of tiles whose positions fit 16 bits
@@ -454,6 +457,11 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
     if ((e = index_reserve(idx, S, nck))) return e;
     j.ckpt = index_ckpt_buf(idx);
   }
+#ifdef HOH_DEBUG_READ
+  if ((e = ensure(c->dbg, (size_t)ntiles * 64 * 4))) return e;
+  j.dbg = (uint32_t*)c->dbg.p;
+  if (hipMemsetAsync(j.dbg, 0, (size_t)ntiles * 64 * 4, s) != hipSuccess) return HOH_E_HIP;
+#endif
   j.gerr = (uint32_t*)c->misc.p;
   j.total = (uint64_t*)((uint8_t*)c->misc.p + 8);
   j.tile_sizes = d_tile_sizes;

@@ -189,6 +189,8 @@ struct EncodeJob {
   uint8_t* idx8;          // -s>=1: [tile][npix_cap] palette indices (the indexed plane's data)
   uint32_t* fpb;          // -s>=1: [tile][npix_cap] 4-pixel window fingerprints (LZ)
   uint32_t* tpx;          // -s>=1: [tile][npix_cap] the tile's pixels as u32 in tile raster order (LZ)
+  uint8_t* run8;          // -s>=1: [tile][npix_cap] length of the run of equal pixels from each position
+                          //   (tile raster order, 1..254 exact, 255 = at least 255)
   uint32_t* lzs;          // -s>=2, tiles <= 65536 px: [tile][npix_cap] positions grouped by hash16(fingerprint),
                           //   ascending inside a group: pos | hash << 16 (k_lzsort); null: no posting lists
   uint16_t* lzrank;       //   [tile][npix_cap] index of each position in lzs
@@ -207,6 +209,7 @@ struct EncodeJob {
   uint64_t slab_words;    // words in slabs (bounds of the encoder's indexed stores; 0 = unchecked)
   Checkpoint* ckpt;
   uint32_t* gerr;         // global error word
+  uint32_t* dbg;          // measurement builds only (HOH_DEBUG_READ): [tile][64] counters, else null
   uint64_t* total;        // total bytes of the tile blob
   uint32_t* tile_sizes;   // out: per tile bytes (may be null)
   uint8_t* out;           // output: [prefix bytes][tile size table][tiles]

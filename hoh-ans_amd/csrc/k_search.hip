@@ -749,21 +749,43 @@ __device__ __forceinline__ uint32_t fp4(uint32_t a, uint32_t b, uint32_t c, uint
 
 // fingerprint of the 4-pixel window starting at every position (0: fewer than 4 pixels left)
 // Also the tile's pixels as u32 in tile raster order (tpx): k_lzscan's ring fills and run lengths
-// read them as contiguous words instead of three bytes behind a division by the tile width.
+// read them as contiguous words instead of three bytes behind a division by the tile width.  And
+// run8[q]: how many pixels from q on equal pixel q (1..254, 255 = at least 255), from a bitmap of
+// the run ends over the chunk and the 259 positions after it (k_lzscan's run-length shortcut).
+#define LZFP_AHEAD 260
 __global__ __launch_bounds__(NT) void k_lzfp(EncodeJob j) {
-  __shared__ uint32_t px[NT + 3];
+  __shared__ uint32_t px[NT + LZFP_AHEAD];
+  __shared__ uint64_t ends[(NT + LZFP_AHEAD + 63) / 64];
   const int t = blockIdx.y;
   const TileInfo ti = j.tiles[t];
-  const uint32_t npix = (uint32_t)ti.w * ti.h, tid = threadIdx.x;
+  const uint32_t npix = (uint32_t)ti.w * ti.h, tid = threadIdx.x, lane = tid & 63;
   uint32_t* fo = j.fpb + (size_t)t * j.npix_cap;
   uint32_t* po = j.tpx + (size_t)t * j.npix_cap;
+  uint8_t* ro = j.run8 + (size_t)t * j.npix_cap;
+  constexpr uint32_t NP = NT + LZFP_AHEAD, NW = (NP + 63) / 64;
   for (uint32_t c0 = blockIdx.x * NT; c0 < npix; c0 += gridDim.x * NT) {
-    for (uint32_t k = tid; k < NT + 3; k += NT) px[k] = c0 + k < npix ? tile_px(j, ti, c0 + k) : 0u;
+    // past the tile: a word no pixel has (pixels are 24-bit), so the tile's last run ends there
+    for (uint32_t k = tid; k < NP; k += NT) px[k] = c0 + k < npix ? tile_px(j, ti, c0 + k) : 0xffffffffu;
+    __syncthreads();
+    for (uint32_t k0 = 0; k0 < NW * 64; k0 += NT) {
+      const uint32_t k = k0 + tid;
+      const uint64_t m = __ballot(k < NP && (k + 1 >= NP || px[k] != px[k + 1]));
+      if (lane == 0 && (k >> 6) < NW) ends[k >> 6] = m;
+    }
     __syncthreads();
     const uint32_t q = c0 + tid;
     if (q < npix) {
       po[q] = px[tid];
       fo[q] = q + 3 < npix ? fp4(px[tid], px[tid + 1], px[tid + 2], px[tid + 3]) : 0u;
+      // the first run end at or after tid (at most 255 positions on)
+      uint32_t e = 0xffffffffu;
+      for (uint32_t w = tid >> 6; w < NW && w <= ((tid + 255) >> 6); w++) {
+        uint64_t m = ends[w];
+        if (w == (tid >> 6)) m &= ~0ull << (tid & 63);
+        if (m) { e = w * 64 + (uint32_t)(__ffsll((unsigned long long)m) - 1); break; }
+      }
+      const uint32_t r = e - tid + 1;
+      ro[q] = (uint8_t)(r < 255 ? r : 255);
     }
     __syncthreads();
   }
@@ -1072,6 +1094,8 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
   const uint64_t* bits = j.candbits + (size_t)t * (j.npix_cap / 64);
   const uint32_t* F = j.fpb + (size_t)t * j.npix_cap;
   const uint32_t* TP = j.tpx + (size_t)t * j.npix_cap;
+  const uint8_t* R8 = j.run8 + (size_t)t * j.npix_cap;
+  uint32_t pq_cur = 0, rq_cur = 0;                                     // pixel q and its run (measure)
   uint32_t* mt = j.matches + (size_t)t * 3 * (j.lz_cap + 1);
   int bonus = 0;                                                      // choh.cpp:139-154
   if (ti.colours != -1) {
@@ -1103,6 +1127,19 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
   // it for b <= rp - 324 (and b <= limit); longer backs read the older side from the image
   const uint32_t reach = rp ? min((uint32_t)limit, (uint32_t)rp - 324u) : 0u;
   uint32_t wend = 0;
+#ifdef HOH_DEBUG_READ
+  // measurement builds: per-tile counters (EncodeJob::dbg; tools/scripts/lzscan_stats.py):
+  // 0 measures, 1 posting batches, 2 hits measured, 3 ring runs, 4 image runs, 5 ring round trips,
+  // 6 image round trips, 7 vertical runs, 8 measure cycles, 9 vertical cycles, 10 posting cycles,
+  // 11 wave cycles, 12 matches, 13 stitch measures, 14 next_cand cycles
+  auto dadd = [&](int k, uint32_t v) { if (j.dbg && lane == 0) atomicAdd(&j.dbg[(size_t)t * 64 + k], v); };
+  const uint64_t t_wave0 = __builtin_amdgcn_s_memtime();
+#define LZS_DBG(k, v) dadd(k, v)
+#define LZS_T() __builtin_amdgcn_s_memtime()
+#else
+#define LZS_DBG(k, v) ((void)0)
+#define LZS_T() 0ull
+#endif
   auto fill_to = [&](uint32_t lo, uint32_t need) {
     if (lo > wend) wend = lo & ~63u;
     while (wend < need) {
@@ -1120,7 +1157,9 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
     const uint32_t lim = min(259u, npix - q);
     uint32_t L = 0;
     if (rp && b <= reach) {
+      LZS_DBG(3, 1);
       for (;;) {
+        LZS_DBG(5, 1);
         // sixteen positions per LDS round trip from two bases (the mirror spares every read its
         // wrap), the first unequal one by two select chains
         const uint32_t* pa = pring + ((q + L) & rmask);
@@ -1140,8 +1179,17 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
       }
     } else {
       // backs beyond the ring (long ones, vertical ones past the window; every back without a
-      // ring): the older side from the tile's pixel words, sixteen positions per round trip
+      // ring): the older side from the tile's pixel words, sixteen positions per round trip.
+      // First the run lengths: both sides start with equal pixels c; where c's runs from q and from
+      // q - b differ in length the copy ends at the shorter (the longer side still holds c where
+      // the other has left it), so only equal runs (or runs of 255+) compare on, behind them.
+      LZS_DBG(4, 1);
+      if (TP[q - b] != pq_cur) return 0u;
+      const uint32_t rb = R8[q - b];
+      if (rb != rq_cur) return min(min(rb, rq_cur), lim);
+      L = min(rq_cur, lim);
       while (L < lim) {
+        LZS_DBG(6, 1);
         uint32_t a[16], c[16];
 #pragma unroll
         for (int u = 0; u < 16; u++) {
@@ -1183,6 +1231,10 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
   };
   // (longest, back) at candidate q as the key (L << 17) | (LZS_KB - b)
   auto measure = [&](uint32_t q) -> uint32_t {
+    [[maybe_unused]] const uint64_t tm0 = LZS_T();
+    LZS_DBG(0, 1);
+    pq_cur = TP[q];
+    rq_cur = R8[q];
     const uint32_t bm = q < (uint32_t)limit ? q : (uint32_t)limit;
     const uint32_t kmax = min(65536u, q) / w;                         // vertical: k * w <= min(65536, q)
     // one batch: f, the first 16 horizontal chunks, the vertical chunks
@@ -1206,6 +1258,7 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
     // walk.  Keys (L << 17) | (LZS_KB - b): L <= 259, b <= 65536 < LZS_KB.
     uint32_t mine = 0;
     bool done = false;
+    [[maybe_unused]] const uint64_t tp0 = LZS_T();
     if (post) {
       // posting list: q's hash group walked back from q's rank, 64 positions a batch (back
       // distances ascending); the batch in which the group or the window ends is the last
@@ -1221,6 +1274,8 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
         const uint64_t m = __ballot(hit);
         if (hit) hl[__popcll(m & lt)] = (uint16_t)(q - p);
         const uint32_t tot = (uint32_t)__popcll(m);
+        LZS_DBG(1, 1);
+        LZS_DBG(2, tot);
         bool top = false;
         for (uint32_t k = lane; k < tot; k += 64) {
           const uint32_t b = hl[k], L = runl(q, b);
@@ -1260,6 +1315,8 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
       done = __ballot(top) != 0;
     }
     uint32_t best = wave_max_u32(mine);
+    [[maybe_unused]] const uint64_t tv0 = LZS_T();
+    LZS_DBG(10, (uint32_t)(tv0 - tp0));
     // vertical (lz.hpp:54-74): whole rows up to 65536 back, strictly longer only
     if ((best >> 17) < 259) {
       uint32_t vmine = 0;
@@ -1271,6 +1328,7 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
           const uint32_t key = (runl(q, b) << 17) | (LZS_KB - b);
           if (key > vmine) vmine = key;
         }
+        LZS_DBG(7, (uint32_t)__popcll(__ballot(hit)));
       };
       uint32_t vh = 0;
 #pragma unroll
@@ -1282,6 +1340,8 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
       const uint32_t vb = wave_max_u32(vmine);
       if ((vb >> 17) > (best >> 17)) best = vb;
     }
+    LZS_DBG(9, (uint32_t)(LZS_T() - tv0));
+    LZS_DBG(8, (uint32_t)(LZS_T() - tm0));
     return best;
   };
   uint32_t nm = 0;
@@ -1317,6 +1377,8 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
       }
     }
     if (lane == 0) { s_cnt[wv] = cnt; s_exit[wv] = max(pos, hi); }
+    LZS_DBG(12, cnt);
+    LZS_DBG(11, (uint32_t)(LZS_T() - t_wave0));
   }
   if (nseg > 1) {
     __syncthreads();
@@ -1333,6 +1395,7 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
           const uint32_t q = next_cand(pos);
           if (q >= hi) { pos = hi; break; }
           if ((vis[q >> 5] >> (q & 31)) & 1) { conv = true; pos = q; break; }
+          LZS_DBG(13, 1);
           const uint32_t best = measure(q);
           const uint32_t longest = best >> 17, bb = LZS_KB - (best & LZS_KB);
           if (longest >= thr) { emit(q, longest, bb); pos = q + longest; }

@@ -3,6 +3,9 @@
 # the in-tree one of the same name) recompiled with extra FLAGS.  Usage: mkvar.sh NAME SRC.hip "FLAGS"
 set -e
 cd "$(dirname "$0")/../.."
+# the other objects come from build/ (the product build): bring them up to date first, so every
+# object of the variant was compiled against the same headers (struct layouts must agree)
+make -s -j8 >/dev/null
 name=$1; src=$2; flags=$3
 mkdir -p var build/var
 b=$(basename $src .hip)
