@@ -667,7 +667,7 @@ STRONG_SIDE, STRONG_SEED = 16384, 2     # configs[3]; seed 2 is the reference ch
 
 
 HW_QUEUE_CAP = 20
-DEFAULT_SLOTS, DEFAULT_BATCH = 4, 8       # N = 1: 4 streams x 8 images (r05 sweep, DESIGN.md section 4)
+DEFAULT_SLOTS, DEFAULT_BATCH = 4, 8       # N = 1: 4 streams x 8 images (r05 sweep, DESIGN.md section 5)
 
 
 def hw_queue_note():
@@ -755,7 +755,7 @@ def main():
     # hardware queues (HIP reads GPU_MAX_HW_QUEUES at runtime init).  The batched N = 1 path runs
     # at HIP's default (4 queues: nothing is set); the single-image paths (--batch 1, and the N > 1
     # path) keep one queue per in-flight image up to HW_QUEUE_CAP, past that shared evenly
-    # ("in-flight sweep": more than ~20 queues per process cost 15-30%)
+    # (docs/EXPERIMENTS.md, "in-flight sweep": more than ~20 queues per process cost 15-30%)
     if args.hw_queues > 0:
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, args.hw_queues))
     elif sharded0 or args.batch == 1:

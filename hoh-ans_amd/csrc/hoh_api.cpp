@@ -161,7 +161,7 @@ int hoh_ctx_create(hoh_ctx** out, int device) {
   if (hipSetDevice(device) != hipSuccess) return HOH_E_NODEV;
   {
     // More hardware queues than ~20 per process oversubscribe the device's queue slots: measured
-    // -15% at 24 and -28% at 28 images in flight, each on its own queue (in-flight
+    // -15% at 24 and -28% at 28 images in flight, each on its own queue (docs/EXPERIMENTS.md, in-flight
     // sweep).  HIP reads the variable once, before this library can act on it, so say it once.
     static std::atomic<int> warned{0};
     const char* q = getenv("GPU_MAX_HW_QUEUES");

@@ -386,7 +386,7 @@ void launch_rans_fast(const EncodeJob& j, int nplane, hipStream_t s, SidMap a, i
   // workgroup with a 56 KB LDS request (8 KB are used) caps the chains at two per CU and, alone,
   // spreads an image's 48 chains over 48 CUs.  The grid covers the chip with a per-launch rotation
   // so that the chains of images in flight land on different CUs.  (Measured alternatives:
-  // DESIGN.md §4.)
+  // docs/EXPERIMENTS.md §4.)
   const int nblk = (nplane + 63) / 64;
   // KIND 1 (LZ / map streams, the ladder's winners): short or few chains, no chip-wide grid
   const int grid = (nblk >= 1024 || kind == 1) ? nblk : 1024;

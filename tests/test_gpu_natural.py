@@ -151,7 +151,7 @@ def test_natural_8192_repeatable(hoh, speed):
     """The same image encoded again on the same context gives the same file (a race in the search
     or LZ kernels shows up as run-to-run differences; tools/scripts/rep_speed.py).  Round 4's
     differences came from k_lzsort's count reset racing the next chunk's count store (DESIGN.md
-    section 4, 'k_lzsort race'); tools/scripts/lzsort_check.py checks the posting lists directly."""
+    section 2); tools/scripts/lzsort_check.py checks the posting lists directly."""
     import torch
     d = hoh.natural_rgb_dev(8192, 8192, 1)
     shas = set()

@@ -1,5 +1,5 @@
 #!/bin/bash
-# The round-4 -s2..-s4 nondeterminism, reproduced on purpose ("k_lzsort race").
+# The round-4 -s2..-s4 nondeterminism, reproduced on purpose.
 # Builds (here, on the CPU) two debug libraries whose k_lzsort makes its last wave sleep ~13 us
 # before clearing the per-wave digit counts of a chunk:
 #   var/race_old.so  the round-4 k_lzsort (git 88ccbb2): every thread clears cnt[*][tid] after a
@@ -17,6 +17,7 @@ if [ "$1" = run ]; then
   exit 0
 fi
 mkdir -p var build/var
+make -s -j8 >/dev/null            # build/*.o current: the variants link them (same struct layouts)
 F="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Wno-unused-result -I hoh-ans_amd/csrc"
 git show 88ccbb2:hoh-ans_amd/csrc/k_search.hip > build/var/k_search_r4.hip
 # the same adversarial sleep, placed before the round-4 code's clear loop
