@@ -406,7 +406,7 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   if (speed) {
     if ((e = ensure(c->idx8, (size_t)ntiles * j.npix_cap))) return e;
     if ((e = ensure(c->fpb, (size_t)ntiles * j.npix_cap * 9))) return e;   // fingerprints + pixels + runs
-    if ((e = ensure(c->pinfo, (size_t)ntiles * HOH_NPLANE_S * sizeof(PlaneInfo)))) return e;
+    if ((e = ensure(c->pinfo, (size_t)ntiles * HOH_NPLANE_S * (sizeof(PlaneInfo) + 8 * 4)))) return e;   // + trial list
     if ((e = ensure_log2_tables(c, W, H, j))) return e;
     j.idx8 = (uint8_t*)c->idx8.p;
     j.fpb = (uint32_t*)c->fpb.p;
@@ -422,6 +422,7 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
       j.lzrank = (uint16_t*)((uint32_t*)c->lzs.p + 2 * per);
     }
     j.pinfo = (PlaneInfo*)c->pinfo.p;
+    j.trials = (uint32_t*)(j.pinfo + (size_t)ntiles * HOH_NPLANE_S);
   }
   if ((e = ensure(c->sym, nsym * 2 + 64))) return e;
   if ((e = ensure(c->hist, S * 512 * 4))) return e;
@@ -464,6 +465,7 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
 #endif
   j.gerr = (uint32_t*)c->misc.p;
   j.total = (uint64_t*)((uint8_t*)c->misc.p + 8);
+  j.ntrial = (uint32_t*)((uint8_t*)c->misc.p + 16);
   j.tile_sizes = d_tile_sizes;
   j.out = d_out;
   j.cap = cap;

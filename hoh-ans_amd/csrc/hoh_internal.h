@@ -88,8 +88,9 @@ struct StreamInfo {
   uint32_t ckpt_off;      // index of the first checkpoint of this stream
   uint32_t drop;          // coded but not part of the file (losing colour mode)
   uint32_t clip;          // nonzero: only the first clip bytes go to the file (Q15 prefix)
-  uint32_t sizeonly;      // rANS state chain only: words counted, none stored
+  uint32_t sizeonly;      // rANS state chain only: words counted, none stored (2: pruned, words = wlo)
   uint32_t hist_src;      // 0: count the symbols; k + 1: the histogram of stream k
+  uint32_t wlo, whi;      // size-only trials: bounds on words (k_tables, from the code length)
 };
 
 struct TileInfo {
@@ -195,6 +196,8 @@ struct EncodeJob {
                           //   ascending inside a group: pos | hash << 16 (k_lzsort); null: no posting lists
   uint16_t* lzrank;       //   [tile][npix_cap] index of each position in lzs
   PlaneInfo* pinfo;       // -s>=1: [tile][6]
+  uint32_t* trials;       // -s>=1 with ladder pruning: the sids of the trials k_prune_s keeps (else null)
+  uint32_t* ntrial;       // their count (zeroed per encode)
   const double* lg;       // -s>=1: -log2(k / n) for k = 0..n+1, one table per tile pixel count
   uint32_t lg_n[4];
   uint64_t lg_off[4];

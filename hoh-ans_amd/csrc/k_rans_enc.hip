@@ -194,12 +194,19 @@ __device__ __forceinline__ void rans_fast_body(const EncodeJob& j, int nplane, S
   asm volatile("s_setreg_imm32_b32 hwreg(HW_REG_MODE, 2, 2), 3");
   const int pi = blk * 64 + lane;
   if (pi >= nplane) return;
-  const uint32_t sid = plane_sid(pi, j.spt, ma, na, mb);
+  uint32_t sid;
+  if (KIND == 2 && j.trials) {             // the ladder trials k_prune_s kept, packed
+    if ((uint32_t)pi >= *j.ntrial) return;
+    sid = j.trials[pi];
+  } else {
+    sid = plane_sid(pi, j.spt, ma, na, mb);
+  }
   StreamInfo st = j.streams[sid];
   if (!st.fast || st.mode != SM_RANS || st.err || st.n == 0) return;
   // another launch's stream: KIND 0 real pb-15 encodes, 1 real encodes at other prob_bits, 2 every
   // size-only trial
   if ((KIND == 2) != (st.sizeonly != 0) || (KIND != 2 && (KIND == 0) != (st.pb == 15))) return;
+  if (st.sizeonly == 2) return;            // pruned trial (k_prune_s): its words are set
   const uint32_t n = st.n;
   const PbShape g{31u - st.pb, 1u << st.pb, 32u - st.pb};
   const char* tb = (const char*)j.tab_fast;
@@ -300,7 +307,7 @@ __global__ __launch_bounds__(64) void k_rans_gen(EncodeJob j, int nstreams, SidM
   if (i >= nstreams) return;
   const int sid = map_sid(sm, j.spt, i);
   StreamInfo st = j.streams[sid];
-  if (st.fast || st.mode != SM_RANS || st.err || st.n == 0) return;
+  if (st.fast || st.mode != SM_RANS || st.err || st.n == 0 || st.sizeonly == 2) return;
   const uint16_t* sp = j.sym + st.sym_off;
   const EncGen* tab = j.tab_gen + (size_t)sid * j.gen_stride;
   uint32_t* slab = j.slabs + st.slab_off;

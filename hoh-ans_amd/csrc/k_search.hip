@@ -258,43 +258,37 @@ __device__ double cell_cost_one(const uint16_t* D, int w, int h, int depth, int 
 // pass computes them once for all masks: with keys (|v - p_k| << 4) | k, the first least
 // predictor over all sixteen is the smallest key and over all but one index e the smallest key
 // other than e's, i.e. the smallest or the second smallest.  kMasks[4..13] are "all but e" for
-// e = 6, 1, 2, 3, 4, 5, 7, 9, the pair {0, 1} and all sixteen.  Per mask only the state differs:
-// its best predictors of the row above and of the left neighbour, the two picks, the residual
-// and its weight, summed in f64 in raster order exactly as cell_cost sums each mask (the weights
-// gathered one pixel ahead of their additions).  The walk's LDS state is dwords only: a version
-// with byte / u16 LDS stores (ds_write_b8 / b16, each lane's own bytes) changed files from run to
-// run (1 encode in 4 to 1 in 48 at -s3); with every LDS access a lane's whole dword, 172 encodes
-// at -s2..-s4 were identical (tools/scripts/rep_speed.py).
+// e = 6, 1, 2, 3, 4, 5, 7, 9, the pair {0, 1} and all sixteen.  So every mask's best predictor at a
+// pixel is one of three candidates: b1 (smallest key), b2 (second smallest) or kp (the pair's), and
+// which one follows from b1 alone.  The walk keeps the candidates, not per-mask predictors: one
+// LDS word per column holds the row-above value and its pixel's (b1, b2, kp) (4 bits each, all 4
+// before a cell's first row, the reference's initial best_pred), and a pixel picks six values
+// (the three candidates of the pixel above and of the left neighbour) instead of two per mask.
+// Per mask only the residual and its weight remain, summed in f64 in raster order exactly as
+// cell_cost sums each mask (the weights gathered one pixel ahead of their additions).  Every LDS
+// access is a lane's whole dword (byte / u16 stores of each lane's own bytes changed files from
+// run to run in round 4).
 #define WM_N 10
-__device__ __forceinline__ uint32_t wm_best(int m, uint32_t k1, uint32_t k2, uint32_t kp) {
-  const uint32_t b1 = k1 & 15u, b2 = k2 & 15u;
-  switch (m) {
-    case 0: return b1 == 6 ? b2 : b1;
-    case 1: return kp & 15u;
-    case 2: return b1 == 1 ? b2 : b1;
-    case 3: return b1 == 2 ? b2 : b1;
-    case 4: return b1 == 3 ? b2 : b1;
-    case 5: return b1 == 4 ? b2 : b1;
-    case 6: return b1 == 5 ? b2 : b1;
-    case 7: return b1 == 7 ? b2 : b1;
-    case 8: return b1 == 9 ? b2 : b1;
-    default: return b1;
-  }
+__device__ __forceinline__ uint32_t wm_excl(int m) {        // the index mask m excludes (m != 1, 9)
+  return m == 0 ? 6u : m <= 6 ? (uint32_t)(m - 1) : m == 7 ? 7u : 9u;
 }
-__device__ void cell_cost_multi(const uint16_t* D, int w, int h, int depth, int xt, int yt, int cx, int cy, int nf,
-                                const double* ent, uint32_t* top, uint32_t* bst, double* out) {
-  // top: this lane's word per column, [col][64 lanes]; bst: this lane's best predictors, eight
-  // 4-bit columns per word, [mask][col / 8][64 lanes] (dword accesses only)
+__device__ __forceinline__ uint32_t wm_pick(int m, uint32_t b1, uint32_t P1, uint32_t P2, uint32_t Pk) {
+  if (m == 1) return Pk;
+  if (m == 9) return P1;
+  return b1 == wm_excl(m) ? P2 : P1;
+}
+#define WM_INIT 0x04440000u                 // b1 = b2 = kp = 4
+template <int NF>
+__device__ void cell_cost_multi(const uint16_t* D, int w, int h, int depth, int xt, int yt, int cx, int cy,
+                                const double* ent, uint32_t* top, double* out) {
+  // top: this lane's word per column, [col][64 lanes]: value | b1 << 16 | b2 << 20 | kp << 24
   const int c = 1 << depth, half = c >> 1;
   const int tw = (w + xt - 1) / xt, th = (h + yt - 1) / yt;
   const int x0 = cx * tw, y0 = cy * th;
-  for (int i = 0; i < tw; i++) top[i * 64] = cy ? D[(long)y0 * w + x0 + i - w] : (uint32_t)half;
-  for (int m = 0; m < WM_N; m++)
-    if (m < nf)
-      for (int g = 0; g < (tw + 7) / 8; g++) bst[(m * 6 + g) * 64] = 0x44444444u;
-  double cost[WM_N], pend[WM_N], cost1[4], pend1[4];
+  for (int i = 0; i < tw; i++) top[i * 64] = WM_INIT | (cy ? D[(long)y0 * w + x0 + i - w] : (uint32_t)half);
+  double cost[NF], pend[NF], cost1[4], pend1[4];
 #pragma unroll
-  for (int m = 0; m < WM_N; m++) { cost[m] = 0.0; pend[m] = 0.0; }
+  for (int m = 0; m < NF; m++) { cost[m] = 0.0; pend[m] = 0.0; }
 #pragma unroll
   for (int m = 0; m < 4; m++) { cost1[m] = 0.0; pend1[m] = 0.0; }
   bool have = false;
@@ -308,73 +302,64 @@ __device__ void cell_cost_multi(const uint16_t* D, int w, int h, int depth, int 
     }
     const uint16_t* row = D + (long)(y0 + ym) * w + x0;
     const int vw = min(tw, w - x0);
-    uint32_t left[WM_N];
-#pragma unroll
-    for (int m = 0; m < WM_N; m++)
-      left[m] = m < nf ? (bst[(m * 6 + ((tw - 1) >> 3)) * 64] >> (((tw - 1) & 7) * 4)) & 15u : 0u;
+    uint32_t lw = top[(tw - 1) * 64];                                  // the left candidates
     const bool a4 = ym == 0, b4first = !(ym > 0 && vw == tw);
     uint32_t vn = vw > 0 ? row[0] : 0u;
     for (int xm = 0; xm < vw; xm++) {
       const uint32_t v = vn;
       if (xm + 1 < vw) vn = row[xm + 1];
-      const uint32_t T = top[xm * 64];
+      const uint32_t wa = top[xm * 64];
       const int xr = xm + 1 == tw ? 0 : xm + 1;
-      const uint32_t TR = top[xr * 64];
+      const uint32_t T = wa & 0xffffu, TR = top[xr * 64] & 0xffffu;
       Preds p;
       preds16(L, T, TL, TR, false, p);
-      uint32_t k1 = 0xffffffffu, k2 = 0xffffffffu;
+      uint32_t k1 = 0xffffffffu, k2 = 0xffffffffu, kp = 0u;
 #pragma unroll
       for (int k = 0; k < 16; k++) {
-        const uint32_t key = ((uint32_t)abs((int)v - (int)p.v[k]) << 4) | (uint32_t)k;
+        // |v - p_k| by v_sad_u16 (values < 2^16: the high halves are 0)
+        const uint32_t key = (__builtin_amdgcn_sad_u16(v, p.v[k], 0u) << 4) | (uint32_t)k;
         k2 = min(k2, max(k1, key));
         k1 = min(k1, key);
+        if (k == 1) kp = k1;                                            // the pair {0, 1}'s key
       }
-      const uint32_t kp = min(((uint32_t)abs((int)v - (int)p.v[0]) << 4), ((uint32_t)abs((int)v - (int)p.v[1]) << 4) | 1u);
       if (have) {
 #pragma unroll
-        for (int m = 0; m < WM_N; m++) cost[m] += pend[m];
+        for (int m = 0; m < NF; m++) cost[m] += pend[m];
 #pragma unroll
         for (int m = 0; m < 4; m++) cost1[m] += pend1[m];
       }
+      const uint32_t vc = v + (uint32_t)(half + c), cm = (uint32_t)(c - 1);
 #pragma unroll
       for (int m = 0; m < 4; m++) {
         const uint32_t pkm = p.v[m == 0 ? 0 : m == 1 ? 1 : m == 2 ? 5 : 4];
         const uint32_t pa = a4 ? p.v[4] : pkm, pb = (xm == 0 && b4first) ? p.v[4] : pkm;
-        const uint32_t r = ((uint32_t)((int)v - (int)midp(pa, pb) + half + c)) & (uint32_t)(c - 1);
-        pend1[m] = ent[r];
+        pend1[m] = ent[(vc - midp(pa, pb)) & cm];
       }
-      const uint32_t sh = (uint32_t)(xm & 7) * 4;
+      const uint32_t a1 = (wa >> 16) & 15u, l1 = (lw >> 16) & 15u;
+      const uint32_t PA1 = pick(p, a1), PA2 = pick(p, (wa >> 20) & 15u), PAk = pick(p, (wa >> 24) & 15u);
+      const uint32_t PB1 = pick(p, l1), PB2 = pick(p, (lw >> 20) & 15u), PBk = pick(p, (lw >> 24) & 15u);
 #pragma unroll
-      for (int m = 0; m < WM_N; m++) {
-        if (m < nf) {
-          uint32_t* bw = bst + (m * 6 + (xm >> 3)) * 64;
-          const uint32_t wd = *bw;
-          const uint32_t bA = (wd >> sh) & 15u, bB = left[m];
-          const uint32_t pr = midp(pick(p, bA), pick(p, bB));
-          const uint32_t r = ((uint32_t)((int)v - (int)pr + half + c)) & (uint32_t)(c - 1);
-          pend[m] = ent[r];
-          const uint32_t nb = wm_best(m, k1, k2, kp);
-          *bw = (wd & ~(15u << sh)) | (nb << sh);
-          left[m] = nb;
-        }
+      for (int m = 0; m < NF; m++) {
+        const uint32_t pr = midp(wm_pick(m, a1, PA1, PA2, PAk), wm_pick(m, l1, PB1, PB2, PBk));
+        pend[m] = ent[(vc - pr) & cm];
       }
+      lw = v | ((k1 & 15u) << 16) | ((k2 & 15u) << 20) | ((kp & 15u) << 24);
+      top[xm * 64] = lw;
       have = true;
       TL = T;
-      top[xm * 64] = v;
       L = v;
     }
   }
   if (have) {
 #pragma unroll
-    for (int m = 0; m < WM_N; m++) cost[m] += pend[m];
+    for (int m = 0; m < NF; m++) cost[m] += pend[m];
 #pragma unroll
     for (int m = 0; m < 4; m++) cost1[m] += pend1[m];
   }
 #pragma unroll
   for (int m = 0; m < 4; m++) out[m] = cost1[m];
 #pragma unroll
-  for (int m = 0; m < WM_N; m++)
-    if (m < nf) out[4 + m] = cost[m];
+  for (int m = 0; m < NF; m++) out[4 + m] = cost[m];
 }
 
 // channelpredict_all (prediction.hpp:153-229) at one pixel, fully parallel: the best predictors
@@ -424,40 +409,56 @@ __device__ __forceinline__ uint32_t resid_all(const AllCtx& a, int x, int y) {
 // slowest wave.  The full walk keeps the cell's top row and best predictors in LDS (8 KB per
 // wave: ~120 VGPRs, four waves per SIMD).  ncmax: cells of the largest plane (host, from the tile
 // size).
-// Task kinds: at -s2..-s4 one task per (plane, cell) walks every mask at once (cell_cost_multi:
-// natural 8192^2 -s3 101 -> 71 ms, -s4 109 -> 84 ms); at -s1, whose one full mask walks faster
-// alone (33 against 36 ms), a task per mask (cell_cost_one / cell_cost).  The multi walk's state
-// is in dynamic LDS (walk_lds), so -s1's walk keeps its occupancy.
+// Task kinds: at -s2..-s4 one task per (plane, cell) walks every mask at once (cell_cost_multi,
+// k_search_walk_multi: its state is one LDS word per column, 42 x 64 lanes = 10.5 KB per wave);
+// at -s1, whose one full mask walks faster alone, a task per mask (cell_cost_one / cell_cost).
 __host__ __device__ inline bool walk_multi(int npred) { return npred == 10 || npred == 14; }
 __host__ __device__ inline int walk_kinds(int npred) { return walk_multi(npred) ? 1 : npred; }
-static inline size_t walk_lds(int npred) { return walk_multi(npred) ? (42 + WM_N * 6) * 64 * 4 : 0; }
-__global__ __launch_bounds__(64) void k_search_walk(EncodeJob j, int npred, int ncmax) {
-  __shared__ uint16_t top[64][42];
-  __shared__ uint8_t bp[64][44];
-  extern __shared__ uint32_t wdyn[];                                  // cell_cost_multi: [42 + 60][64 lanes]
-  const int lane = threadIdx.x;
+#define WM_COLS 42
+struct WalkTask {
+  const uint16_t* D;
+  double* ent;
+  int w, h, depth, xt, yt, cell;
+};
+// task g of the (kind, plane, cell) space; false: nothing to walk
+__device__ __forceinline__ bool walk_task(const EncodeJob& j, int npred, int ncmax, uint64_t g, uint32_t& m, WalkTask& k) {
   const uint32_t npl = (uint32_t)j.ntiles * HOH_NPLANE_S;
-  const uint64_t g = (uint64_t)blockIdx.x * 64 + lane;
-  const uint32_t m = (uint32_t)(g / ((uint64_t)npl * ncmax));
-  if (m >= (uint32_t)walk_kinds(npred)) return;
+  m = (uint32_t)(g / ((uint64_t)npl * ncmax));
+  if (m >= (uint32_t)walk_kinds(npred)) return false;
   const uint32_t rem = (uint32_t)(g % ((uint64_t)npl * ncmax)), pl = rem / ncmax, cell = rem % ncmax;
   const int t = (int)(pl / HOH_NPLANE_S), p = (int)(pl % HOH_NPLANE_S);
   const TileInfo ti = j.tiles[t];
-  if (!plane_present(j, ti, p)) return;
-  const int w = ti.w, h = ti.h, depth = plane_depth(p);
-  const int xt = (w + 39) / 40, yt = (h + 39) / 40;
-  if (!(xt > 1 || yt > 1) || (int)cell >= xt * yt) return;
-  const uint16_t* D = j.sym + fin_plane_off(j, t, p);
-  double* ent = search_scr(j, (int)pl);
-  if (walk_multi(npred)) {
-    cell_cost_multi(D, w, h, depth, xt, yt, (int)cell % xt, (int)cell / xt, npred - 4, ent, wdyn + lane,
-                    wdyn + 42 * 64 + lane, ent + 512 + cell * 14);
-    return;
-  }
+  if (!plane_present(j, ti, p)) return false;
+  k.w = ti.w; k.h = ti.h; k.depth = plane_depth(p);
+  k.xt = (k.w + 39) / 40; k.yt = (k.h + 39) / 40;
+  if (!(k.xt > 1 || k.yt > 1) || (int)cell >= k.xt * k.yt) return false;
+  k.D = j.sym + fin_plane_off(j, t, p);
+  k.ent = search_scr(j, (int)pl);
+  k.cell = (int)cell;
+  return true;
+}
+__global__ __launch_bounds__(64) void k_search_walk(EncodeJob j, int npred, int ncmax) {
+  __shared__ uint16_t top[64][42];
+  __shared__ uint8_t bp[64][44];
+  const int lane = threadIdx.x;
+  uint32_t m;
+  WalkTask k;
+  if (!walk_task(j, npred, ncmax, (uint64_t)blockIdx.x * 64 + lane, m, k)) return;
   const uint32_t mk = kMasks[m];
-  ent[512 + cell * 14 + m] =
-      m < 4 ? cell_cost_one(D, w, h, depth, xt, yt, (int)cell % xt, (int)cell / xt, (uint32_t)__builtin_ctz(mk), ent)
-            : cell_cost(D, w, h, depth, xt, yt, (int)cell % xt, (int)cell / xt, mk, ent, top[lane], bp[lane]);
+  const int cx = k.cell % k.xt, cy = k.cell / k.xt;
+  k.ent[512 + k.cell * 14 + m] =
+      m < 4 ? cell_cost_one(k.D, k.w, k.h, k.depth, k.xt, k.yt, cx, cy, (uint32_t)__builtin_ctz(mk), k.ent)
+            : cell_cost(k.D, k.w, k.h, k.depth, k.xt, k.yt, cx, cy, mk, k.ent, top[lane], bp[lane]);
+}
+__global__ __launch_bounds__(64) void k_search_walk_multi(EncodeJob j, int npred, int ncmax) {
+  __shared__ uint32_t top[WM_COLS * 64];
+  const int lane = threadIdx.x;
+  uint32_t m;
+  WalkTask k;
+  if (!walk_task(j, npred, ncmax, (uint64_t)blockIdx.x * 64 + lane, m, k)) return;
+  const int cx = k.cell % k.xt, cy = k.cell / k.xt;
+  if (npred == 10) cell_cost_multi<6>(k.D, k.w, k.h, k.depth, k.xt, k.yt, cx, cy, k.ent, top + lane, k.ent + 512 + k.cell * 14);
+  else cell_cost_multi<10>(k.D, k.w, k.h, k.depth, k.xt, k.yt, cx, cy, k.ent, top + lane, k.ent + 512 + k.cell * 14);
 }
 
 // One workgroup per (tile, plane).  phase 0: the plane's data staged, the MED residuals'
@@ -521,23 +522,14 @@ __global__ __launch_bounds__(NT) void k_search(EncodeJob j, int phase, int pass)
     }
     __syncthreads();
   }
-  if (j.speed > 2 && pass == 0) {
-    // refine (:215-231): entropy of the first channelpredict_all residuals, then a second walk
-    for (int i = tid; i < 512; i += NT) S.hist[i] = 0;
-    __syncthreads();
-    for (uint32_t q = tid; q < npix; q += NT) {
-      const int y = (int)(q / (uint32_t)w), x = (int)(q - (uint32_t)y * w);
-      atomicAdd(&S.hist[resid_all(a, x, y)], 1u);
-    }
-    __syncthreads();
-    for (int i = tid; i < c; i += NT) ent[i] = lg[1 + S.hist[i]];
-    return;
-  }
-  // final channelpredict_all residuals, in place over the staged data: rows from the last up,
-  // each row read completely before it is overwritten (reads reach rows y-2..y only)
+  // channelpredict_all residuals over the staged data, rows from the last up.  Pass 0 of -s>=3
+  // (refine, :215-231) only counts them: the entropy of those residuals, then a second walk.  The
+  // final pass writes them in place: each row read completely before it is overwritten (reads
+  // reach rows y-2..y only).
   // Each row's best predictors are computed once: bnext holds row y's (from the previous
   // iteration; the last row's are 0, :214-216), bcur gets row y - 1's, so a pixel costs one
   // bp_all and one predictor set instead of resid_all's two and three.  w <= 1024 (hoh_api).
+  const bool refine = j.speed > 2 && pass == 0;
   uint8_t* bnext = S.brow[0];
   uint8_t* bcur = S.brow[1];
   for (int i = tid; i < w; i += NT) bnext[i] = 0;
@@ -569,7 +561,7 @@ __global__ __launch_bounds__(NT) void k_search(EncodeJob j, int phase, int pass)
     __syncthreads();
     n = 0;
     for (int x = tid; x < w && n < 4; x += NT) {
-      D[(long)y * w + x] = (uint16_t)rv[n];
+      if (!refine) D[(long)y * w + x] = (uint16_t)rv[n];
       atomicAdd(&S.hist[rv[n]], 1u);
       if (y >= 3) S.rows[(y - 3) & 3][x] = (uint16_t)nv[n];
       n++;
@@ -578,6 +570,10 @@ __global__ __launch_bounds__(NT) void k_search(EncodeJob j, int phase, int pass)
     uint8_t* const b = bnext;                                           // row y - 1 is next
     bnext = bcur;
     bcur = b;
+  }
+  if (refine) {
+    for (int i = tid; i < c; i += NT) ent[i] = lg[1 + S.hist[i]];
+    return;
   }
   for (int i = tid; i < 512; i += NT) fh[i] = S.hist[i];
   // predictor map: used masks and their order (:279-307)
@@ -1264,9 +1260,15 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
       // distances ascending); the batch in which the group or the window ends is the last
       const uint32_t hq = lzs_hash(f);
       const uint64_t lt = (1ull << lane) - 1;
-      for (int32_t i0 = (int32_t)PR[q] - 1; i0 >= 0 && !done; i0 -= 64) {
+      // the next batch's entries are loaded before this batch's hits are measured (prefetch)
+      int32_t i0 = (int32_t)PR[q] - 1;
+      uint32_t e_n = 0u, fe_n = ~f;
+      if (i0 - lane >= 0) { e_n = PS[i0 - lane]; fe_n = PF[i0 - lane]; }
+      for (; i0 >= 0 && !done; i0 -= 64) {
         const int32_t i = i0 - lane;
-        const uint32_t e = i >= 0 ? PS[i] : 0u, fe = i >= 0 ? PF[i] : ~f;
+        const uint32_t e = e_n, fe = fe_n;
+        e_n = 0u; fe_n = ~f;
+        if (i >= 64) { e_n = PS[i - 64]; fe_n = PF[i - 64]; }
         const uint32_t p = e & 0xffffu;
         const bool inside = i >= 0 && (e >> 16) == hq && q - p <= bm;
         const uint64_t inm = __ballot(inside);
@@ -1322,7 +1324,8 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
       uint32_t vmine = 0;
       auto vchunk = [&](uint32_t k, uint32_t fk) {
         const uint32_t b = k * w;
-        const bool hit = k <= kmax && fk == f;
+        // b <= bm was measured by the horizontal walk: not strictly longer there, skipped
+        const bool hit = k <= kmax && b > bm && fk == f;
         if (!__ballot(hit)) return;
         if (hit) {
           const uint32_t key = (runl(q, b) << 17) | (LZS_KB - b);
@@ -1514,6 +1517,55 @@ __global__ __launch_bounds__(128) void k_setup_s(EncodeJob j) {
     }
   }
   j.streams[sid] = st;
+}
+
+// The prob_bits ladder (layer_encode.hpp:326-398) needs a trial's exact size only where it can
+// change the decision.  From k_tables' word bounds, per plane: t1 / t2 (prob_bits 16 / 15) when
+// their order is uncertain; then, in each branch that can be taken, the trials whose lower bound
+// is <= U = min(the depth bound, the branch trials' upper bounds).  U is at least the smallest
+// value the ladder compares, so a trial above it can never be that minimum: if it comes before
+// the minimum, whatever it sets is overwritten by the minimum's own update (strictly smaller),
+// and after it, it updates nothing.  Such a trial is not encoded: its words are set to the lower
+// bound (still above U, and on the certain side of a decided t1 / t2 order), sizeonly = 2.  The
+// files are those of the full ladder.
+__device__ __forceinline__ uint64_t trial_size(const StreamInfo& v, uint32_t words) {   // k_finalize's size
+  const uint64_t rb = (uint64_t)words * 4, es = v.hdr_len + hoh_varint_len(rb) + rb;
+  return v.expected_stored < es ? v.expected_stored : es;
+}
+__global__ __launch_bounds__(64) void k_prune_s(EncodeJob j) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= j.ntiles * HOH_NPLANE_S) return;
+  const int t = i / HOH_NPLANE_S, p = i % HOH_NPLANE_S;
+  const PlaneInfo pi = j.pinfo[i];
+  if (!pi.present) return;
+  const TileInfo ti = j.tiles[t];
+  StreamInfo* v = j.streams + (size_t)t * SPT_S + KS_VAR + p * 8;
+  uint64_t lo[8], hi[8];
+  for (int k = 0; k < 8; k++) {
+    if (v[k].mode != SM_RANS || !v[k].fast || v[k].err || v[k].sizeonly != 1 || v[k].whi < v[k].wlo || v[k].wlo < 2) {
+      for (int a = 0; a < 8; a++)                                    // not a plain trial: keep them all
+        j.trials[atomicAdd(j.ntrial, 1u)] = (uint32_t)(t * SPT_S + KS_VAR + p * 8 + a);
+      return;
+    }
+    lo[k] = trial_size(v[k], v[k].wlo);
+    hi[k] = trial_size(v[k], v[k].whi);
+  }
+  const uint64_t n = (uint64_t)ti.w * ti.h;
+  const uint64_t dbound = (pi.depth * n + (pi.depth * n) % 8 + 1024) / 8;   // k_choose_s' first `possible`
+  const bool surelyA = hi[0] < lo[1], surelyB = lo[0] >= hi[1];
+  uint32_t need = (!surelyA && !surelyB) ? 3u : 0u;
+  for (int br = 0; br < 2; br++) {
+    if (br == 0 ? surelyB : surelyA) continue;                        // branch not taken
+    const int ks[4] = {br, br ? 5 : 2, br ? 6 : 3, br ? 7 : 4};
+    uint64_t U = dbound;
+    for (int a = 0; a < 4; a++) U = hi[ks[a]] < U ? hi[ks[a]] : U;
+    for (int a = 0; a < 4; a++)
+      if (lo[ks[a]] <= U) need |= 1u << ks[a];
+  }
+  for (int k = 0; k < 8; k++) {
+    if ((need >> k) & 1) j.trials[atomicAdd(j.ntrial, 1u)] = (uint32_t)(t * SPT_S + KS_VAR + p * 8 + k);
+    else { v[k].sizeonly = 2; v[k].words = v[k].wlo; }
+  }
 }
 
 // layer_encode.hpp:22, :115-120, :326-398 on the stream sizes
@@ -1736,6 +1788,7 @@ __global__ __launch_bounds__(64) void k_tilebytes_s(EncodeJob j) {
 
 // ---------------------------------------------------------------- orchestration
 
+static int ladder_prune() { return HOH_KNOB(LADDER_PRUNE, 1); }   // knob LADDER_PRUNE=0: every trial encoded
 static int lzs_ring_max() { return HOH_KNOB(LZS_RING_MAX, 2048); }
 static int lzs_seg() { const int n = HOH_KNOB(LZS_SEG, LZS_SEG); return n < 1 ? 1 : n > LZS_SEG ? LZS_SEG : n; }
 
@@ -1790,7 +1843,8 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, v
     const dim3 gs(j.ntiles * HOH_NPLANE_S), gw((unsigned)((ntask + 63) / 64));
     hipLaunchKernelGGL(k_search, gs, dim3(NT), sizeof(SearchLds), s, j, 0, 0);
     for (int pass = 0; pass < (j.speed > 2 ? 2 : 1); pass++) {
-      hipLaunchKernelGGL(k_search_walk, gw, dim3(64), walk_lds(npred), s, j, npred, ncmax);
+      if (walk_multi(npred)) hipLaunchKernelGGL(k_search_walk_multi, gw, dim3(64), 0, s, j, npred, ncmax);
+      else hipLaunchKernelGGL(k_search_walk, gw, dim3(64), 0, s, j, npred, ncmax);
       hipLaunchKernelGGL(k_search, gs, dim3(NT), sizeof(SearchLds), s, j, 1, pass);
     }
   }
@@ -1801,10 +1855,13 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, v
   hipLaunchKernelGGL(k_setup_s, dim3(j.ntiles), dim3(128), 0, s, j);
   const int S = j.ntiles * SPT_S;
   launch_tables(j, S, s);
+  EncodeJob jr = j;                        // the trial chains: the packed list, or every trial
+  if (ladder_prune()) hipLaunchKernelGGL(k_prune_s, dim3((j.ntiles * HOH_NPLANE_S + 63) / 64), dim3(64), 0, s, j);
+  else jr.trials = nullptr;
   mark(mc, "tables");
   // the MED planes' pb-15 encodes, the prob_bits ladder's trial encodes (size only) and the LZ /
   // predictor-map streams, all on the f64-quotient chain in one launch
-  launch_rans_fast_s(j, s, j.ntiles * 6, SidMap{3, KS_MED}, j.ntiles * 3, SidMap{3, KS_MED + 3},
+  launch_rans_fast_s(jr, s, j.ntiles * 6, SidMap{3, KS_MED}, j.ntiles * 3, SidMap{3, KS_MED + 3},
                      j.ntiles * HOH_NPLANE_S * 8, SidMap{HOH_NPLANE_S * 8, KS_VAR}, j.ntiles * HOH_NPLANE_S * 8, S,
                      SidMap{0, 0}, S);
   launch_rans_gen(j, S, s);

@@ -179,6 +179,27 @@ __global__ __launch_bounds__(64) void k_tables(EncodeJob j, SidMap sm) {
   }
   for (uint32_t i = lane; i < range; i += 64) fr[i] = cum[i + 1] - cum[i];
   __syncthreads();
+  // Size-only trials of the prob_bits ladder: bounds on the words the chain will count, from the
+  // code length I = sum count * log2(2^pb / f) (k_prune_s skips the trials whose bounds cannot
+  // change the ladder's decision).  Rans64 keeps x in [2^31, 2^63): a step multiplies x by
+  // 2^pb / f within a factor 1 +- d, d = 2^(pb - 31) (|x' - x 2^pb / f| < 2^pb and x / f >=
+  // 2^(31 - pb)), a renormalisation loses at most a factor 1 - d, so log2(x) + 32 * emits is
+  // 31 + I + e with -3nd < e < 1.5nd (|log2(1 +- d)| < 1.5d for d <= 2^-12).  The final
+  // log2(x) in [31, 63) leaves (I + e - 32) / 32 < emits < (I + e) / 32; one bit more either
+  // side covers the f64 sum.  words = emits + the two flush words.
+  uint32_t wlo = 0, whi = 0;
+  if (st.sizeonly && j.hist && st.hist_src) {
+    double part = 0.0;
+    for (uint32_t i = lane; i < range; i += 64) {
+      const uint32_t cnt = j.hist[(size_t)(st.hist_src - 1) * 512 + i];
+      if (cnt && fr[i]) part += (double)cnt * ((double)pb - log2((double)fr[i]));
+    }
+    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+    const double d = ldexp(1.0, (int)pb - 31), slack = 1.0 + 1e-9 * part;
+    const double lo = (part - 3.0 * n * d - slack - 32.0) / 32.0, hi = (part + 1.5 * n * d + slack) / 32.0;
+    wlo = lo > 0.0 ? (uint32_t)floor(lo) + 2u : 2u;
+    whi = (uint32_t)floor(hi) + 1u + 2u;
+  }
   // ---- encoder symbol tables.  The f64-quotient chain (k_rans_fast) takes prob_bits 7..19 with
   // range <= 512 (7: its 24-bit multiply of the high quotient; 19: its floors' exactness bound,
   // k_rans_enc.hip step15)
@@ -399,6 +420,8 @@ __global__ __launch_bounds__(64) void k_tables(EncodeJob j, SidMap sm) {
   st.expected_stored = expected_stored;
   st.fast = fast ? 1 : 0;
   st.mode = SM_RANS;
+  st.wlo = wlo;
+  st.whi = whi;
   j.streams[s] = st;
 }
 
