@@ -405,21 +405,24 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   int e = HOH_OK;
   if (speed) {
     if ((e = ensure(c->idx8, (size_t)ntiles * j.npix_cap))) return e;
-    if ((e = ensure(c->fpb, (size_t)ntiles * j.npix_cap * 9))) return e;   // fingerprints + pixels + runs
+    if ((e = ensure(c->fpb, (size_t)ntiles * j.npix_cap * 13))) return e;   // fingerprints + pixels + transposed + runs
     if ((e = ensure(c->pinfo, (size_t)ntiles * HOH_NPLANE_S * (sizeof(PlaneInfo) + 8 * 4)))) return e;   // + trial list
     if ((e = ensure_log2_tables(c, W, H, j))) return e;
     j.idx8 = (uint8_t*)c->idx8.p;
     j.fpb = (uint32_t*)c->fpb.p;
     j.tpx = j.fpb + (size_t)ntiles * j.npix_cap;
-    j.run8 = (uint8_t*)(j.fpb + 2 * (size_t)ntiles * j.npix_cap);
+    j.fpt = j.fpb + 2 * (size_t)ntiles * j.npix_cap;
+    j.run8 = (uint8_t*)(j.fpb + 3 * (size_t)ntiles * j.npix_cap);
     j.lzs = nullptr;
     j.lzrank = nullptr;
     // posting lists for the long LZ windows (-s2..-s4) of tiles whose positions fit 16 bits
     if (speed >= 2 && j.npix_cap <= 65536 && lz_posting()) {
       const size_t per = (size_t)ntiles * j.npix_cap;
-      if ((e = ensure(c->lzs, per * 10))) return e;
+      if ((e = ensure(c->lzs, per * 12))) return e;
       j.lzs = (uint32_t*)c->lzs.p;
       j.lzrank = (uint16_t*)((uint32_t*)c->lzs.p + 2 * per);
+      j.lzend = j.lzrank + per;
+      j.lzs_hmask = (uint32_t)HOH_KNOB(LZS_HMASK, 0xffff);
     }
     j.pinfo = (PlaneInfo*)c->pinfo.p;
     j.trials = (uint32_t*)(j.pinfo + (size_t)ntiles * HOH_NPLANE_S);

@@ -825,7 +825,114 @@ enum { LZC_WALK = 0, LZC_TAB = 1, LZC_MAP = 2 };
 __device__ __forceinline__ uint32_t* lzc_map(const EncodeJob& j, int t) {
   return (uint32_t*)((char*)j.tab_gen + (size_t)t * TAB_TILE_BYTES + LZC_MAP_OFF);
 }
-__global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring, int mode, uint32_t mw) {
+// The fingerprints transposed (column-major per tile: FT[x * h + y] = F[y * w + x]), so that
+// k_lzscan's vertical test loads a column's rows above q with one contiguous read per 64 rows
+// instead of 64 lines at stride w.  64 x 64 blocks through LDS.
+__global__ __launch_bounds__(256) void k_lzft(EncodeJob j) {
+  __shared__ uint32_t blk[64][65];
+  const int t = blockIdx.y, tid = threadIdx.x;
+  const TileInfo ti = j.tiles[t];
+  const uint32_t w = ti.w, h = ti.h, nbx = (w + 63) / 64, nby = (h + 63) / 64;
+  const uint32_t* F = j.fpb + (size_t)t * j.npix_cap;
+  uint32_t* FT = j.fpt + (size_t)t * j.npix_cap;
+  for (uint32_t b = blockIdx.x; b < nbx * nby; b += gridDim.x) {
+    const uint32_t x0 = (b % nbx) * 64, y0 = (b / nbx) * 64;
+    for (uint32_t e = tid; e < 64 * 64; e += 256) {
+      const uint32_t r = e / 64, c = e % 64;
+      if (y0 + r < h && x0 + c < w) blk[r][c] = F[(y0 + r) * w + x0 + c];
+    }
+    __syncthreads();
+    for (uint32_t e = tid; e < 64 * 64; e += 256) {
+      const uint32_t c = e / 64, r = e % 64;
+      if (y0 + r < h && x0 + c < w) FT[(x0 + c) * h + y0 + r] = blk[r][c];
+    }
+    __syncthreads();
+  }
+}
+
+// Vertical backs beyond the window (lz.hpp:54-74: q - k*w, limit < k*w <= min(65536, q)) for the
+// positions k_lzcand left without a candidate, tiles whose every earlier row is in reach
+// ((h - 1) * w <= 65536, w a multiple of 64 up to 256: 256^2 tiles).  A thread per column keeps
+// a 4096-bit Bloom filter (three bits per fingerprint) of its column's rows up to y - kmin,
+// kmin = limit / w + 1: a clear bit is an exact no.  A possible yes is settled by the whole wave
+// on the transposed fingerprints (k_lzft: the column's rows are contiguous, 64 per load).  Row by
+// row the wave of columns x .. x + 63 owns one candidate word; the rows' words are loaded eight
+// rows ahead.  (k_lzcand walked sixteen rows a batch for every position without a candidate: 256
+// loads for most positions of a noisy tile, 14 ms per natural 8192^2 image at -s1.)
+#define LZV_WORDS 128
+#define LZV_AHEAD 8
+__host__ __device__ inline bool lzvert_ok(uint32_t w, uint32_t h) {
+  return w >= 64 && w <= 256 && (w & 63) == 0 && (h - 1) * w <= 65536u;
+}
+__device__ __forceinline__ void lzv_bits(uint32_t f, uint32_t& a, uint32_t& b, uint32_t& c) {
+  const uint32_t g = f * 0x9E3779B1u;
+  a = g >> 20; b = (f ^ (f >> 15)) & 4095u; c = ((f >> 7) * 0x85EBCA6Bu) >> 20;
+}
+__global__ __launch_bounds__(256) void k_lzvert(EncodeJob j, int limit) {
+  __shared__ uint32_t bl[LZV_WORDS][256];                         // [word][column]: conflict-free
+  const int t = blockIdx.x, x = threadIdx.x, lane = x & 63;
+  const TileInfo ti = j.tiles[t];
+  const uint32_t w = ti.w, h = ti.h;
+  if (!lzvert_ok(w, h) || (uint32_t)x >= w) return;                // whole waves (w % 64 == 0)
+  for (int i = 0; i < LZV_WORDS; i++) bl[i][x] = 0u;
+  const uint32_t* F = j.fpb + (size_t)t * j.npix_cap;
+  const uint32_t* FT = j.fpt + (size_t)t * j.npix_cap;
+  uint64_t* cand = j.candbits + (size_t)t * (j.npix_cap / 64);
+  const uint32_t kmin = (uint32_t)limit / w + 1;                  // rows y >= kmin only
+  uint32_t added = 0;
+  uint32_t fi[LZV_AHEAD], fq[LZV_AHEAD];
+  uint64_t cw[LZV_AHEAD];
+  auto load = [&](uint32_t y0) {
+#pragma unroll
+    for (int u = 0; u < LZV_AHEAD; u++) {
+      const uint32_t y = y0 + u;
+      fi[u] = y < h ? F[(y - kmin) * w + x] : 0u;
+      fq[u] = y < h ? F[y * w + x] : 0u;
+      cw[u] = y < h ? cand[(y * w + x) >> 6] : 0ull;
+    }
+  };
+  if (kmin < h) load(kmin);
+  for (uint32_t y0 = kmin; y0 < h; y0 += LZV_AHEAD) {
+    uint32_t gi[LZV_AHEAD], gq[LZV_AHEAD];
+    uint64_t gw[LZV_AHEAD];
+#pragma unroll
+    for (int u = 0; u < LZV_AHEAD; u++) { gi[u] = fi[u]; gq[u] = fq[u]; gw[u] = cw[u]; }
+    if (y0 + LZV_AHEAD < h) load(y0 + LZV_AHEAD);
+#pragma unroll
+    for (int u = 0; u < LZV_AHEAD; u++) {
+      const uint32_t y = y0 + u;
+      if (y >= h) break;
+      const uint32_t r = y - kmin, q = y * w + x, f = gq[u];
+      uint32_t a, b, c;
+      if (gi[u]) {                                                 // row r joins the filter
+        lzv_bits(gi[u], a, b, c);
+        bl[a >> 5][x] |= 1u << (a & 31);
+        bl[b >> 5][x] |= 1u << (b & 31);
+        bl[c >> 5][x] |= 1u << (c & 31);
+      }
+      bool maybe = false;
+      if (f && !((gw[u] >> (q & 63)) & 1)) {
+        lzv_bits(f, a, b, c);
+        maybe = ((bl[a >> 5][x] >> (a & 31)) & (bl[b >> 5][x] >> (b & 31)) & (bl[c >> 5][x] >> (c & 31))) & 1;
+      }
+      // each possible yes: the wave reads the lane's column rows r, r - 1, .. 0, 64 per load
+      bool hit = false;
+      for (uint64_t um = __ballot(maybe); um; um &= um - 1) {
+        const int l = __ffsll((unsigned long long)um) - 1;
+        const uint32_t fl = __shfl(f, l), cl = (uint32_t)(x - lane + l) * h;
+        bool found = false;
+        for (int32_t r0 = (int32_t)r; r0 >= 0 && !found; r0 -= 64)
+          found = __ballot(r0 - lane >= 0 && FT[cl + (uint32_t)(r0 - lane)] == fl) != 0;
+        if (lane == l) hit = found;
+      }
+      const uint64_t m = __ballot(hit);
+      if (lane == 0 && m) { cand[q >> 6] = gw[u] | m; added += (uint32_t)__popcll(m); }
+    }
+  }
+  if (lane == 0 && added) atomicAdd(&j.tiles[t].ncand, added);
+}
+
+__global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring, int mode, uint32_t mw, int lzc_nowalk) {
   extern __shared__ uint32_t fr[];
   uint32_t* ht = fr + ring;                                            // window tables (LZC_TAB)
   uint32_t* ct = ht + (mode == LZC_TAB ? 3 * LZC_W : 0);               // chunk tables (TAB, MAP)
@@ -895,6 +1002,7 @@ __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring,
     // than 8 of them (the long windows of -s3/-s4 fill the tables) every lane walks its own
     // window instead, eight entries per LDS round trip.
     const uint32_t wb = mode == LZC_MAP ? min(bm, q - base) : bm;      // MAP: the chunk only
+    if (lzc_nowalk && walk && !c) { c = true; walk = false; }          // knob LZC_NOWALK (measurement)
     const uint64_t um0 = __ballot(walk && !c);
     if (__popcll(um0) > 8) {
       for (uint32_t b0 = 1; walk && b0 <= wb && !c; b0 += 8) {
@@ -915,8 +1023,9 @@ __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring,
       }
       if (lane == l) c = hit;
     }
-    if (f && !c) {
-      // vertical backs beyond the window: sixteen rows per batch of (coalesced) global loads
+    if (f && !c && !lzvert_ok(w, ti.h)) {
+      // vertical backs beyond the window (k_lzvert's tiles excepted): sixteen rows per batch of
+      // (coalesced) global loads
       const uint32_t vlim = min(65536u, q);
       for (uint32_t b0 = (bm / w + 1) * w; b0 <= vlim && !c; b0 += 16 * w) {
         uint32_t v[16];
@@ -970,21 +1079,37 @@ __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring,
 // 256-position chunk, a wave ranks its lanes by digit with 8 ballots, the 4 waves' per-digit counts
 // are prefix-summed in LDS, and each position lands at its digit's base + the counts of the waves
 // before + its rank in its wave (stable).
-__device__ __forceinline__ uint32_t lzs_hash(uint32_t f) { return (f * 0x9E3779B1u) >> 16; }
+// j.lzs_hmask is 0xffff; a knobs build can narrow it (LZS_HMASK) so that hash collisions are the rule
+// (tools/scripts/r5_collide.sh: the files must not change)
+__device__ __forceinline__ uint32_t lzs_hash(uint32_t f, uint32_t hm) { return ((f * 0x9E3779B1u) >> 16) & hm; }
 #define LZSORT_T 256
 __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
   __shared__ uint32_t base[256];
   __shared__ uint32_t cnt[LZSORT_T / 64][256];
+  __shared__ uint32_t inner[65536 / 32];                       // flat positions inside a run (unlisted)
+  __shared__ uint32_t s_nl;
   const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const TileInfo ti = j.tiles[t];
   const uint32_t n = (uint32_t)ti.w * ti.h;
   const size_t per = (size_t)j.ntiles * j.npix_cap;
   const uint32_t* F = j.fpb + (size_t)t * j.npix_cap;
+  const uint32_t* TP = j.tpx + (size_t)t * j.npix_cap;
+  const uint8_t* R8 = j.run8 + (size_t)t * j.npix_cap;
   uint32_t* S = j.lzs + (size_t)t * j.npix_cap;                   // final order
   uint32_t* T = j.lzs + per + (size_t)t * j.npix_cap;             // after the first pass
   uint16_t* R = j.lzrank + (size_t)t * j.npix_cap;
+  uint16_t* E = j.lzend + (size_t)t * j.npix_cap;
   const uint64_t lt = (1ull << lane) - 1;
   for (int e = tid; e < (LZSORT_T / 64) * 256; e += LZSORT_T) (&cnt[0][0])[e] = 0;
+  // Flat positions (their window one colour: run8 >= 4) other than a run's first are not listed:
+  // k_lzscan measures one representative per run from the run's start (its end in E).  They still
+  // pass through the first pass, so that the second gives each the rank of its own run's start.
+  for (uint32_t c0 = 0; c0 < n; c0 += LZSORT_T) {
+    const uint32_t i = c0 + tid;
+    const bool in = i < n && i > 0 && R8[i] >= 4 && TP[i - 1] == TP[i];
+    const uint64_t m = __ballot(in);
+    if (lane == 0) { inner[i >> 5] = (uint32_t)m; inner[(i >> 5) + 1] = (uint32_t)(m >> 32); }
+  }
   for (int pass = 0; pass < 2; pass++) {
     const uint32_t sh = 16 + 8 * pass;
     const uint32_t* in = pass ? T : nullptr;
@@ -992,8 +1117,9 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
     if (tid < 256) base[tid] = 0;
     __syncthreads();
     for (uint32_t i = tid; i < n; i += LZSORT_T) {
-      const uint32_t key = pass ? in[i] : (i | (lzs_hash(F[i]) << 16));
-      atomicAdd(&base[(key >> sh) & 255], 1u);
+      const uint32_t key = pass ? in[i] : (i | (lzs_hash(F[i], j.lzs_hmask) << 16));
+      const uint32_t pos = key & 0xffffu;
+      if (!pass || !((inner[pos >> 5] >> (pos & 31)) & 1)) atomicAdd(&base[(key >> sh) & 255], 1u);
     }
     __syncthreads();
     if (tid < 64) {                                              // exclusive scan of the 256 counts
@@ -1009,12 +1135,16 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
       uint32_t run = incl - sum;
 #pragma unroll
       for (int k = 0; k < 4; k++) { base[4 * tid + k] = run; run += v[k]; }
+      if (tid == 63 && pass) s_nl = incl;                        // listed positions
     }
     __syncthreads();
     for (uint32_t c0 = 0; c0 < n; c0 += LZSORT_T) {
       const uint32_t i = c0 + tid;
       const bool valid = i < n;
-      const uint32_t key = !valid ? 0u : pass ? in[i] : (i | (lzs_hash(F[i]) << 16));
+      const uint32_t key = !valid ? 0u : pass ? in[i] : (i | (lzs_hash(F[i], j.lzs_hmask) << 16));
+      const uint32_t pos = key & 0xffffu;
+      // the second pass lists the counted positions only; an unlisted one takes no slot
+      const bool listed = valid && (!pass || !((inner[pos >> 5] >> (pos & 31)) & 1));
       const uint32_t d = (key >> sh) & 255;
       uint64_t peers = __ballot(valid);
 #pragma unroll
@@ -1022,8 +1152,10 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
         const uint64_t m = __ballot((d >> b) & 1);
         peers &= ((d >> b) & 1) ? m : ~m;
       }
-      const uint32_t wr = (uint32_t)__popcll(peers & lt);
-      if (valid && wr == 0) cnt[wv][d] = (uint32_t)__popcll(peers);
+      const uint64_t lpeers = peers & __ballot(listed);
+      const uint32_t wr = (uint32_t)__popcll(lpeers & lt);
+      const bool first = listed ? wr == 0 : (lpeers == 0 && (uint32_t)__popcll(peers & lt) == 0);
+      if (valid && first) cnt[wv][d] = (uint32_t)__popcll(lpeers);
       __syncthreads();
       if (tid < 256) {                                           // per digit: the waves in order
         uint32_t run = base[tid];
@@ -1050,16 +1182,31 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
       // gave two positions one slot, a wrong posting list and a different file per run.)
 #pragma unroll
       for (int k = 0; k < 4; k++) cnt[wv][lane + 64 * k] = 0;
-      if (valid) {
+      if (listed) {
         out[o] = key;
-        if (pass) R[key & 0xffffu] = (uint16_t)o;
+        if (pass) R[pos] = (uint16_t)o;
+      } else if (valid) {
+        // the last listed position before it in its group: its run's start, or a hash-colliding
+        // position after that start (k_lzscan steps over its own run's start)
+        R[pos] = (uint16_t)(o - 1);
       }
     }
     __syncthreads();
   }
   // the fingerprints in sorted order, over the ping-pong half (free now): k_lzscan's hit test reads
-  // them coalesced beside the positions instead of gathering F[p] after them
-  for (uint32_t i = tid; i < n; i += LZSORT_T) T[i] = F[S[i] & 0xffffu];
+  // them coalesced beside the positions instead of gathering F[p] after them; E = the last
+  // position of a listed run start's run (the position itself for every other listed position)
+  const uint32_t nl = s_nl;
+  for (uint32_t i = tid; i < nl; i += LZSORT_T) {
+    const uint32_t p = S[i] & 0xffffu;
+    T[i] = F[p];
+    uint32_t e = p;
+    if (R8[p] >= 4) {
+      while (R8[e] == 255) e += 254;                            // R8 saturates: e + 254 is in the run
+      e += R8[e] - 1;
+    }
+    E[i] = (uint16_t)e;
+  }
 }
 
 #define LZS_KB 0x1ffffu      // k_lzscan keys: (L << 17) | (LZS_KB - b)
@@ -1089,6 +1236,8 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
   const uint32_t npix = (uint32_t)ti.w * ti.h, nwords = (npix + 63) / 64, w = ti.w;
   const uint64_t* bits = j.candbits + (size_t)t * (j.npix_cap / 64);
   const uint32_t* F = j.fpb + (size_t)t * j.npix_cap;
+  const uint32_t* FT = j.fpt + (size_t)t * j.npix_cap;
+  const uint32_t th = (uint32_t)ti.h;
   const uint32_t* TP = j.tpx + (size_t)t * j.npix_cap;
   const uint8_t* R8 = j.run8 + (size_t)t * j.npix_cap;
   uint32_t pq_cur = 0, rq_cur = 0;                                     // pixel q and its run (measure)
@@ -1104,6 +1253,7 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
   const bool post = j.lzs != nullptr;                                  // posting lists (k_lzsort)
   const uint32_t* PS = post ? j.lzs + (size_t)t * j.npix_cap : nullptr;
   const uint16_t* PR = post ? j.lzrank + (size_t)t * j.npix_cap : nullptr;
+  const uint16_t* PE = post ? j.lzend + (size_t)t * j.npix_cap : nullptr;
   const uint32_t* PF = post ? j.lzs + (size_t)j.ntiles * j.npix_cap + (size_t)t * j.npix_cap : nullptr;
   const bool lds_bits = nwords <= LZS_BITS;
   const uint32_t nseg = (lds_bits && rp && nwords >= 4 * LZS_SEG && nseg_req > 1) ? (uint32_t)nseg_req : 1u;
@@ -1233,6 +1383,7 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
     rq_cur = R8[q];
     const uint32_t bm = q < (uint32_t)limit ? q : (uint32_t)limit;
     const uint32_t kmax = min(65536u, q) / w;                         // vertical: k * w <= min(65536, q)
+    const uint32_t yq = q / w, cbase = (q - yq * w) * th + yq;        // q's column in FT
     // one batch: f, the first 16 horizontal chunks, the vertical chunks
     const uint32_t f = F[q];
     uint32_t fv[LZS_HB], fw[LZS_VB];
@@ -1244,7 +1395,7 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
 #pragma unroll
     for (int c = 0; c < LZS_VB; c++) {
       const uint32_t k = 1 + 64 * c + lane;
-      fw[c] = k <= kmax ? F[q - k * w] : 0u;
+      fw[c] = k <= kmax && k * w > bm ? FT[cbase - k] : 0u;           // FT[x * h + y - k] = F[q - k * w]
     }
     if (rp) fill_to(q >= reach ? q - reach : 0u, q + 260);
     // horizontal: b = 1 .. min(limit, q), longest first, then the smallest b.  Each batch's hits
@@ -1258,23 +1409,47 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
     if (post) {
       // posting list: q's hash group walked back from q's rank, 64 positions a batch (back
       // distances ascending); the batch in which the group or the window ends is the last
-      const uint32_t hq = lzs_hash(f);
+      const uint32_t hq = lzs_hash(f, j.lzs_hmask);
       const uint64_t lt = (1ull << lane) - 1;
+      // A flat q (its window one colour c) finds c's runs in its group by their starts only
+      // (k_lzsort lists no other position of a flat run; PR[q] is its own run's start).  Of a run
+      // [s, e] the copy from position p is min(e - p + 1, r) long when the lengths differ (r = q's
+      // own run, capped), so p* = max(s, e - r + 1) is at least as long as any other p of the run
+      // and nearer than the equally long ones: it is the run's one candidate (q - bm if p* is
+      // older than the window).  q's own run gives b = 1 with length r.
+      const bool flat = rq_cur >= 4;
+      uint32_t rs = 0;
+      if (flat) {
+        uint32_t rq = rq_cur;
+        if (rq == 255 && q + 255 < npix && TP[q + 255] == pq_cur) rq += R8[q + 255];
+        rs = min(rq, min(259u, npix - q));
+        if (TP[q - 1] == pq_cur) {
+          mine = (rs << 17) | (LZS_KB - 1u);
+          done = rs >= min(259u, npix - q);                            // b = 1 at the cap: nothing beats it
+        }
+      }
       // the next batch's entries are loaded before this batch's hits are measured (prefetch)
       int32_t i0 = (int32_t)PR[q] - 1;
-      uint32_t e_n = 0u, fe_n = ~f;
-      if (i0 - lane >= 0) { e_n = PS[i0 - lane]; fe_n = PF[i0 - lane]; }
+      uint32_t e_n = 0u, fe_n = ~f, en_n = 0u;
+      if (i0 - lane >= 0) { e_n = PS[i0 - lane]; fe_n = PF[i0 - lane]; if (flat) en_n = PE[i0 - lane]; }
       for (; i0 >= 0 && !done; i0 -= 64) {
         const int32_t i = i0 - lane;
-        const uint32_t e = e_n, fe = fe_n;
+        const uint32_t e = e_n, fe = fe_n, en = en_n;
         e_n = 0u; fe_n = ~f;
-        if (i >= 64) { e_n = PS[i - 64]; fe_n = PF[i - 64]; }
+        if (i >= 64) { e_n = PS[i - 64]; fe_n = PF[i - 64]; if (flat) en_n = PE[i - 64]; }
         const uint32_t p = e & 0xffffu;
-        const bool inside = i >= 0 && (e >> 16) == hq && q - p <= bm;
+        const bool run = flat && en > p;                               // a flat run's start
+        // q's own run: PR[q] counts the listed positions before q in its group, which are its own
+        // run's start and any hash-colliding ones after it (never a match: equal windows are flat)
+        const bool own = run && en >= q;
+        const uint32_t last = run ? en - 3u : p;                       // its last position in the group
+        const bool inside = i >= 0 && (e >> 16) == hq && (own || q - last <= bm);
         const uint64_t inm = __ballot(inside);
-        const bool hit = inside && fe == f;
+        const bool hit = inside && !own && fe == f;
         const uint64_t m = __ballot(hit);
-        if (hit) hl[__popcll(m & lt)] = (uint16_t)(q - p);
+        uint32_t ps = p;
+        if (run) ps = max(max(p, en + 1u - min(rs, en + 1u)), q - bm);
+        if (hit) hl[__popcll(m & lt)] = (uint16_t)(q - ps);
         const uint32_t tot = (uint32_t)__popcll(m);
         LZS_DBG(1, 1);
         LZS_DBG(2, tot);
@@ -1816,7 +1991,9 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, v
     const int mode = limit <= 1024 ? LZC_TAB : (size_t)mw * 4 + LZC_MAP_OFF <= TAB_TILE_BYTES ? LZC_MAP : LZC_WALK;
     const int lring = mode == LZC_MAP ? 2 * NT : ring;
     const size_t lds = (size_t)(lring + (mode == LZC_TAB ? 3 * LZC_W : 0) + (mode != LZC_WALK ? 2 * LZC_C : 0)) * 4;
-    hipLaunchKernelGGL(k_lzcand, dim3(j.ntiles), dim3(NT), lds, sl, j, limit, lring, mode, mw);
+    hipLaunchKernelGGL(k_lzft, dim3(16, j.ntiles), dim3(256), 0, sl, j);
+    hipLaunchKernelGGL(k_lzcand, dim3(j.ntiles), dim3(NT), lds, sl, j, limit, lring, mode, mw, HOH_KNOB(LZC_NOWALK, 0));
+    hipLaunchKernelGGL(k_lzvert, dim3(j.ntiles), dim3(256), 0, sl, j, limit);
     if (j.lzs) hipLaunchKernelGGL(k_lzsort, dim3(j.ntiles), dim3(LZSORT_T), 0, sl, j);
     int rp = 1;
     while (rp < limit + 324) rp <<= 1;

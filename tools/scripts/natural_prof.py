@@ -2,6 +2,7 @@
 """Measurement: 8192^2 natural-statistic image (hoh_ans.natural, BASELINE configs[4]) encoded at
 -sN and decoded, a few times, one image at a time; prints ms per encode / decode and the file
 size.  Run under rocprofv3 --kernel-trace --stats for the per-kernel split."""
+import hashlib
 import os
 import sys
 import time
@@ -31,6 +32,6 @@ for _ in range(reps if speed == 0 else 0):          # the decoder takes -s0 file
     hoh_ans.decode_image(out, n, out_dev=dec, ctx=c, index=ix if speed == 0 else None)
     torch.cuda.synchronize()
     td.append(time.perf_counter() - t)
-print("natural %dx%d -s%d: %d B, encode %.2f ms, decode %s ms, lossless %s" %
-      (W, H, speed, n, min(te) * 1e3, "%.2f" % (min(td) * 1e3) if td else "-",
-       bool(torch.equal(dec, rgb)) if td else "-"), flush=True)
+print("natural %dx%d -s%d: %d B (sha %s), encode %.2f ms, decode %s ms, lossless %s" %
+      (W, H, speed, n, hashlib.sha256(out[:n].cpu().numpy().tobytes()).hexdigest()[:12], min(te) * 1e3,
+       "%.2f" % (min(td) * 1e3) if td else "-", bool(torch.equal(dec, rgb)) if td else "-"), flush=True)
