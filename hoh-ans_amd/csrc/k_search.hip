@@ -1741,6 +1741,9 @@ __global__ __launch_bounds__(64) void k_prune_s(EncodeJob j) {
     if ((need >> k) & 1) j.trials[atomicAdd(j.ntrial, 1u)] = (uint32_t)(t * SPT_S + KS_VAR + p * 8 + k);
     else { v[k].sizeonly = 2; v[k].words = v[k].wlo; }
   }
+#ifdef HOH_DEBUG_READ
+  if (j.dbg) atomicAdd(&j.dbg[(size_t)t * 64 + 40 + __popc(need)], 1u);   // planes by trials kept (lzscan_stats.py)
+#endif
 }
 
 // layer_encode.hpp:22, :115-120, :326-398 on the stream sizes
@@ -1964,7 +1967,7 @@ __global__ __launch_bounds__(64) void k_tilebytes_s(EncodeJob j) {
 // ---------------------------------------------------------------- orchestration
 
 static int ladder_prune() { return HOH_KNOB(LADDER_PRUNE, 1); }   // knob LADDER_PRUNE=0: every trial encoded
-static int lzs_ring_max() { return HOH_KNOB(LZS_RING_MAX, 2048); }
+static int lzs_ring_max() { return HOH_KNOB(LZS_RING_MAX, 1024); }
 static int lzs_seg() { const int n = HOH_KNOB(LZS_SEG, LZS_SEG); return n < 1 ? 1 : n > LZS_SEG ? LZS_SEG : n; }
 
 void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, void (*mark)(void*, const char*), void* mc) {
@@ -2001,7 +2004,9 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, v
     // lzs_ring_max() positions; the ring serves backs up to rp - 324, the rest (long backs of
     // -s3/-s4, vertical ones) read the image.  The scan waits on its loads, so workgroups per CU
     // (LDS) count for more than the ring's reach: at -s4 rings of 8192 positions (one workgroup
-    // per CU) took 185 ms per natural 8192^2 encode, 2048 (three) 166 ms.
+    // per CU) took 185 ms per natural 8192^2 encode, 2048 (three) 166 ms (round 4); with the run
+    // walks of round 5, 1024-position rings (33 KB: four workgroups per CU, an 8192^2 image's
+    // 1024 tiles in one round) against 2048: -s3 k_lzscan 16.3 -> 10.2 ms, -s4 18.9 -> 17.3.
     // knobs LZS_RING_MAX / LZS_SEG (measurement).
     if (rp > lzs_ring_max()) rp = lzs_ring_max();
     if (rp < 1024) rp = 0;

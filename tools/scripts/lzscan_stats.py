@@ -37,3 +37,5 @@ for sp in [int(a) for a in sys.argv[1:]] or [1, 4]:
               tot["image_runs"] / m, tot["image_trips"] / m, tot["vert_runs"] / m, tot["cyc_measure"] / m,
               tot["cyc_posting"] / m, tot["cyc_vertical"] / m))
     print("  wave cycles: measure share %.2f of the segment walks" % (tot["cyc_measure"] / max(tot["cyc_wave"], 1)))
+    kept = d[:, 40:49].sum(axis=0)
+    print("  prob_bits ladder (k_prune_s): planes by trials kept 0..8: %s" % " ".join("%d" % v for v in kept))
