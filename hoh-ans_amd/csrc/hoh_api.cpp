@@ -179,7 +179,7 @@ int hoh_ctx_create(hoh_ctx** out, int device) {
   return HOH_OK;
 }
 
-// knob LZ_POSTING=0: -s2..-s4 LZ scans walk every back distance (the round-3 scan, for comparison)
+// knob LZ_POSTING=0: -s1..-s4 LZ scans walk every back distance (the round-3 scan, for comparison)
 static int lz_posting() { return HOH_KNOB(LZ_POSTING, 1); }
 
 static void freebuf(Buf& b) { if (b.p) (void)hipFree(b.p); b.p = nullptr; b.n = 0; }
@@ -415,8 +415,8 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
     j.run8 = (uint8_t*)(j.fpb + 3 * (size_t)ntiles * j.npix_cap);
     j.lzs = nullptr;
     j.lzrank = nullptr;
-    // posting lists for the long LZ windows (-s2..-s4) of tiles whose positions fit 16 bits
-    if (speed >= 2 && j.npix_cap <= 65536 && lz_posting()) {
+    // posting lists for the LZ windows (-s1..-s4) of tiles whose positions fit 16 bits
+    if (speed >= 1 && j.npix_cap <= 65536 && lz_posting()) {
       const size_t per = (size_t)ntiles * j.npix_cap;
       if ((e = ensure(c->lzs, per * 12))) return e;
       j.lzs = (uint32_t*)c->lzs.p;

@@ -749,17 +749,27 @@ __device__ __forceinline__ uint32_t fp4(uint32_t a, uint32_t b, uint32_t c, uint
 // run8[q]: how many pixels from q on equal pixel q (1..254, 255 = at least 255), from a bitmap of
 // the run ends over the chunk and the 259 positions after it (k_lzscan's run-length shortcut).
 #define LZFP_AHEAD 260
+#define LZFP_ROWS 16
 __global__ __launch_bounds__(NT) void k_lzfp(EncodeJob j) {
   __shared__ uint32_t px[NT + LZFP_AHEAD];
   __shared__ uint64_t ends[(NT + LZFP_AHEAD + 63) / 64];
+  __shared__ uint32_t fl[LZFP_ROWS][NT + 1];                      // 256-wide tiles: the block's rows' F
   const int t = blockIdx.y;
   const TileInfo ti = j.tiles[t];
   const uint32_t npix = (uint32_t)ti.w * ti.h, tid = threadIdx.x, lane = tid & 63;
+  const uint32_t w = (uint32_t)ti.w, h = (uint32_t)ti.h;
   uint32_t* fo = j.fpb + (size_t)t * j.npix_cap;
   uint32_t* po = j.tpx + (size_t)t * j.npix_cap;
+  uint32_t* ft = j.fpt + (size_t)t * j.npix_cap;
   uint8_t* ro = j.run8 + (size_t)t * j.npix_cap;
   constexpr uint32_t NP = NT + LZFP_AHEAD, NW = (NP + 63) / 64;
-  for (uint32_t c0 = blockIdx.x * NT; c0 < npix; c0 += gridDim.x * NT) {
+  // block b takes a contiguous range of chunks (of a 256-wide tile: rows [b*S, b*S + S)), so the
+  // transposed fingerprints (k_lzscan's / k_lzvert's columns) leave as 4-word column pieces
+  const uint32_t nch = (npix + NT - 1) / NT, S = (nch + gridDim.x - 1) / gridDim.x;
+  const uint32_t ch0 = blockIdx.x * S, ch1 = min(nch, ch0 + S);
+  const bool rows = w == NT && S <= LZFP_ROWS && (S & 3) == 0;
+  for (uint32_t ch = ch0; ch < ch1; ch++) {
+    const uint32_t c0 = ch * NT;
     // past the tile: a word no pixel has (pixels are 24-bit), so the tile's last run ends there
     for (uint32_t k = tid; k < NP; k += NT) px[k] = c0 + k < npix ? tile_px(j, ti, c0 + k) : 0xffffffffu;
     __syncthreads();
@@ -772,21 +782,30 @@ __global__ __launch_bounds__(NT) void k_lzfp(EncodeJob j) {
     const uint32_t q = c0 + tid;
     if (q < npix) {
       po[q] = px[tid];
-      fo[q] = q + 3 < npix ? fp4(px[tid], px[tid + 1], px[tid + 2], px[tid + 3]) : 0u;
+      const uint32_t f = q + 3 < npix ? fp4(px[tid], px[tid + 1], px[tid + 2], px[tid + 3]) : 0u;
+      fo[q] = f;
+      if (rows) fl[ch - ch0][tid] = f;
+      else ft[(q % w) * h + q / w] = f;
       // the first run end at or after tid (at most 255 positions on)
       uint32_t e = 0xffffffffu;
-      for (uint32_t w = tid >> 6; w < NW && w <= ((tid + 255) >> 6); w++) {
-        uint64_t m = ends[w];
-        if (w == (tid >> 6)) m &= ~0ull << (tid & 63);
-        if (m) { e = w * 64 + (uint32_t)(__ffsll((unsigned long long)m) - 1); break; }
+      for (uint32_t wd = tid >> 6; wd < NW && wd <= ((tid + 255) >> 6); wd++) {
+        uint64_t m = ends[wd];
+        if (wd == (tid >> 6)) m &= ~0ull << (tid & 63);
+        if (m) { e = wd * 64 + (uint32_t)(__ffsll((unsigned long long)m) - 1); break; }
       }
-      const uint32_t r = e - tid + 1;
+      // no end within 255 positions: 255 (e - tid + 1 would wrap to 0 at tid 0)
+      const uint32_t r = e == 0xffffffffu ? 255u : e - tid + 1;
       ro[q] = (uint8_t)(r < 255 ? r : 255);
     }
     __syncthreads();
   }
+  if (rows && ch0 < ch1) {
+    // column x = tid, rows ch0 .. ch1 - 1: (ch1 - ch0) consecutive words of FT
+    uint4* dst = (uint4*)(ft + (size_t)tid * h + ch0);
+    for (uint32_t i = 0; i + 4 <= ch1 - ch0; i += 4)
+      dst[i / 4] = make_uint4(fl[i][tid], fl[i + 1][tid], fl[i + 2][tid], fl[i + 3][tid]);
+  }
 }
-
 // exact candidate screen: q can start a match of length >= 4 only if an equal window starts at
 // q - b for some b <= min(limit, q), or at q - k*w with k*w <= 65536 (lz.hpp:35, :55); equal
 // windows have equal fingerprints, so the screen never misses one.  Chunks of 256 positions in
@@ -825,37 +844,12 @@ enum { LZC_WALK = 0, LZC_TAB = 1, LZC_MAP = 2 };
 __device__ __forceinline__ uint32_t* lzc_map(const EncodeJob& j, int t) {
   return (uint32_t*)((char*)j.tab_gen + (size_t)t * TAB_TILE_BYTES + LZC_MAP_OFF);
 }
-// The fingerprints transposed (column-major per tile: FT[x * h + y] = F[y * w + x]), so that
-// k_lzscan's vertical test loads a column's rows above q with one contiguous read per 64 rows
-// instead of 64 lines at stride w.  64 x 64 blocks through LDS.
-__global__ __launch_bounds__(256) void k_lzft(EncodeJob j) {
-  __shared__ uint32_t blk[64][65];
-  const int t = blockIdx.y, tid = threadIdx.x;
-  const TileInfo ti = j.tiles[t];
-  const uint32_t w = ti.w, h = ti.h, nbx = (w + 63) / 64, nby = (h + 63) / 64;
-  const uint32_t* F = j.fpb + (size_t)t * j.npix_cap;
-  uint32_t* FT = j.fpt + (size_t)t * j.npix_cap;
-  for (uint32_t b = blockIdx.x; b < nbx * nby; b += gridDim.x) {
-    const uint32_t x0 = (b % nbx) * 64, y0 = (b / nbx) * 64;
-    for (uint32_t e = tid; e < 64 * 64; e += 256) {
-      const uint32_t r = e / 64, c = e % 64;
-      if (y0 + r < h && x0 + c < w) blk[r][c] = F[(y0 + r) * w + x0 + c];
-    }
-    __syncthreads();
-    for (uint32_t e = tid; e < 64 * 64; e += 256) {
-      const uint32_t c = e / 64, r = e % 64;
-      if (y0 + r < h && x0 + c < w) FT[(x0 + c) * h + y0 + r] = blk[r][c];
-    }
-    __syncthreads();
-  }
-}
-
 // Vertical backs beyond the window (lz.hpp:54-74: q - k*w, limit < k*w <= min(65536, q)) for the
 // positions k_lzcand left without a candidate, tiles whose every earlier row is in reach
 // ((h - 1) * w <= 65536, w a multiple of 64 up to 256: 256^2 tiles).  A thread per column keeps
 // a 4096-bit Bloom filter (three bits per fingerprint) of its column's rows up to y - kmin,
 // kmin = limit / w + 1: a clear bit is an exact no.  A possible yes is settled by the whole wave
-// on the transposed fingerprints (k_lzft: the column's rows are contiguous, 64 per load).  Row by
+// on the transposed fingerprints (k_lzfp's FT: a column's rows are contiguous, 64 per load).  Row by
 // row the wave of columns x .. x + 63 owns one candidate word; the rows' words are loaded eight
 // rows ahead.  (k_lzcand walked sixteen rows a batch for every position without a candidate: 256
 // loads for most positions of a noisy tile, 14 ms per natural 8192^2 image at -s1.)
@@ -868,13 +862,15 @@ __device__ __forceinline__ void lzv_bits(uint32_t f, uint32_t& a, uint32_t& b, u
   const uint32_t g = f * 0x9E3779B1u;
   a = g >> 20; b = (f ^ (f >> 15)) & 4095u; c = ((f >> 7) * 0x85EBCA6Bu) >> 20;
 }
-__global__ __launch_bounds__(256) void k_lzvert(EncodeJob j, int limit) {
-  __shared__ uint32_t bl[LZV_WORDS][256];                         // [word][column]: conflict-free
-  const int t = blockIdx.x, x = threadIdx.x, lane = x & 63;
+__global__ __launch_bounds__(64) void k_lzvert(EncodeJob j, int limit) {
+  // one wave per 64 columns (32 KB: a 128 KB workgroup per tile waited for a whole CU's LDS
+  // behind the concurrent predictor search)
+  __shared__ uint32_t bl[LZV_WORDS][64];                          // [word][column]: conflict-free
+  const int t = blockIdx.y, lane = threadIdx.x, x = blockIdx.x * 64 + lane;
   const TileInfo ti = j.tiles[t];
   const uint32_t w = ti.w, h = ti.h;
   if (!lzvert_ok(w, h) || (uint32_t)x >= w) return;                // whole waves (w % 64 == 0)
-  for (int i = 0; i < LZV_WORDS; i++) bl[i][x] = 0u;
+  for (int i = 0; i < LZV_WORDS; i++) bl[i][lane] = 0u;
   const uint32_t* F = j.fpb + (size_t)t * j.npix_cap;
   const uint32_t* FT = j.fpt + (size_t)t * j.npix_cap;
   uint64_t* cand = j.candbits + (size_t)t * (j.npix_cap / 64);
@@ -906,14 +902,14 @@ __global__ __launch_bounds__(256) void k_lzvert(EncodeJob j, int limit) {
       uint32_t a, b, c;
       if (gi[u]) {                                                 // row r joins the filter
         lzv_bits(gi[u], a, b, c);
-        bl[a >> 5][x] |= 1u << (a & 31);
-        bl[b >> 5][x] |= 1u << (b & 31);
-        bl[c >> 5][x] |= 1u << (c & 31);
+        bl[a >> 5][lane] |= 1u << (a & 31);
+        bl[b >> 5][lane] |= 1u << (b & 31);
+        bl[c >> 5][lane] |= 1u << (c & 31);
       }
       bool maybe = false;
       if (f && !((gw[u] >> (q & 63)) & 1)) {
         lzv_bits(f, a, b, c);
-        maybe = ((bl[a >> 5][x] >> (a & 31)) & (bl[b >> 5][x] >> (b & 31)) & (bl[c >> 5][x] >> (c & 31))) & 1;
+        maybe = ((bl[a >> 5][lane] >> (a & 31)) & (bl[b >> 5][lane] >> (b & 31)) & (bl[c >> 5][lane] >> (c & 31))) & 1;
       }
       // each possible yes: the wave reads the lane's column rows r, r - 1, .. 0, 64 per load
       bool hit = false;
@@ -1217,6 +1213,54 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
 // greedy scan (lz.hpp:32-95) over the candidates + the four LZ streams.
 // Per candidate one batch of global loads (its fingerprint, 16 chunks of 64 horizontal back
 // distances and the vertical ones) and then LDS only: the candidate bitmap is staged in LDS and
+// The candidate screen from the posting lists (tiles that have them, -s1..-s4): q is a horizontal
+// candidate iff an equal fingerprint starts at some b <= min(limit, q) -- the first fingerprint-
+// equal entry of q's group walked back from PR[q] (k_lzscan's walk, stopped at its first hit): a
+// flat q inside its run has b = 1; a flat run start finds its colour's earlier run starts, in
+// the window when the run's last listed position (E - 3) is; a hash collision steps on.  A thread
+// per position, every candidate word written (k_lzvert then adds the vertical ones).  It replaces
+// k_lzcand's hash tables / global map for these tiles.
+__global__ __launch_bounds__(256) void k_lzscreen(EncodeJob j, int limit) {
+  const int t = blockIdx.y, lane = threadIdx.x & 63;
+  const TileInfo ti = j.tiles[t];
+  const uint32_t npix = (uint32_t)ti.w * ti.h;
+  const size_t o = (size_t)t * j.npix_cap;
+  const uint32_t* F = j.fpb + o;
+  const uint32_t* TP = j.tpx + o;
+  const uint8_t* R8 = j.run8 + o;
+  const uint32_t* PS = j.lzs + o;
+  const uint32_t* PF = j.lzs + (size_t)j.ntiles * j.npix_cap + o;
+  const uint16_t* PR = j.lzrank + o;
+  const uint16_t* PE = j.lzend + o;
+  uint64_t* cand = j.candbits + (size_t)t * (j.npix_cap / 64);
+  uint32_t ncand = 0;
+  for (uint32_t q0 = blockIdx.x * 256u; q0 < npix; q0 += gridDim.x * 256u) {
+    const uint32_t q = q0 + threadIdx.x;
+    bool c = false;
+    const uint32_t f = q < npix ? F[q] : 0u;
+    if (f && q > 0) {
+      const uint32_t bm = min(q, (uint32_t)limit), pq = TP[q];
+      const bool flat = R8[q] >= 4;
+      if (flat && TP[q - 1] == pq) {
+        c = true;                                                      // b = 1 inside its run
+      } else {
+        const uint32_t hq = lzs_hash(f, j.lzs_hmask);
+        for (int32_t i = (int32_t)PR[q] - 1; i >= 0; i--) {
+          const uint32_t e = PS[i], p = e & 0xffffu;
+          if ((e >> 16) != hq) break;                                  // q's group starts after i
+          const uint32_t en = flat ? (uint32_t)PE[i] : p;
+          const bool run = flat && en > p, own = run && en >= q;
+          if (!own && q - (run ? en - 3u : p) > bm) break;             // older than the window
+          if (!own && PF[i] == f) { c = true; break; }
+        }
+      }
+    }
+    const uint64_t word = __ballot(c);
+    if (lane == 0 && q < npix) { cand[q >> 6] = word; ncand += (uint32_t)__popcll(word); }
+  }
+  if (lane == 0 && ncand) atomicAdd(&j.tiles[t].ncand, ncand);
+}
+
 // the run lengths compare pixels from an LDS ring of the positions [q - limit, q + 260) (filled
 // 64 positions at a time as the scan moves: each pixel read once per tile), sixteen positions per
 // LDS round trip; vertical backs beyond the ring read the image.  rp = ring size (0: -s4, whose
@@ -1492,6 +1536,11 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
       done = __ballot(top) != 0;
     }
     uint32_t best = wave_max_u32(mine);
+#ifdef LZS_PRINTF
+    if (lane == 0 && (q == 1 || q == 256 || q == 515))
+      printf("lzscan t %d q %u: post %d rq %u pq %x R8[q+255] %u TP[q+255] %x best %u npix %u\n", t, q, (int)post,
+             rq_cur, pq_cur, q + 255 < npix ? (uint32_t)R8[q + 255] : 999u, q + 255 < npix ? TP[q + 255] : 0u, best >> 17, npix);
+#endif
     [[maybe_unused]] const uint64_t tv0 = LZS_T();
     LZS_DBG(10, (uint32_t)(tv0 - tp0));
     // vertical (lz.hpp:54-74): whole rows up to 65536 back, strictly longer only
@@ -1994,10 +2043,13 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, v
     const int mode = limit <= 1024 ? LZC_TAB : (size_t)mw * 4 + LZC_MAP_OFF <= TAB_TILE_BYTES ? LZC_MAP : LZC_WALK;
     const int lring = mode == LZC_MAP ? 2 * NT : ring;
     const size_t lds = (size_t)(lring + (mode == LZC_TAB ? 3 * LZC_W : 0) + (mode != LZC_WALK ? 2 * LZC_C : 0)) * 4;
-    hipLaunchKernelGGL(k_lzft, dim3(16, j.ntiles), dim3(256), 0, sl, j);
-    hipLaunchKernelGGL(k_lzcand, dim3(j.ntiles), dim3(NT), lds, sl, j, limit, lring, mode, mw, HOH_KNOB(LZC_NOWALK, 0));
-    hipLaunchKernelGGL(k_lzvert, dim3(j.ntiles), dim3(256), 0, sl, j, limit);
-    if (j.lzs) hipLaunchKernelGGL(k_lzsort, dim3(j.ntiles), dim3(LZSORT_T), 0, sl, j);
+    if (j.lzs) {                      // posting lists: the screen is their first hit (k_lzscreen)
+      hipLaunchKernelGGL(k_lzsort, dim3(j.ntiles), dim3(LZSORT_T), 0, sl, j);
+      hipLaunchKernelGGL(k_lzscreen, dim3(16, j.ntiles), dim3(256), 0, sl, j, limit);
+    } else {
+      hipLaunchKernelGGL(k_lzcand, dim3(j.ntiles), dim3(NT), lds, sl, j, limit, lring, mode, mw, HOH_KNOB(LZC_NOWALK, 0));
+    }
+    hipLaunchKernelGGL(k_lzvert, dim3(4, j.ntiles), dim3(64), 0, sl, j, limit);
     int rp = 1;
     while (rp < limit + 324) rp <<= 1;
     // Four segment walks per tile (stitched as in k_lz), each with a pixel ring of up to

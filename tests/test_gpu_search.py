@@ -36,6 +36,26 @@ def cases():
     out.append(("palette-s1", 1, img.copy()))
     out.append(("palette-s3", 3, img.copy()))
     out.append(("flat-s1", 1, np.full((256, 512, 3), 77, np.uint8)))
+    for sp in (2, 4):
+        out.append(("flat-s%d" % sp, sp, np.full((256, 512, 3), 77, np.uint8)))
+    # long runs of a few colours (runs of 1..700 pixels, many starting at tile row starts, colour
+    # repeats): the run-length shortcut, the flat-run posting walk and k_lzfp's run lengths at
+    # chunk boundaries
+    cols = rs.randint(0, 256, (6, 3)).astype(np.uint8)
+    flat = rs.randint(0, 256, (256 * 512, 3)).astype(np.uint8)            # > 256 colours: RGB tiles
+    p = 0
+    while p < flat.shape[0]:
+        n = int(rs.choice([1, 3, 5, 40, 254, 255, 256, 300, 700]))
+        if rs.randint(0, 3):
+            flat[p:p + n] = cols[rs.randint(0, 6)]
+        p += n
+    runs = flat.reshape(256, 512, 3)
+    runs[100:110] = 9                                                     # two flat tile-row bands
+    for sp in (1, 2, 3, 4):
+        out.append(("runs-s%d" % sp, sp, runs.copy()))
+    half = np.full((256, 512, 3), 77, np.uint8)
+    half[128:] = 9
+    out.append(("halfflat-s3", 3, half))
     out.append(("untiled200x100-s2", 2, synth_rgb(200, 100, 11, 3)))
     out.append(("tiny30x20-s1", 1, synth_rgb(30, 20, 12, 3)))
     return out
