@@ -1080,9 +1080,13 @@ __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring,
 __device__ __forceinline__ uint32_t lzs_hash(uint32_t f, uint32_t hm) { return ((f * 0x9E3779B1u) >> 16) & hm; }
 #define LZSORT_T 256
 __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
-  __shared__ uint32_t base[256];
-  __shared__ uint32_t cnt[LZSORT_T / 64][256];
-  __shared__ uint32_t inner[65536 / 32];                       // flat positions inside a run (unlisted)
+  // Stable LSD counting sort by the 16-bit hash, two 8-bit passes.  Each wave owns a contiguous
+  // quarter of the pass's input and ranks it alone (64 at a time: ballot peers per digit, a
+  // wave-private running base per digit), so a pass has two barriers, not three per 256
+  // positions; the bases come from one scan over (digit, wave).  The next 64 keys are loaded
+  // while the current 64 are ranked.
+  __shared__ uint32_t cnt[LZSORT_T / 64][256];                   // per wave: digit counts, then bases
+  __shared__ uint32_t inner[65536 / 32];                         // flat positions inside a run (unlisted)
   __shared__ uint32_t s_nl;
   const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const TileInfo ti = j.tiles[t];
@@ -1095,8 +1099,8 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
   uint32_t* T = j.lzs + per + (size_t)t * j.npix_cap;             // after the first pass
   uint16_t* R = j.lzrank + (size_t)t * j.npix_cap;
   uint16_t* E = j.lzend + (size_t)t * j.npix_cap;
+  const uint32_t hm = j.lzs_hmask;
   const uint64_t lt = (1ull << lane) - 1;
-  for (int e = tid; e < (LZSORT_T / 64) * 256; e += LZSORT_T) (&cnt[0][0])[e] = 0;
   // Flat positions (their window one colour: run8 >= 4) other than a run's first are not listed:
   // k_lzscan measures one representative per run from the run's start (its end in E).  They still
   // pass through the first pass, so that the second gives each the rank of its own run's start.
@@ -1106,78 +1110,78 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
     const uint64_t m = __ballot(in);
     if (lane == 0) { inner[i >> 5] = (uint32_t)m; inner[(i >> 5) + 1] = (uint32_t)(m >> 32); }
   }
+  const uint32_t quarter = ((n + LZSORT_T / 64 - 1) / (LZSORT_T / 64) + 63) & ~63u;
+  const uint32_t lo = min(n, (uint32_t)wv * quarter), hi = min(n, lo + quarter);
   for (int pass = 0; pass < 2; pass++) {
     const uint32_t sh = 16 + 8 * pass;
     const uint32_t* in = pass ? T : nullptr;
     uint32_t* out = pass ? S : T;
-    if (tid < 256) base[tid] = 0;
-    __syncthreads();
-    for (uint32_t i = tid; i < n; i += LZSORT_T) {
-      const uint32_t key = pass ? in[i] : (i | (lzs_hash(F[i], j.lzs_hmask) << 16));
+    auto key_at = [&](uint32_t i) -> uint32_t {
+      return i >= hi ? 0u : pass ? in[i] : (i | (lzs_hash(F[i], hm) << 16));
+    };
+    // the second pass lists the counted positions only; an unlisted one takes no slot
+    auto listed_of = [&](uint32_t i, uint32_t key) -> bool {
       const uint32_t pos = key & 0xffffu;
-      if (!pass || !((inner[pos >> 5] >> (pos & 31)) & 1)) atomicAdd(&base[(key >> sh) & 255], 1u);
-    }
-    __syncthreads();
-    if (tid < 64) {                                              // exclusive scan of the 256 counts
-      uint32_t v[4], sum = 0;
-#pragma unroll
-      for (int k = 0; k < 4; k++) { v[k] = base[4 * tid + k]; sum += v[k]; }
-      uint32_t incl = sum;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t u = __shfl_up(incl, o);
-        if (lane >= o) incl += u;
-      }
-      uint32_t run = incl - sum;
-#pragma unroll
-      for (int k = 0; k < 4; k++) { base[4 * tid + k] = run; run += v[k]; }
-      if (tid == 63 && pass) s_nl = incl;                        // listed positions
-    }
-    __syncthreads();
-    for (uint32_t c0 = 0; c0 < n; c0 += LZSORT_T) {
-      const uint32_t i = c0 + tid;
-      const bool valid = i < n;
-      const uint32_t key = !valid ? 0u : pass ? in[i] : (i | (lzs_hash(F[i], j.lzs_hmask) << 16));
-      const uint32_t pos = key & 0xffffu;
-      // the second pass lists the counted positions only; an unlisted one takes no slot
-      const bool listed = valid && (!pass || !((inner[pos >> 5] >> (pos & 31)) & 1));
-      const uint32_t d = (key >> sh) & 255;
+      return i < hi && (!pass || !((inner[pos >> 5] >> (pos & 31)) & 1));
+    };
+    // this lane's digit group among the 64: the lanes with the same digit
+    auto group = [&](bool valid, uint32_t d) -> uint64_t {
       uint64_t peers = __ballot(valid);
 #pragma unroll
       for (int b = 0; b < 8; b++) {
         const uint64_t m = __ballot((d >> b) & 1);
         peers &= ((d >> b) & 1) ? m : ~m;
       }
-      const uint64_t lpeers = peers & __ballot(listed);
-      const uint32_t wr = (uint32_t)__popcll(lpeers & lt);
-      const bool first = listed ? wr == 0 : (lpeers == 0 && (uint32_t)__popcll(peers & lt) == 0);
-      if (valid && first) cnt[wv][d] = (uint32_t)__popcll(lpeers);
-      __syncthreads();
-      if (tid < 256) {                                           // per digit: the waves in order
-        uint32_t run = base[tid];
+      return peers;
+    };
 #pragma unroll
-        for (int w = 0; w < LZSORT_T / 64; w++) {
-          const uint32_t c = cnt[w][tid];
-          cnt[w][tid] = run;
-          run += c;
-        }
-        base[tid] = run;
+    for (int k = 0; k < 4; k++) cnt[wv][lane + 64 * k] = 0;
+    __syncthreads();                                               // inner / the previous pass done
+    // 1. this wave's listed count per digit
+    uint32_t kn = key_at(lo + lane);
+    for (uint32_t i0 = lo; i0 < hi; i0 += 64) {
+      const uint32_t i = i0 + lane, key = kn;
+      kn = key_at(i + 64);
+      const bool listed = listed_of(i, key);
+      const uint32_t d = (key >> sh) & 255;
+      const uint64_t lp = group(i < hi, d) & __ballot(listed);
+      if (listed && __popcll(lp & lt) == 0) cnt[wv][d] += (uint32_t)__popcll(lp);
+    }
+    __syncthreads();
+    // 2. bases: digits in order, the waves in order inside a digit
+    {
+      const uint32_t d = (uint32_t)tid;
+      uint32_t c[LZSORT_T / 64], tot = 0;
+#pragma unroll
+      for (int w = 0; w < LZSORT_T / 64; w++) { c[w] = cnt[w][d]; tot += c[w]; }
+      // exclusive scan of the 256 digit totals (thread d holds digit d)
+      uint32_t incl = tot;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(incl, o);
+        if (lane >= o) incl += u;
       }
+      __syncthreads();                                             // every count read
+      if (lane == 63) cnt[0][wv] = incl;                           // wave totals (digits 64wv..)
       __syncthreads();
-      const uint32_t o = valid ? cnt[wv][d] + wr : 0u;
-#ifdef LZSORT_DELAY_TEST
-      // adversarial schedule (tools/scripts/lzsort_race.sh, never in the product build): the last
-      // wave clears late, so every other wave's next chunk runs ahead of it
-      if (wv == LZSORT_T / 64 - 1)
-        for (int z = 0; z < 4; z++) __builtin_amdgcn_s_sleep(127);
-#endif
-      // each wave clears only its own row, after its own reads (LDS operations of one wave are
-      // performed in order): the row is written next by this wave's next chunk and read by the
-      // per-digit scan only behind that chunk's first barrier.  (Clearing every row by digit
-      // owner after a barrier raced with a faster wave's next-chunk count store: a lost count
-      // gave two positions one slot, a wrong posting list and a different file per run.)
+      uint32_t run = incl - tot;
+      for (int w = 0; w < wv; w++) run += cnt[0][w];
+      if (pass && tid == LZSORT_T - 1) s_nl = run + tot;           // listed positions
+      __syncthreads();
 #pragma unroll
-      for (int k = 0; k < 4; k++) cnt[wv][lane + 64 * k] = 0;
+      for (int w = 0; w < LZSORT_T / 64; w++) { cnt[w][d] = run; run += c[w]; }
+    }
+    __syncthreads();
+    // 3. scatter in order: rank = the wave's running base of the digit + listed peers before
+    kn = key_at(lo + lane);
+    for (uint32_t i0 = lo; i0 < hi; i0 += 64) {
+      const uint32_t i = i0 + lane, key = kn;
+      kn = key_at(i + 64);
+      const bool valid = i < hi, listed = listed_of(i, key);
+      const uint32_t d = (key >> sh) & 255, pos = key & 0xffffu;
+      const uint64_t lp = group(valid, d) & __ballot(listed);
+      const uint32_t o = valid ? cnt[wv][d] + (uint32_t)__popcll(lp & lt) : 0u;
+      if (listed && __popcll(lp & lt) == 0) cnt[wv][d] = o + (uint32_t)__popcll(lp);   // the group's first
       if (listed) {
         out[o] = key;
         if (pass) R[pos] = (uint16_t)o;
@@ -1187,8 +1191,8 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
         R[pos] = (uint16_t)(o - 1);
       }
     }
-    __syncthreads();
   }
+  __syncthreads();
   // the fingerprints in sorted order, over the ping-pong half (free now): k_lzscan's hit test reads
   // them coalesced beside the positions instead of gathering F[p] after them; E = the last
   // position of a listed run start's run (the position itself for every other listed position)

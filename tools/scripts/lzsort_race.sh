@@ -4,7 +4,8 @@
 # before clearing the per-wave digit counts of a chunk:
 #   var/race_old.so  the round-4 k_lzsort (git 88ccbb2): every thread clears cnt[*][tid] after a
 #                    barrier, so a faster wave's next-chunk count store can be wiped
-#   var/race_new.so  the fixed k_lzsort: each wave clears only its own row
+#   var/race_new.so  the fixed round-5 k_lzsort (git 3af4c21): each wave clears only its own row
+# (the current k_lzsort ranks each wave's quarter alone: no count row is shared between waves)
 # and, with `run` (on the GPU box), checks the posting lists of -s2 encodes against an exact
 # recomputation (tools/scripts/lzsort_check.py).  Expected: wrong lists with race_old, none with
 # race_new.
@@ -32,7 +33,8 @@ open(p, "w").write(s.replace(old, new))
 EOF
 /opt/rocm/bin/hipcc $F -DHOH_DEBUG_READ -c -o build/var/dbg.hoh_api.o hoh-ans_amd/csrc/hoh_api.cpp
 /opt/rocm/bin/hipcc $F -c -o build/var/race_old.k_search.o build/var/k_search_r4.hip
-/opt/rocm/bin/hipcc $F -DLZSORT_DELAY_TEST -c -o build/var/race_new.k_search.o hoh-ans_amd/csrc/k_search.hip
+git show 3af4c21:hoh-ans_amd/csrc/k_search.hip > build/var/k_search_r5fix.hip
+/opt/rocm/bin/hipcc $F -DLZSORT_DELAY_TEST -c -o build/var/race_new.k_search.o build/var/k_search_r5fix.hip
 objs=$(ls build/*.o | grep -v -e /hoh_api.cpp.o -e /k_search.hip.o)
 for v in old new; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o var/race_$v.so $objs build/var/dbg.hoh_api.o \
