@@ -280,7 +280,7 @@ __device__ __forceinline__ uint32_t wm_pick(int m, uint32_t b1, uint32_t P1, uin
 #define WM_INIT 0x04440000u                 // b1 = b2 = kp = 4
 template <int NF>
 __device__ void cell_cost_multi(const uint16_t* D, int w, int h, int depth, int xt, int yt, int cx, int cy,
-                                const double* ent, uint32_t* top, double* out) {
+                                const double* ent, uint32_t* top, uint32_t* pk, double* out) {
   // top: this lane's word per column, [col][64 lanes]: value | b1 << 16 | b2 << 20 | kp << 24
   const int c = 1 << depth, half = c >> 1;
   const int tw = (w + xt - 1) / xt, th = (h + yt - 1) / yt;
@@ -335,9 +335,17 @@ __device__ void cell_cost_multi(const uint16_t* D, int w, int h, int depth, int 
         const uint32_t pa = a4 ? p.v[4] : pkm, pb = (xm == 0 && b4first) ? p.v[4] : pkm;
         pend1[m] = ent[(vc - midp(pa, pb)) & cm];
       }
+      // the six picks through LDS: the 16 predictions as 8 dwords of u16 pairs, [pair][64 lanes]
+      // (a lane's reads hit its own bank whatever the index), read back as dwords (one access
+      // type for the location) and the half selected
+#pragma unroll
+      for (int k = 0; k < 8; k++) pk[k * 64] = p.v[2 * k] | (p.v[2 * k + 1] << 16);
+      auto lpick = [&](uint32_t k) -> uint32_t {
+        return __builtin_amdgcn_ubfe(pk[(k >> 1) * 64], (k & 1) * 16, 16);
+      };
       const uint32_t a1 = (wa >> 16) & 15u, l1 = (lw >> 16) & 15u;
-      const uint32_t PA1 = pick(p, a1), PA2 = pick(p, (wa >> 20) & 15u), PAk = pick(p, (wa >> 24) & 15u);
-      const uint32_t PB1 = pick(p, l1), PB2 = pick(p, (lw >> 20) & 15u), PBk = pick(p, (lw >> 24) & 15u);
+      const uint32_t PA1 = lpick(a1), PA2 = lpick((wa >> 20) & 15u), PAk = lpick((wa >> 24) & 15u);
+      const uint32_t PB1 = lpick(l1), PB2 = lpick((lw >> 20) & 15u), PBk = lpick((lw >> 24) & 15u);
 #pragma unroll
       for (int m = 0; m < NF; m++) {
         const uint32_t pr = midp(wm_pick(m, a1, PA1, PA2, PAk), wm_pick(m, l1, PB1, PB2, PBk));
@@ -452,13 +460,14 @@ __global__ __launch_bounds__(64) void k_search_walk(EncodeJob j, int npred, int 
 }
 __global__ __launch_bounds__(64) void k_search_walk_multi(EncodeJob j, int npred, int ncmax) {
   __shared__ uint32_t top[WM_COLS * 64];
+  __shared__ uint32_t pk[8 * 64];
   const int lane = threadIdx.x;
   uint32_t m;
   WalkTask k;
   if (!walk_task(j, npred, ncmax, (uint64_t)blockIdx.x * 64 + lane, m, k)) return;
   const int cx = k.cell % k.xt, cy = k.cell / k.xt;
-  if (npred == 10) cell_cost_multi<6>(k.D, k.w, k.h, k.depth, k.xt, k.yt, cx, cy, k.ent, top + lane, k.ent + 512 + k.cell * 14);
-  else cell_cost_multi<10>(k.D, k.w, k.h, k.depth, k.xt, k.yt, cx, cy, k.ent, top + lane, k.ent + 512 + k.cell * 14);
+  if (npred == 10) cell_cost_multi<6>(k.D, k.w, k.h, k.depth, k.xt, k.yt, cx, cy, k.ent, top + lane, pk + lane, k.ent + 512 + k.cell * 14);
+  else cell_cost_multi<10>(k.D, k.w, k.h, k.depth, k.xt, k.yt, cx, cy, k.ent, top + lane, pk + lane, k.ent + 512 + k.cell * 14);
 }
 
 // One workgroup per (tile, plane).  phase 0: the plane's data staged, the MED residuals'
