@@ -79,15 +79,17 @@ __device__ __forceinline__ uint32_t pick(const Preds& p, uint32_t k) {
 }
 
 // first masked predictor of least |v - p| (prediction.hpp:138-146, :213-224)
+// (the smallest key (|v - p_k| << 4) | k over the masked k: |v - p_k| < 2^16 < 2c never fails the
+// reference's d < 2c test)
 __device__ __forceinline__ uint32_t best_pred(uint32_t v, const Preds& p, uint32_t mask, int c) {
-  int bv = 2 * c;
-  uint32_t b = 0;
+  (void)c;
+  uint32_t best = 0xffffffffu;
 #pragma unroll
   for (int k = 0; k < 16; k++) {
-    const int d = abs((int)v - (int)p.v[k]);
-    if (d < bv && ((mask >> k) & 1)) { bv = d; b = k; }
+    const uint32_t key = (__builtin_amdgcn_sad_u16(v, p.v[k], 0u) << 4) | (uint32_t)k;
+    best = min(best, ((mask >> k) & 1) ? key : 0xffffffffu);
   }
-  return b;
+  return best & 15u;
 }
 
 // ---------------------------------------------------------------- plane data
@@ -550,12 +552,28 @@ __global__ __launch_bounds__(NT) void k_search(EncodeJob j, int phase, int pass)
   a.ring = &S.rows[0][0];
   a.use_ring = true;
   __syncthreads();
+  // tiles up to NT wide (one pixel per thread): the predictor set row y - 1's best predictors were
+  // computed from is kept (u16 pairs) for row y - 1's residuals in the next iteration
+  const bool keep = w <= NT;
+  uint32_t pc[8], pn[8];
+  bool have = false;
   for (int y = h - 1; y >= 0; y--) {
     uint32_t nv[4];
     int n = 0;
     for (int x = tid; x < w && n < 4; x += NT) nv[n++] = y >= 3 ? D[(long)(y - 3) * w + x] : 0u;
-    if (y > 0)
-      for (int x = tid; x < w; x += NT) bcur[x] = (uint8_t)bp_all(a, x, y - 1);
+    if (y > 0) {
+      if (keep) {
+        if (tid < w) {                                                 // bp_all(a, tid, y - 1)
+          Preds p;
+          preds_all_at(a, tid, y - 1, p);
+#pragma unroll
+          for (int k = 0; k < 8; k++) pn[k] = p.v[2 * k] | (p.v[2 * k + 1] << 16);
+          bcur[tid] = y >= h ? 0 : (uint8_t)best_pred(a.px(y - 1, tid), p, a.plist[(y / th) * xt + tid / tw], c);
+        }
+      } else {
+        for (int x = tid; x < w; x += NT) bcur[x] = (uint8_t)bp_all(a, x, y - 1);
+      }
+    }
     __syncthreads();
     uint32_t rv[4];
     n = 0;
@@ -563,7 +581,12 @@ __global__ __launch_bounds__(NT) void k_search(EncodeJob j, int phase, int pass)
       const uint32_t bA = y ? bcur[x] : 4u;
       const uint32_t bB = x ? bnext[x - 1] : (y ? bcur[w - 1] : 4u);
       Preds p;
-      preds_all_at(a, x, y, p);
+      if (keep && have) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) { p.v[2 * k] = pc[k] & 0xffffu; p.v[2 * k + 1] = pc[k] >> 16; }
+      } else {
+        preds_all_at(a, x, y, p);
+      }
       const uint32_t pr = midp(pick(p, bA), pick(p, bB));
       rv[n++] = ((uint32_t)((int)a.px(y, x) - (int)pr + half + c)) & (uint32_t)(c - 1);
     }
@@ -579,6 +602,9 @@ __global__ __launch_bounds__(NT) void k_search(EncodeJob j, int phase, int pass)
     uint8_t* const b = bnext;                                           // row y - 1 is next
     bnext = bcur;
     bcur = b;
+#pragma unroll
+    for (int k = 0; k < 8; k++) pc[k] = pn[k];
+    have = keep && y > 0;
   }
   if (refine) {
     for (int i = tid; i < c; i += NT) ent[i] = lg[1 + S.hist[i]];
