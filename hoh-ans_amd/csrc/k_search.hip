@@ -1248,7 +1248,9 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
 #define LZS_HB 16        // horizontal back-distance chunks of 64 whose fingerprints load at once
 #define LZS_VB 4         // vertical chunks (k * w <= 65536: 256 rows of a 256-wide tile)
 #define LZS_BITS 1024    // candidate words in LDS (tiles up to 65,536 pixels)
-#define LZS_SEG 4        // waves per tile at -s1 (segment walks stitched as in k_lz)
+#ifndef LZS_SEG
+#define LZS_SEG 4        // waves per tile (segment walks stitched as in k_lz); 8 measured: -s4 scan 12.1 -> 9.9 ms alone, the encode 41.5 -> 42.9 ms beside the search
+#endif
 // greedy scan (lz.hpp:32-95) over the candidates + the four LZ streams.
 // Per candidate one batch of global loads (its fingerprint, 16 chunks of 64 horizontal back
 // distances and the vertical ones) and then LDS only: the candidate bitmap is staged in LDS and
