@@ -189,7 +189,7 @@ struct EncodeJob {
   int32_t* ncol;          // [tile] distinct colours (<= 256) or -1 (k_colours)
   uint8_t* idx8;          // -s>=1: [tile][npix_cap] palette indices (the indexed plane's data)
   uint32_t* fpb;          // -s>=1: [tile][npix_cap] 4-pixel window fingerprints (LZ)
-  uint32_t* tpx;          // -s>=1: [tile][npix_cap] the tile's pixels as u32 in tile raster order (LZ)
+  uint32_t* tpx;          // -s>=1: [tile][npix_cap] the tile's pixels in tile raster order (LZ): rgb | run8 << 24
   uint32_t* fpt;          // -s>=1: [tile][npix_cap] the fingerprints transposed, FT[x * h + y] (k_lzfp)
   uint8_t* run8;          // -s>=1: [tile][npix_cap] length of the run of equal pixels from each position
                           //   (tile raster order, 1..254 exact, 255 = at least 255)

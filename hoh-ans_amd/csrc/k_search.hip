@@ -816,7 +816,6 @@ __global__ __launch_bounds__(NT) void k_lzfp(EncodeJob j) {
     __syncthreads();
     const uint32_t q = c0 + tid;
     if (q < npix) {
-      po[q] = px[tid];
       const uint32_t f = q + 3 < npix ? fp4(px[tid], px[tid + 1], px[tid + 2], px[tid + 3]) : 0u;
       fo[q] = f;
       if (rows) fl[ch - ch0][tid] = f;
@@ -829,8 +828,9 @@ __global__ __launch_bounds__(NT) void k_lzfp(EncodeJob j) {
         if (m) { e = wd * 64 + (uint32_t)(__ffsll((unsigned long long)m) - 1); break; }
       }
       // no end within 255 positions: 255 (e - tid + 1 would wrap to 0 at tid 0)
-      const uint32_t r = e == 0xffffffffu ? 255u : e - tid + 1;
-      ro[q] = (uint8_t)(r < 255 ? r : 255);
+      const uint32_t r = e == 0xffffffffu ? 255u : e - tid + 1, r8 = r < 255 ? r : 255;
+      ro[q] = (uint8_t)r8;
+      po[q] = px[tid] | (r8 << 24);                                    // the pixel and its run, one gather
     }
     __syncthreads();
   }
@@ -1141,7 +1141,7 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
   // pass through the first pass, so that the second gives each the rank of its own run's start.
   for (uint32_t c0 = 0; c0 < n; c0 += LZSORT_T) {
     const uint32_t i = c0 + tid;
-    const bool in = i < n && i > 0 && R8[i] >= 4 && TP[i - 1] == TP[i];
+    const bool in = i < n && i > 0 && R8[i] >= 4 && ((TP[i - 1] ^ TP[i]) & 0xffffffu) == 0;
     const uint64_t m = __ballot(in);
     if (lane == 0) { inner[i >> 5] = (uint32_t)m; inner[(i >> 5) + 1] = (uint32_t)(m >> 32); }
   }
@@ -1280,9 +1280,9 @@ __global__ __launch_bounds__(256) void k_lzscreen(EncodeJob j, int limit) {
     bool c = false;
     const uint32_t f = q < npix ? F[q] : 0u;
     if (f && q > 0) {
-      const uint32_t bm = min(q, (uint32_t)limit), pq = TP[q];
+      const uint32_t bm = min(q, (uint32_t)limit), pq = TP[q] & 0xffffffu;
       const bool flat = R8[q] >= 4;
-      if (flat && TP[q - 1] == pq) {
+      if (flat && (TP[q - 1] & 0xffffffu) == pq) {
         c = true;                                                      // b = 1 inside its run
       } else {
         const uint32_t hq = lzs_hash(f, j.lzs_hmask);
@@ -1324,7 +1324,7 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
   const uint32_t* FT = j.fpt + (size_t)t * j.npix_cap;
   const uint32_t th = (uint32_t)ti.h;
   const uint32_t* TP = j.tpx + (size_t)t * j.npix_cap;
-  const uint8_t* R8 = j.run8 + (size_t)t * j.npix_cap;
+  [[maybe_unused]] const uint8_t* R8 = j.run8 + (size_t)t * j.npix_cap;
   uint32_t pq_cur = 0, rq_cur = 0;                                     // pixel q and its run (measure)
   uint32_t* mt = j.matches + (size_t)t * 3 * (j.lz_cap + 1);
   int bonus = 0;                                                      // choh.cpp:139-154
@@ -1376,7 +1376,7 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
     while (wend < need) {
       const uint32_t p = wend + (uint32_t)lane;
       const uint32_t v = TP[min(p, npix - 1)], e = p & rmask;              // unconditional load
-      const uint32_t x = p < npix ? v : 0xff000000u;
+      const uint32_t x = p < npix ? v & 0xffffffu : 0xff000000u;
       pring[e] = x;
       if (e < 16) pring[e + rp] = x;                                 // the mirror of entries 0..15
       wend += 64;
@@ -1415,8 +1415,9 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
       // q - b differ in length the copy ends at the shorter (the longer side still holds c where
       // the other has left it), so only equal runs (or runs of 255+) compare on, behind them.
       LZS_DBG(4, 1);
-      if (TP[q - b] != pq_cur) return 0u;
-      const uint32_t rb = R8[q - b];
+      const uint32_t wb = TP[q - b];                                   // pixel | run << 24
+      if ((wb & 0xffffffu) != pq_cur) return 0u;
+      const uint32_t rb = wb >> 24;
       if (rb != rq_cur) return min(min(rb, rq_cur), lim);
       L = min(rq_cur, lim);
       while (L < lim) {
@@ -1425,8 +1426,8 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
 #pragma unroll
         for (int u = 0; u < 16; u++) {
           const uint32_t p = min(q + L + (uint32_t)u, npix - 1);
-          a[u] = rp ? pring[p & rmask] : TP[p];
-          c[u] = TP[p - b];
+          a[u] = rp ? pring[p & rmask] : TP[p] & 0xffffffu;
+          c[u] = TP[p - b] & 0xffffffu;
         }
         uint32_t r0 = 8, r1 = 16;
 #pragma unroll
@@ -1464,8 +1465,9 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
   auto measure = [&](uint32_t q) -> uint32_t {
     [[maybe_unused]] const uint64_t tm0 = LZS_T();
     LZS_DBG(0, 1);
-    pq_cur = TP[q];
-    rq_cur = R8[q];
+    const uint32_t wq = TP[q];
+    pq_cur = wq & 0xffffffu;
+    rq_cur = wq >> 24;
     const uint32_t bm = q < (uint32_t)limit ? q : (uint32_t)limit;
     const uint32_t kmax = min(65536u, q) / w;                         // vertical: k * w <= min(65536, q)
     const uint32_t yq = q / w, cbase = (q - yq * w) * th + yq;        // q's column in FT
@@ -1506,9 +1508,12 @@ __global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit,
       uint32_t rs = 0;
       if (flat) {
         uint32_t rq = rq_cur;
-        if (rq == 255 && q + 255 < npix && TP[q + 255] == pq_cur) rq += R8[q + 255];
+        if (rq == 255 && q + 255 < npix) {
+          const uint32_t w2 = TP[q + 255];
+          if ((w2 & 0xffffffu) == pq_cur) rq += w2 >> 24;
+        }
         rs = min(rq, min(259u, npix - q));
-        if (TP[q - 1] == pq_cur) {
+        if ((TP[q - 1] & 0xffffffu) == pq_cur) {
           mine = (rs << 17) | (LZS_KB - 1u);
           done = rs >= min(259u, npix - q);                            // b = 1 at the cap: nothing beats it
         }

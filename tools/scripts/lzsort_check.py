@@ -39,7 +39,7 @@ for r in range(reps):
     assert L.hoh_debug_read(c.h, 3, lzs.ctypes.data, lzs.nbytes) == 0
     assert L.hoh_debug_read(c.h, 4, fpb.ctypes.data, fpb.nbytes) == 0
     F = fpb[:per].reshape(ntiles, cap)
-    TP = fpb[per:2 * per].reshape(ntiles, cap)
+    TP = fpb[per:2 * per].reshape(ntiles, cap) & 0xffffff                    # rgb | run8 << 24
     R8 = fpb[3 * per:].view(np.uint8)[:per].reshape(ntiles, cap)
     S = lzs[:per].reshape(ntiles, cap)
     T = lzs[per:2 * per].reshape(ntiles, cap)
