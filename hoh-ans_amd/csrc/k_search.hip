@@ -422,7 +422,7 @@ __device__ __forceinline__ uint32_t resid_all(const AllCtx& a, int x, int y) {
 // Task kinds: at -s2..-s4 one task per (plane, cell) walks every mask at once (cell_cost_multi,
 // k_search_walk_multi: its state is one LDS word per column, 42 x 64 lanes = 10.5 KB per wave);
 // at -s1, whose one full mask walks faster alone, a task per mask (cell_cost_one / cell_cost).
-__host__ __device__ inline bool walk_multi(int npred) { return npred == 10 || npred == 14; }
+__host__ __device__ inline bool walk_multi(int npred) { return npred == 5 || npred == 10 || npred == 14; }
 __host__ __device__ inline int walk_kinds(int npred) { return walk_multi(npred) ? 1 : npred; }
 #define WM_COLS 42
 struct WalkTask {
@@ -468,7 +468,8 @@ __global__ __launch_bounds__(64) void k_search_walk_multi(EncodeJob j, int npred
   WalkTask k;
   if (!walk_task(j, npred, ncmax, (uint64_t)blockIdx.x * 64 + lane, m, k)) return;
   const int cx = k.cell % k.xt, cy = k.cell / k.xt;
-  if (npred == 10) cell_cost_multi<6>(k.D, k.w, k.h, k.depth, k.xt, k.yt, cx, cy, k.ent, top + lane, pk + lane, k.ent + 512 + k.cell * 14);
+  if (npred == 5) cell_cost_multi<1>(k.D, k.w, k.h, k.depth, k.xt, k.yt, cx, cy, k.ent, top + lane, pk + lane, k.ent + 512 + k.cell * 14);
+  else if (npred == 10) cell_cost_multi<6>(k.D, k.w, k.h, k.depth, k.xt, k.yt, cx, cy, k.ent, top + lane, pk + lane, k.ent + 512 + k.cell * 14);
   else cell_cost_multi<10>(k.D, k.w, k.h, k.depth, k.xt, k.yt, cx, cy, k.ent, top + lane, pk + lane, k.ent + 512 + k.cell * 14);
 }
 

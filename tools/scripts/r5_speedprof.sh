@@ -1,0 +1,17 @@
+#!/bin/bash
+# Measurement (GPU box): the natural-image speed pipeline (tools/scripts/speed_pipe.py, D contexts)
+# under rocprofv3 --kernel-trace: per-kernel total time and share.  Usage: r5_speedprof.sh TAG SPEED D
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
+tag=$1; sp=$2; D=${3:-4}
+timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/$tag -o p -- python3 tools/scripts/speed_pipe.py $sp $D 6 \
+  > gpurun_out/$tag.log 2>&1 || { tail -5 gpurun_out/$tag.log; exit 1; }
+grep '^-s' gpurun_out/$tag.log
+python3 - gpurun_out/$tag <<'PY'
+import glob, sqlite3, sys
+db = sqlite3.connect(glob.glob(sys.argv[1] + "/*.db")[0])
+rows = db.execute("select name, count(*), sum(end-start)/1e6 from kernels group by name order by 3 desc").fetchall()
+tot = sum(r[2] for r in rows)
+for n, c, t in rows[:18]:
+    print("  %-40s %5d %10.1f %6.1f%%" % (n[:40], c, t, 100 * t / tot))
+PY
