@@ -576,7 +576,6 @@ __global__ __launch_bounds__(NT) void k_search(EncodeJob j, int phase, int pass)
       }
     }
     __syncthreads();
-    uint32_t rv[4];
     n = 0;
     for (int x = tid; x < w && n < 4; x += NT) {                      // resid_all(a, x, y)
       const uint32_t bA = y ? bcur[x] : 4u;
@@ -589,13 +588,11 @@ __global__ __launch_bounds__(NT) void k_search(EncodeJob j, int phase, int pass)
         preds_all_at(a, x, y, p);
       }
       const uint32_t pr = midp(pick(p, bA), pick(p, bB));
-      rv[n++] = ((uint32_t)((int)a.px(y, x) - (int)pr + half + c)) & (uint32_t)(c - 1);
-    }
-    __syncthreads();
-    n = 0;
-    for (int x = tid; x < w && n < 4; x += NT) {
-      if (!refine) D[(long)y * w + x] = (uint16_t)rv[n];
-      atomicAdd(&S.hist[rv[n]], 1u);
+      const uint32_t r = ((uint32_t)((int)a.px(y, x) - (int)pr + half + c)) & (uint32_t)(c - 1);
+      // no barrier before these: the residuals read rows y .. y - 2 of the ring, and row y - 3
+      // lands in row y + 1's slot (read last iteration, before the barrier that ended it)
+      if (!refine) D[(long)y * w + x] = (uint16_t)r;
+      atomicAdd(&S.hist[r], 1u);
       if (y >= 3) S.rows[(y - 3) & 3][x] = (uint16_t)nv[n];
       n++;
     }
