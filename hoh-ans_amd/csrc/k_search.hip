@@ -378,10 +378,11 @@ struct AllCtx {
   const uint16_t* D;
   int w, h, tw, th, xt, c, half;
   const uint16_t* plist;
-  const uint16_t* ring;   // k_search's final pass (use_ring): rows y - 2..y staged in LDS, row y at (y & 3) << 10
+  const uint16_t* ring;   // k_search's final pass (use_ring): original rows in LDS, row y at (y & rmask) << rsh
   bool use_ring;
+  int rmask, rsh;
   __device__ __forceinline__ uint32_t px(int y, int x) const {
-    return use_ring ? ring[((y & 3) << 10) + x] : D[(long)y * w + x];
+    return use_ring ? ring[((y & rmask) << rsh) + x] : D[(long)y * w + x];
   }
 };
 
@@ -520,7 +521,7 @@ __global__ __launch_bounds__(NT) void k_search(EncodeJob j, int phase, int pass)
   if (!grid) return;
   const int ncell = xt * yt, npred = j.speed * 5 < 14 ? j.speed * 5 : 14;
   const int tw = (w + xt - 1) / xt, th = (h + yt - 1) / yt;
-  AllCtx a{D, w, h, tw, th, xt, c, half, S.plist, D, false};
+  AllCtx a{D, w, h, tw, th, xt, c, half, S.plist, D, false, 3, 10};
   {
     for (int cell = tid; cell < ncell; cell += NT) {
       double best = 99999999999.0;                                // :177
@@ -546,6 +547,66 @@ __global__ __launch_bounds__(NT) void k_search(EncodeJob j, int phase, int pass)
   uint8_t* bcur = S.brow[1];
   for (int i = tid; i < w; i += NT) bnext[i] = 0;
   for (int i = tid; i < 512; i += NT) S.hist[i] = 0;
+  if (w <= 256) {
+    // Tiles up to 256 wide: bands of SB_R rows, two barriers a band.  A row's best predictors
+    // depend on original pixels only, so a band's (rows y_lo - 1 .. yb - 1; row yb's from the
+    // band before) are computed first, then all its residuals; the originals live in a 16-row LDS
+    // ring (the plane is overwritten in place: a band reads rows y_lo - 2 .. yb, the next band's
+    // new rows y_lo - SB_R - 2 .. y_lo - 3 are loaded meanwhile into other slots).
+    constexpr int SB_R = 4;
+    uint16_t* ring = &S.rows[0][0];                                   // [16][256]
+    uint8_t* bpb = &S.brow[0][0];                                     // [SB_R + 1][256]
+    a.ring = ring;
+    a.use_ring = true;
+    a.rmask = 15;
+    a.rsh = 8;
+    for (int r = max(0, h - SB_R - 2); r < h; r++)
+      if (tid < w) ring[((r & 15) << 8) + tid] = D[(long)r * w + tid];
+    uint32_t bkeep = 0;                                               // best predictor of (tid, yb): 0 in the last row
+    __syncthreads();
+    for (int yb = h - 1; yb >= 0; yb -= SB_R) {
+      const int y_lo = max(0, yb - SB_R + 1), nr = yb - y_lo + 1;
+      uint32_t nv[SB_R];
+#pragma unroll
+      for (int k = 0; k < SB_R; k++) {
+        const int r = y_lo - SB_R - 2 + k;
+        nv[k] = (r >= 0 && tid < w) ? D[(long)r * w + tid] : 0u;
+      }
+      // slot k: the best predictors of row y_lo - 1 + k (k = nr: row yb, kept from the band before)
+      if (tid < w) {
+        bpb[nr * 256 + tid] = (uint8_t)bkeep;
+        for (int k = 0; k < nr; k++) {
+          const int r = y_lo - 1 + k;
+          if (r < 0) continue;
+          Preds p;
+          preds_all_at(a, tid, r, p);
+          bpb[k * 256 + tid] = (uint8_t)best_pred(a.px(r, tid), p, a.plist[((r + 1) / th) * xt + tid / tw], c);
+        }
+      }
+      __syncthreads();
+      if (tid < w) {
+        const int x = tid;
+        for (int y = yb; y >= y_lo; y--) {
+          const int k = y - y_lo + 1;                                  // row y's slot
+          const uint32_t bA = y ? bpb[(k - 1) * 256 + x] : 4u;
+          const uint32_t bB = x ? bpb[k * 256 + x - 1] : (y ? bpb[(k - 1) * 256 + w - 1] : 4u);
+          Preds p;
+          preds_all_at(a, x, y, p);
+          const uint32_t pr = midp(pick(p, bA), pick(p, bB));
+          const uint32_t r = ((uint32_t)((int)a.px(y, x) - (int)pr + half + c)) & (uint32_t)(c - 1);
+          if (!refine) D[(long)y * w + x] = (uint16_t)r;
+          atomicAdd(&S.hist[r], 1u);
+        }
+        bkeep = bpb[x];                                                // row y_lo - 1: the next band's yb
+#pragma unroll
+        for (int k = 0; k < SB_R; k++) {
+          const int r = y_lo - SB_R - 2 + k;
+          if (r >= 0) ring[((r & 15) << 8) + x] = (uint16_t)nv[k];
+        }
+      }
+      __syncthreads();
+    }
+  } else {
   // the original rows in an LDS ring (the global plane is overwritten row by row): rows y, y - 1
   // and y - 2 are read at row y, row y - 3 is loaded meanwhile and lands in row y + 1's slot
   for (int k = 0; k < 3 && h - 1 - k >= 0; k++)
@@ -603,6 +664,7 @@ __global__ __launch_bounds__(NT) void k_search(EncodeJob j, int phase, int pass)
 #pragma unroll
     for (int k = 0; k < 8; k++) pc[k] = pn[k];
     have = keep && y > 0;
+  }
   }
   if (refine) {
     for (int i = tid; i < c; i += NT) ent[i] = lg[1 + S.hist[i]];
