@@ -41,7 +41,8 @@ __device__ __forceinline__ uint32_t med16s(uint32_t a, uint32_t b, uint32_t c) {
   return b < c ? b : (c > a ? c : a);
 }
 __device__ __forceinline__ uint32_t midp(uint32_t a, uint32_t b) {                 // :8-10
-  return (uint32_t)((int)a + ((int)b - (int)a) / 2);
+  // a + (b - a) / 2 (truncated) == (a + b + (b < a)) / 2 for a, b < 2^31 (every value here is u16)
+  return (a + b + (b < a ? 1u : 0u)) >> 1;
 }
 __device__ __forceinline__ uint32_t avg3(uint32_t a, uint32_t b, uint32_t c) { return (a + b + c) / 3; }   // :66-68
 __device__ __forceinline__ uint32_t paeth(int A, int B, int C) {                   // :89-106
@@ -320,7 +321,10 @@ __device__ void cell_cost_multi(const uint16_t* D, int w, int h, int depth, int 
       for (int k = 0; k < 16; k++) {
         // |v - p_k| by v_sad_u16 (values < 2^16: the high halves are 0)
         const uint32_t key = (__builtin_amdgcn_sad_u16(v, p.v[k], 0u) << 4) | (uint32_t)k;
-        k2 = min(k2, max(k1, key));
+        // k1 <= k2 always, so the new second smallest is the median of the three
+        uint32_t k2n;
+        asm("v_med3_u32 %0, %1, %2, %3" : "=v"(k2n) : "v"(k1), "v"(k2), "v"(key));
+        k2 = k2n;
         k1 = min(k1, key);
         if (k == 1) kp = k1;                                            // the pair {0, 1}'s key
       }
