@@ -121,11 +121,29 @@ __global__ __launch_bounds__(64 * LZ_SEG) void k_lz(EncodeJob j) {
   auto measure = [&](uint32_t q) -> uint32_t {
     fill_to(q >= 64 ? q - 64 : 0, q + 260);
     const uint32_t b = lane + 1;
+    const uint32_t lim = min(259u, npix - q);
     uint32_t L = 0;
-    if (b <= q) {
+    // Inside a run of equal pixels (q - 1 equals q): for every back b whose q - b .. q - 1 are
+    // all that pixel the copy runs exactly to the end of q's own run (the older side still holds
+    // the pixel where q's run has ended), so those lanes take q's run length (64 positions per
+    // LDS read) instead of comparing 16 at a time up to 259.
+    bool inrun = false;
+    const uint32_t c0 = rg[q & (LZR - 1)];
+    if (q >= 1 && rg[(q - 1) & (LZR - 1)] == c0) {                     // wave-uniform
+      const uint64_t m = __ballot(b <= q && rg[(q - b) & (LZR - 1)] == c0);
+      const uint32_t B = ~m ? (uint32_t)(__ffsll((unsigned long long)~m) - 1) : 64u;   // backs 1..B in the run
+      uint32_t rq = 0;
+      for (;;) {
+        const uint64_t e = __ballot(rq + lane < lim && rg[(q + rq + lane) & (LZR - 1)] == c0);
+        if (~e) { rq += (uint32_t)(__ffsll((unsigned long long)~e) - 1); break; }
+        rq += 64;
+      }
+      inrun = b <= B;
+      if (inrun) L = rq;
+    }
+    if (b <= q && !inrun) {
       // sixteen positions per LDS round trip from two bases (the mirror spares every read its
       // wrap), the first unequal one by a select chain
-      const uint32_t lim = min(259u, npix - q);
       for (;;) {
         const uint32_t* pa = rg + ((q + L) & (LZR - 1));
         const uint32_t* pc = rg + ((q + L - b) & (LZR - 1));
