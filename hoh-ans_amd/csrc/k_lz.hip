@@ -417,12 +417,19 @@ __device__ __forceinline__ void nuke_tile(const EncodeJob& j, int t, uint32_t* n
   }
   if (np == 0) return;
   uint32_t outc = 0;
+  // the next block's values are loaded before this block's ranks (they lie above every write of
+  // this block: a block's writes land below its own end)
+  uint16_t vn[2 * HOH_NPLANE_S];
+#pragma unroll
+  for (int k = 0; k < 2 * HOH_NPLANE_S; k++) vn[k] = (k < np && (uint32_t)tid < npix) ? r[k][tid] : 0;
   for (uint32_t base = 0; base < npix; base += 256) {
     const uint32_t p = base + tid;
     const bool valid = p < npix;
     uint16_t v[2 * HOH_NPLANE_S];
 #pragma unroll
-    for (int k = 0; k < 2 * HOH_NPLANE_S; k++) v[k] = (k < np && valid) ? r[k][p] : 0;
+    for (int k = 0; k < 2 * HOH_NPLANE_S; k++) v[k] = vn[k];
+#pragma unroll
+    for (int k = 0; k < 2 * HOH_NPLANE_S; k++) vn[k] = (k < np && p + 256 < npix) ? r[k][p + 256] : 0;
     const bool nuked = valid && (in_lds ? ((nk_bits[p >> 5] >> (p & 31)) & 1) : nuked_search(mt, nm, p));
     if (nuked) {                                        // counted in LDS, applied once below
 #pragma unroll
