@@ -155,50 +155,133 @@ def pmc_probe(args):
     print(json.dumps({"probe": "ok", "n": n}))
 
 
-def pmc_traffic_live(args):
-    """HBM bytes per launch of each main kernel, from two rocprofv3 --pmc passes (FETCH_SIZE and
-    WRITE_SIZE do not fit one pass) over `bench.py --pmc-probe`.  Returns (per-kernel dict, note)."""
+def pmc_passes(passes, probe_argv, keep_last=None):
+    """Run `bench.py <probe_argv>` under one rocprofv3 --pmc pass per entry of `passes` (each a
+    tuple of counters that fits one pass), each under timeout -s KILL.  Returns ({kernel base name:
+    {"launches": n, "ns": summed dispatch durations, counter: summed value}}, error or None).
+    keep_last: keep only each kernel's last `keep_last` fraction of dispatches (the probe's final
+    encode, past first-call set-up)."""
     exe = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(exe):
         return None, "rocprofv3 not found"
-    vals = {}
+    res = {}
     tmp = tempfile.mkdtemp(prefix="hohpmc", dir="/tmp")
     try:
-        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
-            d = os.path.join(tmp, ctr)
-            cmd = ["timeout", "-s", "KILL", "150", exe, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "p",
-                   "--", sys.executable, os.path.abspath(__file__), "--pmc-probe", "--size", str(args.size),
-                   "--seed", str(args.seed), "--noise", str(args.noise)]
+        for i, ctrs in enumerate(passes):
+            d = os.path.join(tmp, "p%d" % i)
+            cmd = ["timeout", "-s", "KILL", "150", exe, "--pmc", *ctrs, "--output-format", "csv", "-d", d, "-o", "p",
+                   "--", sys.executable, os.path.abspath(__file__), *probe_argv]
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=180)
             files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
             if r.returncode != 0 or not files:
-                return None, "rocprofv3 --pmc %s failed (rc %d): %s" % (ctr, r.returncode, (r.stderr or "")[-200:])
-            acc, disp = {}, {}
+                return None, "rocprofv3 --pmc %s failed (rc %d): %s" % (" ".join(ctrs), r.returncode, (r.stderr or "")[-200:])
+            per = {}     # kernel -> {dispatch: [ns, {ctr: value}]}
             for row in csv.DictReader(open(files[0])):
-                if row.get("Counter_Name") != ctr:
+                if row.get("Counter_Name") not in ctrs:
                     continue
                 k = row["Kernel_Name"].split("(")[0].replace("void ", "").split("<")[0].strip()
-                name = PMC_KERNELS.get(k)
-                if name is None:
-                    continue
-                acc[name] = acc.get(name, 0.0) + float(row["Counter_Value"]) * 1024.0   # KB
-                disp.setdefault(name, set()).add(row["Dispatch_Id"])
-            for name in acc:
-                vals.setdefault(name, {})[ctr] = acc[name] / len(disp[name])
+                dd = per.setdefault(k, {}).setdefault(int(row["Dispatch_Id"]),
+                                                       [int(row["End_Timestamp"]) - int(row["Start_Timestamp"]), {}])
+                dd[1][row["Counter_Name"]] = dd[1].get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
+            for k, disp in per.items():
+                ids = sorted(disp)
+                if keep_last:
+                    ids = ids[len(ids) - max(1, int(round(len(ids) * keep_last))):]
+                e = res.setdefault(k, {})
+                if "launches" not in e:
+                    e["launches"] = len(ids)
+                    e["ns"] = sum(disp[j][0] for j in ids)
+                for c in ctrs:
+                    e[c] = sum(disp[j][1].get(c, 0.0) for j in ids)
+                e.setdefault("n_" + str(i), len(ids))
     except Exception as e:      # reported, never invented
         return None, "pmc: %r" % (e,)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
+    return res, None
+
+
+def pmc_traffic_live(args):
+    """HBM bytes per launch of each main kernel, from two rocprofv3 --pmc passes (FETCH_SIZE and
+    WRITE_SIZE do not fit one pass) over `bench.py --pmc-probe`.  Returns (per-kernel dict, note)."""
+    res, err = pmc_passes([("FETCH_SIZE",), ("WRITE_SIZE",)],
+                          ["--pmc-probe", "--size", str(args.size), "--seed", str(args.seed), "--noise", str(args.noise)])
+    if err:
+        return None, err
+    vals = {}
+    for k, e in res.items():
+        name = PMC_KERNELS.get(k)
+        if name is None or "FETCH_SIZE" not in e or "WRITE_SIZE" not in e:
+            continue
+        v = vals.setdefault(name, {"FETCH_SIZE": 0.0, "WRITE_SIZE": 0.0, "n0": 0, "n1": 0})
+        v["FETCH_SIZE"] += e["FETCH_SIZE"] * 1024.0    # KB
+        v["WRITE_SIZE"] += e["WRITE_SIZE"] * 1024.0
+        v["n0"] += e.get("n_0", 0)
+        v["n1"] += e.get("n_1", 0)
     out = {}
     for name, v in vals.items():
-        if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
-            out[name] = {"fetch_raw": round(v["FETCH_SIZE"]), "write": round(v["WRITE_SIZE"]),
-                         "hbm_bytes": round(2 * v["FETCH_SIZE"] + v["WRITE_SIZE"])}
+        if v["n0"] and v["n1"]:
+            f, w = v["FETCH_SIZE"] / v["n0"], v["WRITE_SIZE"] / v["n1"]
+            out[name] = {"fetch_raw": round(f), "write": round(w), "hbm_bytes": round(2 * f + w)}
     return out, "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE (separate passes), bench.py --pmc-probe, " \
                 "per launch; hbm_bytes = 2 x FETCH_SIZE (gfx950 correction) + WRITE_SIZE"
 
 
-# ------------------------------------------------------------------------------ CPU baseline
+def pmc_probe_speed(args):
+    """Child of rocprofv3 --pmc: configs[4]'s natural image encoded twice at choh -s<speed>."""
+    import torch
+    import hoh_ans
+    W, H = args.size, args.size
+    ctx = hoh_ans.Context(0)
+    rgb = hoh_ans.natural_rgb_dev(W, H, args.seed, ctx=ctx)
+    out = torch.empty(hoh_ans.lib().hoh_encode_bound(W, H), dtype=torch.uint8, device="cuda")
+    for _ in range(2):
+        _, n, _ = hoh_ans.encode_image(rgb, W, H, out_dev=out, ctx=ctx, speed=args.pmc_probe_speed)
+    torch.cuda.synchronize()
+    print(json.dumps({"probe": "ok", "n": n}))
+
+
+SPEED_PMC_TOP = 8        # kernels reported per speed, by summed duration
+VALU_SIMDS = 1024        # 256 CUs x 4 SIMDs
+VALU_CYCLES = 2          # measured: one wave64 VALU instruction issues per 2 cycles per SIMD (DESIGN.md)
+CLOCK_HZ = 2.4e9         # MI355X max engine clock (MI355X_MICROARCH.md)
+
+
+def speed_roofline_live(args, speed):
+    """Roofline fractions of the -s<speed> encode's kernels (k_lzscan,
+    k_search_walk_multi, k_search ...), from three rocprofv3 --pmc passes over `bench.py
+    --pmc-probe-speed`: FETCH_SIZE | WRITE_SIZE | SQ_INSTS_VALU + SQ_INSTS_LDS, the second encode's
+    dispatches only.  Per kernel, per launch: HBM bytes (2 x FETCH_SIZE + WRITE_SIZE), duration
+    (dispatch timestamps of the FETCH pass: the profiler serialises dispatches, so this is the
+    kernel alone, not beside the other stream), hbm GB/s and its fraction of 8 TB/s, and the VALU
+    issue fraction = VALU wave-instructions x 2 cycles / (duration x 1024 SIMDs x 2.4 GHz)."""
+    res, err = pmc_passes([("FETCH_SIZE",), ("WRITE_SIZE",), ("SQ_INSTS_VALU", "SQ_INSTS_LDS")],
+                          ["--pmc-probe-speed", str(speed), "--size", str(args.size), "--seed", str(args.seed)],
+                          keep_last=0.5)
+    if err:
+        return {"error": err}
+    rows = []
+    for k, e in res.items():
+        if not e.get("launches") or "FETCH_SIZE" not in e or "WRITE_SIZE" not in e:
+            continue
+        n = e["launches"]
+        ns = e["ns"] / n
+        hb = (2 * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024.0 / n
+        valu = e.get("SQ_INSTS_VALU", 0.0) / n
+        r = {"launches_per_encode": n, "ms": round(ns / 1e6, 4), "hbm_bytes": round(hb),
+             "hbm_GBps": round(hb / ns, 1) if ns else None,
+             "hbm_frac": round(hb / ns / HBM_PEAK_GBS, 4) if ns else None,
+             "valu_insts": round(valu), "lds_insts": round(e.get("SQ_INSTS_LDS", 0.0) / n),
+             "valu_frac": round(valu * VALU_CYCLES / (ns * 1e-9 * VALU_SIMDS * CLOCK_HZ), 4) if ns else None}
+        rows.append((e["ns"], k, r))
+    rows.sort(reverse=True)
+    out = {k: r for _, k, r in rows[:SPEED_PMC_TOP]}
+    out["source"] = ("rocprofv3 --pmc, 3 passes over bench.py --pmc-probe-speed %d (natural %dx%d, second "
+                     "encode); durations are each kernel alone (the profiler serialises dispatches); "
+                     "valu_frac = VALU x %d cycles / (ms x %d SIMDs x %.1f GHz)"
+                     % (speed, args.size, args.size, VALU_CYCLES, VALU_SIMDS, CLOCK_HZ / 1e9))
+    return out
+
 
 def cpu_baseline(rgb_host, W, H, args):
     """The reference's CPU hot path (oracle/_ref, compiled from its own sources) on the bench
@@ -725,11 +808,17 @@ def main():
     ap.add_argument("--batch-only", action="store_true",
                     help="N = 1: the timed batched leg alone (no one-in-flight / no-index / roofline detail)")
     ap.add_argument("--pmc-probe", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-probe-speed", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-speed", type=int, default=4,
+                    help="the -sN encode whose kernels get live PMC roofline fractions (0: none)")
     args = ap.parse_args()
     if args.size <= 0:
         args.size = STRONG_SIDE if args.strong else 8192
     if args.pmc_probe:
         pmc_probe(args)
+        return
+    if args.pmc_probe_speed >= 0:
+        pmc_probe_speed(args)
         return
     sharded0 = int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.sharded
     if args.batch <= 0:
@@ -745,12 +834,17 @@ def main():
     sharded = world > 1 or args.sharded
 
     # live PMC traffic first, before this process initialises the GPU
-    pmc, pmc_note = None, "skipped"
+    pmc, pmc_note, pmc_speed = None, "skipped", None
     if world == 1 and not args.no_pmc and not sharded:
         if under_profiler():
             pmc_note = "skipped: the bench itself runs under a profiler"
         else:
             pmc, pmc_note = pmc_traffic_live(args)
+            if args.pmc_speed > 0 and not args.no_legs and not args.batch_only:
+                try:
+                    pmc_speed = speed_roofline_live(args, args.pmc_speed)
+                except Exception as e:      # reported, never invented
+                    pmc_speed = {"error": repr(e)[:300]}
 
     # hardware queues (HIP reads GPU_MAX_HW_QUEUES at runtime init).  The batched N = 1 path runs
     # at HIP's default (4 queues: nothing is set); the single-image paths (--batch 1, and the N > 1
@@ -772,7 +866,7 @@ def main():
     elif args.batch > 1 and args.batch_only:
         batch_main(args, D, args.batch, dev, torch, hoh_ans, hd)
     else:
-        single_main(args, D, dev, torch, hoh_ans, hd, pmc, pmc_note)
+        single_main(args, D, dev, torch, hoh_ans, hd, pmc, pmc_note, pmc_speed)
 
 
 def roofline_obj(kms, kavg, ratio, rows_raw, raw_total, K, el, pmc, B=1):
@@ -1005,7 +1099,7 @@ def batch_main(args, D, B, dev, torch, hoh_ans, hd):
         sys.exit(3)
 
 
-def single_main(args, D, dev, torch, hoh_ans, hd, pmc, pmc_note):
+def single_main(args, D, dev, torch, hoh_ans, hd, pmc, pmc_note, pmc_speed):
     """N = 1: D slots of B = --batch images each (B * D images in flight), enqueue-only encode +
     decode, no host round trip per step.  B > 1: one step encodes and decodes the slot's B images
     through the batched calls (hoh_encode_images_async / hoh_decode_images_async: every kernel
@@ -1217,6 +1311,7 @@ def single_main(args, D, dev, torch, hoh_ans, hd, pmc, pmc_note):
             "kernel_avg_ms_one_in_flight": {k: round(v, 4) for k, v in iso.items()},
             "pmc_hbm_bytes_per_launch": pmc,
             "pmc_source": pmc_note,
+            "speed_roofline_s%d" % args.pmc_speed: pmc_speed,
         },
     }
     if not args.no_config2:
