@@ -241,6 +241,7 @@ def pmc_probe_speed(args):
     print(json.dumps({"probe": "ok", "n": n}))
 
 
+PMC_SETUP_KERNELS = ("k_natural", "k_synth")   # the probe's input generation, not the encode
 SPEED_PMC_TOP = 8        # kernels reported per speed, by summed duration
 VALU_SIMDS = 1024        # 256 CUs x 4 SIMDs
 VALU_CYCLES = 2          # measured: one wave64 VALU instruction issues per 2 cycles per SIMD
@@ -262,7 +263,7 @@ def speed_roofline_live(args, speed):
         return {"error": err}
     rows = []
     for k, e in res.items():
-        if not e.get("launches") or "FETCH_SIZE" not in e or "WRITE_SIZE" not in e:
+        if not e.get("launches") or "FETCH_SIZE" not in e or "WRITE_SIZE" not in e or k in PMC_SETUP_KERNELS:
             continue
         n = e["launches"]
         ns = e["ns"] / n

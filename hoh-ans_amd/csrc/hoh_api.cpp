@@ -423,6 +423,7 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
       j.lzrank = (uint16_t*)((uint32_t*)c->lzs.p + 2 * per);
       j.lzend = j.lzrank + per;
       j.lzs_hmask = (uint32_t)HOH_KNOB(LZS_HMASK, 0xffff);
+      j.cus = c->cus;
     }
     j.pinfo = (PlaneInfo*)c->pinfo.p;
     j.trials = (uint32_t*)(j.pinfo + (size_t)ntiles * HOH_NPLANE_S);

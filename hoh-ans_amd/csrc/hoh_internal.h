@@ -197,6 +197,7 @@ struct EncodeJob {
                           //   ascending inside a group: pos | hash << 16 (k_lzsort); null: no posting lists
   uint16_t* lzrank;       //   [tile][npix_cap] index of each position in lzs (flat run-inner positions: their run start's)
   uint32_t lzs_hmask;     //   the posting hash's mask (0xffff; knob LZS_HMASK in measurement builds)
+  int cus;                //   compute units of the device (k_lzsort's grid: one tile workgroup per CU)
   uint16_t* lzend;        //   [tile][npix_cap] per lzs entry: the last position of a flat run start's run, else the position
   PlaneInfo* pinfo;       // -s>=1: [tile][6]
   uint32_t* trials;       // -s>=1 with ladder pruning: the sids of the trials k_prune_s keeps (else null)

@@ -1177,7 +1177,9 @@ __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring,
 // j.lzs_hmask is 0xffff; a knobs build can narrow it (LZS_HMASK) so that hash collisions are the rule
 // (tools/scripts/r5_collide.sh: the files must not change)
 __device__ __forceinline__ uint32_t lzs_hash(uint32_t f, uint32_t hm) { return ((f * 0x9E3779B1u) >> 16) & hm; }
-#define LZSORT_T 256
+#ifndef LZSORT_T
+#define LZSORT_T 1024         // threads per tile (one wave per contiguous share of the positions)
+#endif
 __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
   // Stable LSD counting sort by the 16-bit hash, two 8-bit passes.  Each wave owns a contiguous
   // quarter of the pass's input and ranks it alone (64 at a time: ballot peers per digit, a
@@ -1187,7 +1189,10 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
   __shared__ uint32_t cnt[LZSORT_T / 64][256];                   // per wave: digit counts, then bases
   __shared__ uint32_t inner[65536 / 32];                         // flat positions inside a run (unlisted)
   __shared__ uint32_t s_nl;
-  const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // tiles strided over the grid (a smaller grid keeps fewer tiles' scatter targets in L2 at once)
+  for (int t = blockIdx.x; t < j.ntiles; t += gridDim.x) {
+  __syncthreads();                                               // the previous tile done
   const TileInfo ti = j.tiles[t];
   const uint32_t n = (uint32_t)ti.w * ti.h;
   const size_t per = (size_t)j.ntiles * j.npix_cap;
@@ -1234,7 +1239,7 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
       return peers;
     };
 #pragma unroll
-    for (int k = 0; k < 4; k++) cnt[wv][lane + 64 * k] = 0;
+    for (int k = 0; k < 4; k++) cnt[wv][lane + 64 * k] = 0;        // each wave its own row
     __syncthreads();                                               // inner / the previous pass done
     // 1. this wave's listed count per digit
     uint32_t kn = key_at(lo + lane);
@@ -1247,12 +1252,13 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
       if (listed && __popcll(lp & lt) == 0) cnt[wv][d] += (uint32_t)__popcll(lp);
     }
     __syncthreads();
-    // 2. bases: digits in order, the waves in order inside a digit
+    // 2. bases: digits in order, the waves in order inside a digit (threads 0..255: digit tid)
     {
-      const uint32_t d = (uint32_t)tid;
+      const uint32_t d = (uint32_t)tid & 255u;
+      const bool dg = tid < 256;
       uint32_t c[LZSORT_T / 64], tot = 0;
 #pragma unroll
-      for (int w = 0; w < LZSORT_T / 64; w++) { c[w] = cnt[w][d]; tot += c[w]; }
+      for (int w = 0; w < LZSORT_T / 64; w++) { c[w] = dg ? cnt[w][d] : 0u; tot += c[w]; }
       // exclusive scan of the 256 digit totals (thread d holds digit d)
       uint32_t incl = tot;
 #pragma unroll
@@ -1261,14 +1267,16 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
         if (lane >= o) incl += u;
       }
       __syncthreads();                                             // every count read
-      if (lane == 63) cnt[0][wv] = incl;                           // wave totals (digits 64wv..)
+      if (dg && lane == 63) cnt[0][wv] = incl;                     // wave totals (digits 64wv..)
       __syncthreads();
       uint32_t run = incl - tot;
-      for (int w = 0; w < wv; w++) run += cnt[0][w];
-      if (pass && tid == LZSORT_T - 1) s_nl = run + tot;           // listed positions
+      for (int w = 0; w < wv && w < 4; w++) run += cnt[0][w];
+      if (pass && tid == 255) s_nl = run + tot;                    // listed positions
       __syncthreads();
+      if (dg) {
 #pragma unroll
-      for (int w = 0; w < LZSORT_T / 64; w++) { cnt[w][d] = run; run += c[w]; }
+        for (int w = 0; w < LZSORT_T / 64; w++) { cnt[w][d] = run; run += c[w]; }
+      }
     }
     __syncthreads();
     // 3. scatter in order: rank = the wave's running base of the digit + listed peers before
@@ -1306,6 +1314,7 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
     }
     E[i] = (uint16_t)e;
   }
+  }
 }
 
 #define LZS_KB 0x1ffffu      // k_lzscan keys: (L << 17) | (LZS_KB - b)
@@ -1325,8 +1334,9 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
 // the window when the run's last listed position (E - 3) is; a hash collision steps on.  A thread
 // per position, every candidate word written (k_lzvert then adds the vertical ones).  It replaces
 // k_lzcand's hash tables / global map for these tiles.
+#define LZSCREEN_G 16         // workgroups per tile
 __global__ __launch_bounds__(256) void k_lzscreen(EncodeJob j, int limit) {
-  const int t = blockIdx.y, lane = threadIdx.x & 63;
+  const int t = blockIdx.y, bx = blockIdx.x, lane = threadIdx.x & 63;
   const TileInfo ti = j.tiles[t];
   const uint32_t npix = (uint32_t)ti.w * ti.h;
   const size_t o = (size_t)t * j.npix_cap;
@@ -1339,7 +1349,7 @@ __global__ __launch_bounds__(256) void k_lzscreen(EncodeJob j, int limit) {
   const uint16_t* PE = j.lzend + o;
   uint64_t* cand = j.candbits + (size_t)t * (j.npix_cap / 64);
   uint32_t ncand = 0;
-  for (uint32_t q0 = blockIdx.x * 256u; q0 < npix; q0 += gridDim.x * 256u) {
+  for (uint32_t q0 = bx * 256u; q0 < npix; q0 += LZSCREEN_G * 256u) {
     const uint32_t q = q0 + threadIdx.x;
     bool c = false;
     const uint32_t f = q < npix ? F[q] : 0u;
@@ -2154,8 +2164,14 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, v
     const int lring = mode == LZC_MAP ? 2 * NT : ring;
     const size_t lds = (size_t)(lring + (mode == LZC_TAB ? 3 * LZC_W : 0) + (mode != LZC_WALK ? 2 * LZC_C : 0)) * 4;
     if (j.lzs) {                      // posting lists: the screen is their first hit (k_lzscreen)
-      hipLaunchKernelGGL(k_lzsort, dim3(j.ntiles), dim3(LZSORT_T), 0, sl, j);
-      hipLaunchKernelGGL(k_lzscreen, dim3(16, j.ntiles), dim3(256), 0, sl, j, limit);
+      // one 1024-thread workgroup per CU striding over the tiles: against a workgroup per tile
+      // (1024 in flight) the scatter targets of 4x fewer tiles share the L2s, the launch leaves
+      // most of each CU to the predictor search beside it, and the natural 8192^2 encodes drop
+      // by 1.4-1.7 ms at -s1..-s4 (k_lzsort 5.2 -> 3.7 ms at -s1; tools/scripts/r5_ab_lzsort.sh)
+      const int sgk = HOH_KNOB(LZSORT_GRID, 0);                      // 0: the CU count
+      const int sg = sgk > 0 ? sgk : j.cus > 0 ? j.cus : 256;
+      hipLaunchKernelGGL(k_lzsort, dim3(sg > 0 && sg < j.ntiles ? sg : j.ntiles), dim3(LZSORT_T), 0, sl, j);
+      hipLaunchKernelGGL(k_lzscreen, dim3(LZSCREEN_G, j.ntiles), dim3(256), 0, sl, j, limit);
     } else {
       hipLaunchKernelGGL(k_lzcand, dim3(j.ntiles), dim3(NT), lds, sl, j, limit, lring, mode, mw, HOH_KNOB(LZC_NOWALK, 0));
     }
