@@ -1383,7 +1383,11 @@ __global__ __launch_bounds__(256) void k_lzscreen(EncodeJob j, int limit) {
 // nseg waves per tile (LZS_SEG, each with its own pixel ring): the tile's walk
 // is cut into segments walked at once and stitched by wave 0, exactly as k_lz does at -s0
 // (segment matches packed into lzspec as two words: pos | (len - 4) << 16, back).
-__global__ __launch_bounds__(64 * LZS_SEG) void k_lzscan(EncodeJob j, int limit, int rp, int nseg_req, int hls) {
+// OCC: waves per SIMD the register allocation is held to (0: the compiler's choice, 122 VGPRs,
+// four workgroups per CU); the -s3/-s4 scan runs at five with 512-position rings (below)
+template <int OCC>
+__global__ __launch_bounds__(64 * LZS_SEG) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1, OCC ? OCC : 10)))
+void k_lzscan(EncodeJob j, int limit, int rp, int nseg_req, int hls) {
   // dynamic LDS: nseg rings of rp + 16 positions, then nseg hit lists of hls entries (a batch's
   // hits: 64 with posting lists, LZS_HB * 64 for the window walk)
   extern __shared__ uint32_t pring_all[];
@@ -2186,12 +2190,18 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, v
     // walks of round 5, 1024-position rings (33 KB: four workgroups per CU, an 8192^2 image's
     // 1024 tiles in one round) against 2048: -s3 k_lzscan 16.3 -> 10.2 ms, -s4 18.9 -> 17.3.
     // knobs LZS_RING_MAX / LZS_SEG (measurement).
-    if (rp > lzs_ring_max()) rp = lzs_ring_max();
-    if (rp < 1024) rp = 0;
+    // -s3/-s4 (windows of 8192 / 16384, most backs beyond any ring): 512-position rings and the
+    // registers held to five waves per SIMD (25 KB: five workgroups per CU instead of four) --
+    // natural -s4 37.5 -> 34.9 ms; at -s1 the 1024 rings stay (24.5 against 25.4 ms)
+    const bool occ5 = j.speed >= HOH_KNOB(LZS_OCC_SPEED, 3);
+    const int rmax = occ5 ? HOH_KNOB(LZS_RING_HI, 512) : lzs_ring_max();
+    if (rp > rmax) rp = rmax;
+    if (rp < (occ5 ? 512 : 1024)) rp = 0;
     const int nseg = rp ? lzs_seg() : 1;
     const int hls = j.lzs ? 64 : LZS_HB * 64;
     const size_t dyn = (size_t)nseg * (rp ? rp + 16 : 1) * 4 + (size_t)nseg * hls * 2;
-    hipLaunchKernelGGL(k_lzscan, dim3(j.ntiles), dim3(64 * LZS_SEG), dyn, sl, j, limit, rp, nseg, hls);
+    if (occ5) hipLaunchKernelGGL(k_lzscan<5>, dim3(j.ntiles), dim3(64 * LZS_SEG), dyn, sl, j, limit, rp, nseg, hls);
+    else hipLaunchKernelGGL(k_lzscan<0>, dim3(j.ntiles), dim3(64 * LZS_SEG), dyn, sl, j, limit, rp, nseg, hls);
   }
   // the join: if its record fails, s waits for the whole side stream instead
   const bool joined = fork && hipEventRecord(side.join, sl) == hipSuccess;
