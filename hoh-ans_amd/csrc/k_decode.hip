@@ -545,7 +545,26 @@ __device__ __forceinline__ uint32_t dstep(uint32_t bk, uint32_t sy, uint32_t bma
 // per-symbol chain is LDS round trips only and five workgroups fit a CU (staging the whole payload
 // needed a 40 KB stage and allowed three); the symbol stores are never awaited.
 // Output is the flat plane: each thread stores its segment 16 symbols (32 B) at a time.
-__global__ __launch_bounds__(DR_T) void k_drans(DecJob j, int nstreams) {
+// k_drans's registers held to 4 waves per SIMD (128 VGPRs, was 129: three workgroups per CU
+// where its 28 KB of LDS allows five; a 12-byte spill): batched decode 0.476 -> 0.459 ms/image,
+// the headline pipeline +0.5 % (5 waves: 96 VGPRs, a 124-byte spill, 0.51 ms/image)
+#ifndef DRANS_WPE
+#define DRANS_WPE 4
+#endif
+#ifndef DUNF_WPE
+#define DUNF_WPE 0
+#endif
+#if DRANS_WPE
+#define DRANS_ATTR __attribute__((amdgpu_waves_per_eu(DRANS_WPE, DRANS_WPE)))
+#else
+#define DRANS_ATTR
+#endif
+#if DUNF_WPE
+#define DUNF_ATTR __attribute__((amdgpu_waves_per_eu(DUNF_WPE, DUNF_WPE)))
+#else
+#define DUNF_ATTR
+#endif
+__global__ __launch_bounds__(DR_T) DRANS_ATTR void k_drans(DecJob j, int nstreams) {
   extern __shared__ __attribute__((aligned(16))) uint32_t dr_lds[];
   uint32_t* wtot = dr_lds + (DR_FIXED + DR_RW * DR_T * 4) / 4;
   // dec_abort through the dynamic area (read before the barrier that follows the table clear)
@@ -1638,7 +1657,7 @@ __device__ __forceinline__ void dunpred_fast_tile(const DecJob& j, const DecTile
   }
 }
 
-__global__ __launch_bounds__(64) void k_dunpred_fast(DecJob j) {
+__global__ __launch_bounds__(64) DUNF_ATTR void k_dunpred_fast(DecJob j) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   if (dec_abort(j)) return;
   const int t = blockIdx.x;
