@@ -357,7 +357,18 @@ __host__ __device__ static inline int nuke_slots(const EncodeJob& j) { return j.
 
 // A small grid strides over the tiles (most have no match): a launch over every tile dispatches
 // ~1000 idle workgroups, which waits for free CUs when other images are in flight.
-__global__ __launch_bounds__(256) void k_nuke(EncodeJob j, int in_lds) {
+// registers held to 6 waves per SIMD (80 VGPRs, was 116: four workgroups per CU where the 16 KB
+// of LDS allows nine; a 112-byte spill): natural -s0 pipeline 47.8 -> 48.7 GB/s (8 waves, 64
+// VGPRs: 47.5)
+#ifndef NUKE_WPE
+#define NUKE_WPE 6
+#endif
+#if NUKE_WPE
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NUKE_WPE, NUKE_WPE)))
+#else
+__global__ __launch_bounds__(256)
+#endif
+void k_nuke(EncodeJob j, int in_lds) {
   extern __shared__ uint32_t nk_bits[];                  // npix_cap / 32 words, then the counts
   __shared__ uint32_t wsum[4];
   for (int t = blockIdx.x; t < j.ntiles; t += gridDim.x) nuke_tile(j, t, nk_bits, wsum, in_lds != 0);
