@@ -193,12 +193,14 @@ struct EncodeJob {
   uint32_t* fpt;          // -s>=1: [tile][npix_cap] the fingerprints transposed, FT[x * h + y] (k_lzfp)
   uint8_t* run8;          // -s>=1: [tile][npix_cap] length of the run of equal pixels from each position
                           //   (tile raster order, 1..254 exact, 255 = at least 255)
-  uint32_t* lzs;          // -s>=2, tiles <= 65536 px: [tile][npix_cap] positions grouped by hash16(fingerprint),
-                          //   ascending inside a group: pos | hash << 16 (k_lzsort); null: no posting lists
-  uint16_t* lzrank;       //   [tile][npix_cap] index of each position in lzs (flat run-inner positions: their run start's)
+  uint32_t* lzs;          // -s>=1, tiles <= 65536 px: [tile][npix_cap] k_lzsort's first-pass keys; null: no
+                          //   posting lists.  The lists themselves are lzsf: positions grouped by
+                          //   hash16(fingerprint), ascending inside a group
+  uint16_t* lzrank;       //   [tile][npix_cap] index of each position in lzsf (flat run-inner positions: their run start's)
   uint32_t lzs_hmask;     //   the posting hash's mask (0xffff; knob LZS_HMASK in measurement builds)
   int cus;                //   compute units of the device (k_lzsort's grid: one tile workgroup per CU)
-  uint16_t* lzend;        //   [tile][npix_cap] per lzs entry: the last position of a flat run start's run, else the position
+  uint16_t* lzend;        //   [tile][npix_cap] per lzsf entry: the last position of a flat run start's run, else the position
+  uint64_t* lzsf;         //   [tile][npix_cap] the listed positions in order: key (pos | hash << 16) | fingerprint << 32
   PlaneInfo* pinfo;       // -s>=1: [tile][6]
   uint32_t* trials;       // -s>=1 with ladder pruning: the sids of the trials k_prune_s keeps (else null)
   uint32_t* ntrial;       // their count (zeroed per encode)

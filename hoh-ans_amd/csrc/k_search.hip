@@ -1195,12 +1195,13 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
   __syncthreads();                                               // the previous tile done
   const TileInfo ti = j.tiles[t];
   const uint32_t n = (uint32_t)ti.w * ti.h;
-  const size_t per = (size_t)j.ntiles * j.npix_cap;
   const uint32_t* F = j.fpb + (size_t)t * j.npix_cap;
   const uint32_t* TP = j.tpx + (size_t)t * j.npix_cap;
   const uint8_t* R8 = j.run8 + (size_t)t * j.npix_cap;
-  uint32_t* S = j.lzs + (size_t)t * j.npix_cap;                   // final order
-  uint32_t* T = j.lzs + per + (size_t)t * j.npix_cap;             // after the first pass
+  // final order: one 8-byte entry per listed position, key (pos | hash << 16) low, fingerprint high
+  uint64_t* SF = j.lzsf + (size_t)t * j.npix_cap;
+  uint32_t* S = (uint32_t*)SF;                                    // the keys at even words
+  uint32_t* T = j.lzs + (size_t)t * j.npix_cap;                   // after the first pass
   uint16_t* R = j.lzrank + (size_t)t * j.npix_cap;
   uint16_t* E = j.lzend + (size_t)t * j.npix_cap;
   const uint32_t hm = j.lzs_hmask;
@@ -1219,7 +1220,8 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
   for (int pass = 0; pass < 2; pass++) {
     const uint32_t sh = 16 + 8 * pass;
     const uint32_t* in = pass ? T : nullptr;
-    uint32_t* out = pass ? S : T;
+    uint32_t* out = pass ? S : T;                                 // S: stride 2 (the entry's low word)
+    const uint32_t os = pass ? 2u : 1u;
     auto key_at = [&](uint32_t i) -> uint32_t {
       return i >= hi ? 0u : pass ? in[i] : (i | (lzs_hash(F[i], hm) << 16));
     };
@@ -1290,7 +1292,7 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
       const uint32_t o = valid ? cnt[wv][d] + (uint32_t)__popcll(lp & lt) : 0u;
       if (listed && __popcll(lp & lt) == 0) cnt[wv][d] = o + (uint32_t)__popcll(lp);   // the group's first
       if (listed) {
-        out[o] = key;
+        out[os * o] = key;
         if (pass) R[pos] = (uint16_t)o;
       } else if (valid) {
         // the last listed position before it in its group: its run's start, or a hash-colliding
@@ -1300,13 +1302,13 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
     }
   }
   __syncthreads();
-  // the fingerprints in sorted order, over the ping-pong half (free now): k_lzscan's hit test reads
-  // them coalesced beside the positions instead of gathering F[p] after them; E = the last
-  // position of a listed run start's run (the position itself for every other listed position)
+  // the fingerprints beside the keys (k_lzscan's hit test and k_lzscreen's walk read both with one
+  // 8-byte load instead of gathering F[p] after the key); E = the last position of a listed run
+  // start's run (the position itself for every other listed position)
   const uint32_t nl = s_nl;
   for (uint32_t i = tid; i < nl; i += LZSORT_T) {
-    const uint32_t p = S[i] & 0xffffu;
-    T[i] = F[p];
+    const uint32_t key = S[2 * i], p = key & 0xffffu;
+    SF[i] = (uint64_t)F[p] << 32 | key;
     uint32_t e = p;
     if (R8[p] >= 4) {
       while (R8[e] == 255) e += 254;                            // R8 saturates: e + 254 is in the run
@@ -1343,8 +1345,7 @@ __global__ __launch_bounds__(256) void k_lzscreen(EncodeJob j, int limit) {
   const uint32_t* F = j.fpb + o;
   const uint32_t* TP = j.tpx + o;
   const uint8_t* R8 = j.run8 + o;
-  const uint32_t* PS = j.lzs + o;
-  const uint32_t* PF = j.lzs + (size_t)j.ntiles * j.npix_cap + o;
+  const uint64_t* PSF = j.lzsf + o;                                   // key | fingerprint << 32
   const uint16_t* PR = j.lzrank + o;
   const uint16_t* PE = j.lzend + o;
   uint64_t* cand = j.candbits + (size_t)t * (j.npix_cap / 64);
@@ -1361,12 +1362,13 @@ __global__ __launch_bounds__(256) void k_lzscreen(EncodeJob j, int limit) {
       } else {
         const uint32_t hq = lzs_hash(f, j.lzs_hmask);
         for (int32_t i = (int32_t)PR[q] - 1; i >= 0; i--) {
-          const uint32_t e = PS[i], p = e & 0xffffu;
+          const uint64_t v = PSF[i];
+          const uint32_t e = (uint32_t)v, p = e & 0xffffu;
           if ((e >> 16) != hq) break;                                  // q's group starts after i
           const uint32_t en = flat ? (uint32_t)PE[i] : p;
           const bool run = flat && en > p, own = run && en >= q;
           if (!own && q - (run ? en - 3u : p) > bm) break;             // older than the window
-          if (!own && PF[i] == f) { c = true; break; }
+          if (!own && (uint32_t)(v >> 32) == f) { c = true; break; }
         }
       }
     }
@@ -1414,10 +1416,9 @@ void k_lzscan(EncodeJob j, int limit, int rp, int nseg_req, int hls) {
   }
   const uint32_t thr = 4 + bonus;
   const bool post = j.lzs != nullptr;                                  // posting lists (k_lzsort)
-  const uint32_t* PS = post ? j.lzs + (size_t)t * j.npix_cap : nullptr;
+  const uint64_t* PSF = post ? j.lzsf + (size_t)t * j.npix_cap : nullptr;   // key | fingerprint << 32
   const uint16_t* PR = post ? j.lzrank + (size_t)t * j.npix_cap : nullptr;
   const uint16_t* PE = post ? j.lzend + (size_t)t * j.npix_cap : nullptr;
-  const uint32_t* PF = post ? j.lzs + (size_t)j.ntiles * j.npix_cap + (size_t)t * j.npix_cap : nullptr;
   const bool lds_bits = nwords <= LZS_BITS;
   const uint32_t nseg = (lds_bits && rp && nwords >= 4 * LZS_SEG && nseg_req > 1) ? (uint32_t)nseg_req : 1u;
   const uint32_t segcap = j.lz_cap / LZS_SEG;
@@ -1599,12 +1600,12 @@ void k_lzscan(EncodeJob j, int limit, int rp, int nseg_req, int hls) {
       // the next batch's entries are loaded before this batch's hits are measured (prefetch)
       int32_t i0 = (int32_t)PR[q] - 1;
       uint32_t e_n = 0u, fe_n = ~f, en_n = 0u;
-      if (i0 - lane >= 0) { e_n = PS[i0 - lane]; fe_n = PF[i0 - lane]; if (flat) en_n = PE[i0 - lane]; }
+      if (i0 - lane >= 0) { const uint64_t v = PSF[i0 - lane]; e_n = (uint32_t)v; fe_n = (uint32_t)(v >> 32); if (flat) en_n = PE[i0 - lane]; }
       for (; i0 >= 0 && !done; i0 -= 64) {
         const int32_t i = i0 - lane;
         const uint32_t e = e_n, fe = fe_n, en = en_n;
         e_n = 0u; fe_n = ~f;
-        if (i >= 64) { e_n = PS[i - 64]; fe_n = PF[i - 64]; if (flat) en_n = PE[i - 64]; }
+        if (i >= 64) { const uint64_t v = PSF[i - 64]; e_n = (uint32_t)v; fe_n = (uint32_t)(v >> 32); if (flat) en_n = PE[i - 64]; }
         const uint32_t p = e & 0xffffu;
         const bool run = flat && en > p;                               // a flat run's start
         // q's own run: PR[q] counts the listed positions before q in its group, which are its own
