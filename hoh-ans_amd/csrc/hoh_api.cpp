@@ -249,7 +249,7 @@ extern "C" int hoh_debug_read(hoh_ctx* c, int which, void* dst, size_t bytes) {
     return hipMemcpy(dst, (const uint8_t*)c->dec.bufs[15] + c->dec.sizes[15] - bytes, bytes, hipMemcpyDeviceToHost) == hipSuccess
                ? HOH_OK : HOH_E_HIP;
   }
-  // 3: k_lzsort's posting lists of the last -s1..-s4 encode (per entry key | fingerprint << 32, first-pass keys,
+  // 3: k_lzsort's posting lists of the last -s1..-s4 encode (per entry key | fingerprint << 32, first-pass entries,
   // u16 ranks: tools/scripts/lzsort_check.py); 4: the fingerprints + tile pixel words (k_lzfp)
   // 5: the per-tile kernel counters of the last encode (EncodeJob::dbg, [tile][64] u32)
   const Buf& b = which == 0 ? c->matches : which == 3 ? c->lzs : which == 4 ? c->fpb : which == 5 ? c->dbg : c->lzspec;
@@ -418,11 +418,11 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
     // posting lists for the LZ windows (-s1..-s4) of tiles whose positions fit 16 bits
     if (speed >= 1 && j.npix_cap <= 65536 && lz_posting()) {
       const size_t per = (size_t)ntiles * j.npix_cap;
-      // [entries: 8 B][first-pass keys: 4 B][ranks: 2 B][run ends: 2 B] per position
-      if ((e = ensure(c->lzs, per * 16))) return e;
+      // [entries: 8 B][first-pass entries: 8 B][ranks: 2 B][run ends: 2 B] per position
+      if ((e = ensure(c->lzs, per * 20))) return e;
       j.lzsf = (uint64_t*)c->lzs.p;
       j.lzs = (uint32_t*)(j.lzsf + per);
-      j.lzrank = (uint16_t*)(j.lzs + per);
+      j.lzrank = (uint16_t*)(j.lzsf + 2 * per);
       j.lzend = j.lzrank + per;
       j.lzs_hmask = (uint32_t)HOH_KNOB(LZS_HMASK, 0xffff);
       j.cus = c->cus;

@@ -193,7 +193,7 @@ struct EncodeJob {
   uint32_t* fpt;          // -s>=1: [tile][npix_cap] the fingerprints transposed, FT[x * h + y] (k_lzfp)
   uint8_t* run8;          // -s>=1: [tile][npix_cap] length of the run of equal pixels from each position
                           //   (tile raster order, 1..254 exact, 255 = at least 255)
-  uint32_t* lzs;          // -s>=1, tiles <= 65536 px: [tile][npix_cap] k_lzsort's first-pass keys; null: no
+  uint32_t* lzs;          // -s>=1, tiles <= 65536 px: [tile][npix_cap] k_lzsort's first-pass entries (u64); null: no
                           //   posting lists.  The lists themselves are lzsf: positions grouped by
                           //   hash16(fingerprint), ascending inside a group
   uint16_t* lzrank;       //   [tile][npix_cap] index of each position in lzsf (flat run-inner positions: their run start's)

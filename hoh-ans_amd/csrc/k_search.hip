@@ -1200,8 +1200,7 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
   const uint8_t* R8 = j.run8 + (size_t)t * j.npix_cap;
   // final order: one 8-byte entry per listed position, key (pos | hash << 16) low, fingerprint high
   uint64_t* SF = j.lzsf + (size_t)t * j.npix_cap;
-  uint32_t* S = (uint32_t*)SF;                                    // the keys at even words
-  uint32_t* T = j.lzs + (size_t)t * j.npix_cap;                   // after the first pass
+  uint64_t* T = (uint64_t*)j.lzs + (size_t)t * j.npix_cap;       // after the first pass
   uint16_t* R = j.lzrank + (size_t)t * j.npix_cap;
   uint16_t* E = j.lzend + (size_t)t * j.npix_cap;
   const uint32_t hm = j.lzs_hmask;
@@ -1219,11 +1218,14 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
   const uint32_t lo = min(n, (uint32_t)wv * quarter), hi = min(n, lo + quarter);
   for (int pass = 0; pass < 2; pass++) {
     const uint32_t sh = 16 + 8 * pass;
-    const uint32_t* in = pass ? T : nullptr;
-    uint32_t* out = pass ? S : T;                                 // S: stride 2 (the entry's low word)
-    const uint32_t os = pass ? 2u : 1u;
-    auto key_at = [&](uint32_t i) -> uint32_t {
-      return i >= hi ? 0u : pass ? in[i] : (i | (lzs_hash(F[i], hm) << 16));
+    // entries travel as key | fingerprint << 32 (the fingerprint read once, coalesced, here)
+    const uint64_t* in = pass ? T : nullptr;
+    uint64_t* out = pass ? SF : T;
+    auto key_at = [&](uint32_t i) -> uint64_t {
+      if (i >= hi) return 0u;
+      if (pass) return in[i];
+      const uint32_t f = F[i];
+      return (uint64_t)f << 32 | (i | (lzs_hash(f, hm) << 16));
     };
     // the second pass lists the counted positions only; an unlisted one takes no slot
     auto listed_of = [&](uint32_t i, uint32_t key) -> bool {
@@ -1244,9 +1246,9 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
     for (int k = 0; k < 4; k++) cnt[wv][lane + 64 * k] = 0;        // each wave its own row
     __syncthreads();                                               // inner / the previous pass done
     // 1. this wave's listed count per digit
-    uint32_t kn = key_at(lo + lane);
+    uint64_t kn = key_at(lo + lane);
     for (uint32_t i0 = lo; i0 < hi; i0 += 64) {
-      const uint32_t i = i0 + lane, key = kn;
+      const uint32_t i = i0 + lane, key = (uint32_t)kn;
       kn = key_at(i + 64);
       const bool listed = listed_of(i, key);
       const uint32_t d = (key >> sh) & 255;
@@ -1284,7 +1286,8 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
     // 3. scatter in order: rank = the wave's running base of the digit + listed peers before
     kn = key_at(lo + lane);
     for (uint32_t i0 = lo; i0 < hi; i0 += 64) {
-      const uint32_t i = i0 + lane, key = kn;
+      const uint64_t ent = kn;
+      const uint32_t i = i0 + lane, key = (uint32_t)ent;
       kn = key_at(i + 64);
       const bool valid = i < hi, listed = listed_of(i, key);
       const uint32_t d = (key >> sh) & 255, pos = key & 0xffffu;
@@ -1292,7 +1295,7 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
       const uint32_t o = valid ? cnt[wv][d] + (uint32_t)__popcll(lp & lt) : 0u;
       if (listed && __popcll(lp & lt) == 0) cnt[wv][d] = o + (uint32_t)__popcll(lp);   // the group's first
       if (listed) {
-        out[os * o] = key;
+        out[o] = ent;
         if (pass) R[pos] = (uint16_t)o;
       } else if (valid) {
         // the last listed position before it in its group: its run's start, or a hash-colliding
@@ -1302,13 +1305,12 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
     }
   }
   __syncthreads();
-  // the fingerprints beside the keys (k_lzscan's hit test and k_lzscreen's walk read both with one
-  // 8-byte load instead of gathering F[p] after the key); E = the last position of a listed run
-  // start's run (the position itself for every other listed position)
+  // E = the last position of a listed run start's run (the position itself for every other
+  // listed position).  (The fingerprints came through the sort beside the keys: k_lzscan's hit test
+  // and k_lzscreen's walk read both with one 8-byte load.)
   const uint32_t nl = s_nl;
   for (uint32_t i = tid; i < nl; i += LZSORT_T) {
-    const uint32_t key = S[2 * i], p = key & 0xffffu;
-    SF[i] = (uint64_t)F[p] << 32 | key;
+    const uint32_t p = (uint32_t)SF[i] & 0xffffu;
     uint32_t e = p;
     if (R8[p] >= 4) {
       while (R8[e] == 255) e += 254;                            // R8 saturates: e + 254 is in the run

@@ -28,7 +28,7 @@ L = hoh_ans.lib()
 L.hoh_debug_read.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]
 c = hoh_ans.Context(0)
 rgb = hoh_ans.natural_rgb_dev(W, W, 1, ctx=c)
-lzs = np.zeros(per * 4, np.uint32)               # entries (key, fingerprint: u32 pairs), first-pass keys (u32), rank, end (u16 each)
+lzs = np.zeros(per * 5, np.uint32)               # entries, first-pass entries (key, fingerprint: u32 pairs), rank, end (u16 each)
 fpb = np.zeros(per * 13 // 4, np.uint32)         # F, pixels, transposed F (u32 each), run8 (u8)
 bad_total = 0
 ar = np.arange(cap, dtype=np.int64)[None, :]
@@ -43,8 +43,8 @@ for r in range(reps):
     R8 = fpb[3 * per:].view(np.uint8)[:per].reshape(ntiles, cap)
     S = lzs[:2 * per:2].reshape(ntiles, cap)
     T = lzs[1:2 * per:2].reshape(ntiles, cap)                                 # the sorted fingerprints
-    R = lzs[3 * per:].view(np.uint16)[:per].reshape(ntiles, cap)
-    E = lzs[3 * per:].view(np.uint16)[per:2 * per].reshape(ntiles, cap)
+    R = lzs[4 * per:].view(np.uint16)[:per].reshape(ntiles, cap)
+    E = lzs[4 * per:].view(np.uint16)[per:2 * per].reshape(ntiles, cap)
     start = np.ones_like(TP, dtype=bool)
     start[:, 1:] = TP[:, 1:] != TP[:, :-1]
     inner = (R8 >= 4) & ~start
