@@ -1180,7 +1180,7 @@ __device__ __forceinline__ uint32_t lzs_hash(uint32_t f, uint32_t hm) { return (
 #ifndef LZSORT_T
 #define LZSORT_T 1024         // threads per tile (one wave per contiguous share of the positions)
 #endif
-__global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
+__global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j, int limit) {
   // Stable LSD counting sort by the 16-bit hash, two 8-bit passes.  Each wave owns a contiguous
   // quarter of the pass's input and ranks it alone (64 at a time: ballot peers per digit, a
   // wave-private running base per digit), so a pass has two barriers, not three per 256
@@ -1188,7 +1188,8 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
   // while the current 64 are ranked.
   __shared__ uint32_t cnt[LZSORT_T / 64][256];                   // per wave: digit counts, then bases
   __shared__ uint32_t inner[65536 / 32];                         // flat positions inside a run (unlisted)
-  __shared__ uint32_t s_nl;
+  __shared__ uint32_t cbit[65536 / 32];                          // the candidate screen (below)
+  __shared__ uint32_t s_nl, s_ncand;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   // tiles strided over the grid (a smaller grid keeps fewer tiles' scatter targets in L2 at once)
   for (int t = blockIdx.x; t < j.ntiles; t += gridDim.x) {
@@ -1208,12 +1209,18 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
   // Flat positions (their window one colour: run8 >= 4) other than a run's first are not listed:
   // k_lzscan measures one representative per run from the run's start (its end in E).  They still
   // pass through the first pass, so that the second gives each the rank of its own run's start.
+  // A flat position inside its run is a candidate at b = 1 (when it has a window: F != 0); the
+  // listed ones are screened after the sort
   for (uint32_t c0 = 0; c0 < n; c0 += LZSORT_T) {
     const uint32_t i = c0 + tid;
     const bool in = i < n && i > 0 && R8[i] >= 4 && ((TP[i - 1] ^ TP[i]) & 0xffffffu) == 0;
-    const uint64_t m = __ballot(in);
-    if (lane == 0) { inner[i >> 5] = (uint32_t)m; inner[(i >> 5) + 1] = (uint32_t)(m >> 32); }
+    const uint64_t m = __ballot(in), mc = __ballot(in && F[i] != 0u);
+    if (lane == 0) {
+      inner[i >> 5] = (uint32_t)m; inner[(i >> 5) + 1] = (uint32_t)(m >> 32);
+      cbit[i >> 5] = (uint32_t)mc; cbit[(i >> 5) + 1] = (uint32_t)(mc >> 32);
+    }
   }
+  if (tid == 0) s_ncand = 0;
   const uint32_t quarter = ((n + LZSORT_T / 64 - 1) / (LZSORT_T / 64) + 63) & ~63u;
   const uint32_t lo = min(n, (uint32_t)wv * quarter), hi = min(n, lo + quarter);
   for (int pass = 0; pass < 2; pass++) {
@@ -1307,7 +1314,7 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
   __syncthreads();
   // E = the last position of a listed run start's run (the position itself for every other
   // listed position).  (The fingerprints came through the sort beside the keys: k_lzscan's hit test
-  // and k_lzscreen's walk read both with one 8-byte load.)
+  // and the screen's walk read both with one 8-byte load.)
   const uint32_t nl = s_nl;
   for (uint32_t i = tid; i < nl; i += LZSORT_T) {
     const uint32_t p = (uint32_t)SF[i] & 0xffffu;
@@ -1318,6 +1325,40 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
     }
     E[i] = (uint16_t)e;
   }
+  __syncthreads();
+  // The candidate screen (-s1..-s4, lz.hpp:37-42 at the seek window): a listed q is a horizontal
+  // candidate iff an equal fingerprint starts at some b <= min(limit, q) -- walking back from q's
+  // own entry over its hash group (the entries just before it here, read coalesced), a flat run
+  // start seeing its colour's earlier runs in the window when the run's last listed position
+  // (E - 3) is, stepping over its own run's start and hash collisions
+  for (uint32_t iq = tid; iq < nl; iq += LZSORT_T) {
+    const uint64_t vq = SF[iq];
+    const uint32_t kq = (uint32_t)vq, q = kq & 0xffffu, f = (uint32_t)(vq >> 32);
+    if (!f || q == 0) continue;
+    const uint32_t bm = min(q, (uint32_t)limit), hq = kq >> 16;
+    const bool flat = R8[q] >= 4;
+    for (int32_t i = (int32_t)iq - 1; i >= 0; i--) {
+      const uint64_t v = SF[i];
+      const uint32_t e = (uint32_t)v, p = e & 0xffffu;
+      if ((e >> 16) != hq) break;                                  // q's group starts after i
+      const uint32_t en = flat ? (uint32_t)E[i] : p;
+      const bool run = flat && en > p, own = run && en >= q;
+      if (!own && q - (run ? en - 3u : p) > bm) break;             // older than the window
+      if (!own && (uint32_t)(v >> 32) == f) { atomicOr(&cbit[q >> 5], 1u << (q & 31)); break; }
+    }
+  }
+  __syncthreads();
+  // every candidate word of the tile (k_lzvert then adds the vertical ones)
+  uint64_t* cand = j.candbits + (size_t)t * (j.npix_cap / 64);
+  uint32_t nc = 0;
+  for (uint32_t w = tid; w < (n + 63) / 64; w += LZSORT_T) {
+    const uint64_t word = (uint64_t)cbit[2 * w] | (uint64_t)cbit[2 * w + 1] << 32;
+    cand[w] = word;
+    nc += (uint32_t)__popcll(word);
+  }
+  if (nc) atomicAdd(&s_ncand, nc);
+  __syncthreads();
+  if (tid == 0 && s_ncand) atomicAdd(&j.tiles[t].ncand, s_ncand);
   }
 }
 
@@ -1331,54 +1372,6 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j) {
 // greedy scan (lz.hpp:32-95) over the candidates + the four LZ streams.
 // Per candidate one batch of global loads (its fingerprint, 16 chunks of 64 horizontal back
 // distances and the vertical ones) and then LDS only: the candidate bitmap is staged in LDS and
-// The candidate screen from the posting lists (tiles that have them, -s1..-s4): q is a horizontal
-// candidate iff an equal fingerprint starts at some b <= min(limit, q) -- the first fingerprint-
-// equal entry of q's group walked back from PR[q] (k_lzscan's walk, stopped at its first hit): a
-// flat q inside its run has b = 1; a flat run start finds its colour's earlier run starts, in
-// the window when the run's last listed position (E - 3) is; a hash collision steps on.  A thread
-// per position, every candidate word written (k_lzvert then adds the vertical ones).  It replaces
-// k_lzcand's hash tables / global map for these tiles.
-#define LZSCREEN_G 16         // workgroups per tile
-__global__ __launch_bounds__(256) void k_lzscreen(EncodeJob j, int limit) {
-  const int t = blockIdx.y, bx = blockIdx.x, lane = threadIdx.x & 63;
-  const TileInfo ti = j.tiles[t];
-  const uint32_t npix = (uint32_t)ti.w * ti.h;
-  const size_t o = (size_t)t * j.npix_cap;
-  const uint32_t* F = j.fpb + o;
-  const uint32_t* TP = j.tpx + o;
-  const uint8_t* R8 = j.run8 + o;
-  const uint64_t* PSF = j.lzsf + o;                                   // key | fingerprint << 32
-  const uint16_t* PR = j.lzrank + o;
-  const uint16_t* PE = j.lzend + o;
-  uint64_t* cand = j.candbits + (size_t)t * (j.npix_cap / 64);
-  uint32_t ncand = 0;
-  for (uint32_t q0 = bx * 256u; q0 < npix; q0 += LZSCREEN_G * 256u) {
-    const uint32_t q = q0 + threadIdx.x;
-    bool c = false;
-    const uint32_t f = q < npix ? F[q] : 0u;
-    if (f && q > 0) {
-      const uint32_t bm = min(q, (uint32_t)limit), pq = TP[q] & 0xffffffu;
-      const bool flat = R8[q] >= 4;
-      if (flat && (TP[q - 1] & 0xffffffu) == pq) {
-        c = true;                                                      // b = 1 inside its run
-      } else {
-        const uint32_t hq = lzs_hash(f, j.lzs_hmask);
-        for (int32_t i = (int32_t)PR[q] - 1; i >= 0; i--) {
-          const uint64_t v = PSF[i];
-          const uint32_t e = (uint32_t)v, p = e & 0xffffu;
-          if ((e >> 16) != hq) break;                                  // q's group starts after i
-          const uint32_t en = flat ? (uint32_t)PE[i] : p;
-          const bool run = flat && en > p, own = run && en >= q;
-          if (!own && q - (run ? en - 3u : p) > bm) break;             // older than the window
-          if (!own && (uint32_t)(v >> 32) == f) { c = true; break; }
-        }
-      }
-    }
-    const uint64_t word = __ballot(c);
-    if (lane == 0 && q < npix) { cand[q >> 6] = word; ncand += (uint32_t)__popcll(word); }
-  }
-  if (lane == 0 && ncand) atomicAdd(&j.tiles[t].ncand, ncand);
-}
 
 // the run lengths compare pixels from an LDS ring of the positions [q - limit, q + 260) (filled
 // 64 positions at a time as the scan moves: each pixel read once per tile), sixteen positions per
@@ -2170,15 +2163,14 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, v
     const int mode = limit <= 1024 ? LZC_TAB : (size_t)mw * 4 + LZC_MAP_OFF <= TAB_TILE_BYTES ? LZC_MAP : LZC_WALK;
     const int lring = mode == LZC_MAP ? 2 * NT : ring;
     const size_t lds = (size_t)(lring + (mode == LZC_TAB ? 3 * LZC_W : 0) + (mode != LZC_WALK ? 2 * LZC_C : 0)) * 4;
-    if (j.lzs) {                      // posting lists: the screen is their first hit (k_lzscreen)
+    if (j.lzs) {                      // posting lists: the screen is their first hit (k_lzsort's last loop)
       // one 1024-thread workgroup per CU striding over the tiles: against a workgroup per tile
       // (1024 in flight) the scatter targets of 4x fewer tiles share the L2s, the launch leaves
       // most of each CU to the predictor search beside it, and the natural 8192^2 encodes drop
       // by 1.4-1.7 ms at -s1..-s4 (k_lzsort 5.2 -> 3.7 ms at -s1; tools/scripts/r5_ab_lzsort.sh)
       const int sgk = HOH_KNOB(LZSORT_GRID, 0);                      // 0: the CU count
       const int sg = sgk > 0 ? sgk : j.cus > 0 ? j.cus : 256;
-      hipLaunchKernelGGL(k_lzsort, dim3(sg > 0 && sg < j.ntiles ? sg : j.ntiles), dim3(LZSORT_T), 0, sl, j);
-      hipLaunchKernelGGL(k_lzscreen, dim3(LZSCREEN_G, j.ntiles), dim3(256), 0, sl, j, limit);
+      hipLaunchKernelGGL(k_lzsort, dim3(sg > 0 && sg < j.ntiles ? sg : j.ntiles), dim3(LZSORT_T), 0, sl, j, limit);
     } else {
       hipLaunchKernelGGL(k_lzcand, dim3(j.ntiles), dim3(NT), lds, sl, j, limit, lring, mode, mw, HOH_KNOB(LZC_NOWALK, 0));
     }
