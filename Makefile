@@ -15,7 +15,26 @@ HDRS := $(wildcard $(CSRC)/*.h) include/hoh_ans.h
 
 BINDIR := hoh-ans_amd/bin
 
-all: $(LIBDIR)/libhohgpu.so oracle/liboracle.so $(BINDIR)/choh $(BINDIR)/dhoh $(BINDIR)/dropin_test
+all: $(LIBDIR)/libhohgpu.so $(LIBDIR)/libhohgpu_check.so oracle/liboracle.so $(BINDIR)/choh $(BINDIR)/dhoh $(BINDIR)/dropin_test
+
+# Checking build (test infrastructure, never the product): the same sources with hoh_debug_read
+# (workspace read-back) and the measurement knobs, so -m gpu tests can recompute the -s>=1 posting
+# lists exactly (tests/test_gpu_lzsort_exact.py) and run the prob_bits ladder unpruned.  Kernels
+# touched by the flags only gain counters; k_lzsort / k_lzfp compile identically.
+CHECKFLAGS := -DHOH_DEBUG_READ -DHOH_KNOBS
+CHECK_OBJS := $(patsubst $(CSRC)/%,build/check/%.o,$(SRCS))
+
+build/check/%.hip.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p build/check
+	$(HIPCC) $(HIPFLAGS) $(CHECKFLAGS) -c -o $@ $<
+
+build/check/%.cpp.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p build/check
+	$(HIPCC) $(HIPFLAGS) $(CHECKFLAGS) -c -o $@ $<
+
+$(LIBDIR)/libhohgpu_check.so: $(CHECK_OBJS)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(CHECK_OBJS) -ldl -lpthread
 
 build/%.hip.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p build

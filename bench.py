@@ -11,18 +11,20 @@ One step = one pass of the hot path over one batch of the workload, inputs resid
          (hoh_encode_images_async: every kernel covers the B images' tiles; it also records the
          decode side index), then dhoh of the B files back into HBM (hoh_decode_images_async).
          --batch 1: one image per step through hoh_encode_image_async / hoh_decode_image_async.
-  N > 1: weak scaling (default) -- the image is 8192 x (8192*N) and rank r owns a band of tile
-         rows (8192^2 pixels per GPU).  --strong: configs[3], one 16384x16384 image sharded over
-         the N GPUs.  A step is: encode the shard's tiles (hoh_encode_tiles_async), gather every
-         shard to rank 0 over RCCL (all-gather of the tile sizes, point-to-point blobs straight
-         into rank 0's file behind the header + tile table: byte-identical to a 1-GPU encode),
-         and decode the shard (hoh_decode_tiles_async, tile sizes read on the device).
+  N > 1: weak scaling (default) -- the images are 8192 x (8192*N) and rank r owns a band of tile
+         rows (8192^2 pixels per GPU per image).  --strong: configs[3], 16384x16384 images sharded
+         over the N GPUs.  A step is: encode the shard of B images (hoh_encode_tiles_images_async:
+         every kernel covers the B bands' tiles), gather every shard to rank 0 over RCCL (one
+         all-gather of the B images' tile sizes, point-to-point blobs straight into rank 0's B
+         files behind their header + tile table: byte-identical to a 1-GPU encode), and decode the
+         B bands (hoh_decode_tiles_images_async, tile sizes read on the device).
 value = raw RGB bytes of the step's images x K / max-over-ranks(time of the K steps) / 1e6.
 
 Slots in flight (--inflight): at N = 1 D = 4 slots of B = 8 images (32 images in flight), each
 slot with its own library context (HIP stream, workspaces) and its OWN input images (seeds 1..32,
 so no image is a cache hit of another's), at HIP's default of 4 hardware queues (nothing set); the
-N > 1 path and --batch 1 keep 20 single-image slots on up to 20 queues.  One host thread per rank
+N > 1 path runs the same 4 slots x 8 images per GPU; --batch 1 keeps 20 single-image slots on up to
+20 queues.  One host thread per rank
 deals the steps round-robin to the slots through enqueue-only calls; at N > 1 the gathers are
 issued in step order on one process group (hoh_ans.dist.run_pipeline).  A set-up pass of one
 step per slot (workspaces sized outside the timed region), then W warmup steps, then K timed.
@@ -608,49 +610,57 @@ def speed_legs(args, slots, nat, W, H, D, B, stride, status, torch, hoh_ans, hd)
 
 class GpuShardOps:
     """Device side of hoh_ans.dist.run_sharded_leg for bench.py's N > 1 path: rank `rank` owns the
-    tile-row band of a W x H image; a step encodes the band (hoh_encode_tiles_async: tile sizes and
-    status stay on the device), copies the tile sizes to pinned host memory behind an event, and
-    when the step finishes all-gathers the sizes, sends the blob to rank 0 (straight into its
-    place in the file behind hoh_file_prefix) and decodes the band (hoh_decode_tiles_async, tile
-    sizes read on the device) on the slot's stream."""
+    tile-row band [t0, t0+nt) of every W x H image.  A slot holds the bands of B images; a step
+    encodes them in one batched call (hoh_encode_tiles_images_async: every kernel covers the B
+    bands' tiles, tile sizes and statuses stay on the device), copies the tile sizes to pinned host
+    memory behind an event and, when the step finishes, all-gathers the B images' sizes once, sends
+    the B blobs to rank 0 (each straight into its place in its file behind hoh_file_prefix) and
+    decodes the B bands (hoh_decode_tiles_images_async, tile sizes read on the device) on the slot's
+    stream.  The same D slots x B images schedule as the N = 1 line, at HIP's default queues."""
 
-    def __init__(self, args, W, H, seed0, rank, world, dev, torch, hoh_ans, hd, nrows):
-        self.args, self.W, self.H, self.seed0 = args, W, H, seed0
+    def __init__(self, args, W, H, seed0, rank, world, dev, torch, hoh_ans, hd, nrows, B):
+        self.args, self.W, self.H, self.seed0, self.B = args, W, H, seed0, B
         self.torch, self.hoh_ans, self.hd, self.dev = torch, hoh_ans, hd, dev
         self.device = dev
         self.t0, self.nt, self.y0, y1 = hd.shard(W, H, rank, world)
         self.rows = y1 - self.y0
+        self.band = W * self.rows * 3
         self.L = hoh_ans.lib()
-        self.status = torch.zeros((nrows, 4), dtype=torch.int64, device=dev)
+        self.stride = self.L.hoh_encode_bound(W, self.rows)
+        self.status = torch.zeros((nrows, 4 * B), dtype=torch.int64, device=dev)
 
     def new_slot(self, k):
-        torch, hoh_ans = self.torch, self.hoh_ans
+        torch, hoh_ans, B = self.torch, self.hoh_ans, self.B
 
         class Slot:
             pass
         s = Slot()
-        s.seed = self.seed0 + k
+        s.seeds = [self.seed0 + k * B + b for b in range(B)]
+        s.seed = s.seeds[0]
         s.ctx = hoh_ans.Context(self.dev.index)
         s.stream = torch.cuda.Stream(device=self.dev)
-        s.rgb = hoh_ans.synth_rgb_dev(self.W, self.rows, s.seed, self.args.noise, ctx=s.ctx, row0=self.y0)
+        s.rgb = torch.empty(B * self.band, dtype=torch.uint8, device=self.dev)
+        for b, sd in enumerate(s.seeds):
+            s.rgb[b * self.band:(b + 1) * self.band] = hoh_ans.synth_rgb_dev(self.W, self.rows, sd, self.args.noise,
+                                                                           ctx=s.ctx, row0=self.y0)
         s.index = None if self.args.no_index else hoh_ans.Index()
-        s.out = torch.empty(self.L.hoh_encode_bound(self.W, self.rows), dtype=torch.uint8, device=self.dev)
-        s.dec = torch.empty(self.W * self.rows * 3, dtype=torch.uint8, device=self.dev)
+        s.out = torch.empty(B * self.stride, dtype=torch.uint8, device=self.dev)
+        s.dec = torch.empty(B * self.band, dtype=torch.uint8, device=self.dev)
         s.events = []
-        s.sizes = torch.empty(self.nt, dtype=torch.int32, device=self.dev)
-        s.sizes_host = torch.empty(self.nt, dtype=torch.int32).pin_memory()
+        s.sizes = torch.empty(B * self.nt, dtype=torch.int32, device=self.dev)
+        s.sizes_host = torch.empty(B * self.nt, dtype=torch.int32).pin_memory()
         s.enc_done = torch.cuda.Event()
-        s.gather = self.hd.FileGather(self.W, self.H, self.dev)
+        s.gather = self.hd.BatchGather(self.W, self.H, B, self.dev)
         s.ctx.profiling(True)
         return s
 
     def enqueue(self, s, i):
-        torch = self.torch
+        torch, B = self.torch, self.B
         with torch.cuda.stream(s.stream):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            self.hoh_ans.encode_tiles_async(s.rgb, self.W, self.H, self.t0, self.nt, s.out, s.sizes,
-                                            self.status[i, 0:2], ctx=s.ctx, index=s.index, row0=self.y0)
+            self.hoh_ans.encode_tiles_images_async(s.rgb, B, self.W, self.H, self.t0, self.nt, s.out, self.stride,
+                                                   s.sizes, self.status[i, 0:2 * B], ctx=s.ctx, index=s.index)
             e1.record()
             s.sizes_host.copy_(s.sizes, non_blocking=True)
             s.enc_done.record()
@@ -658,29 +668,31 @@ class GpuShardOps:
 
     def finish(self, s, i):
         import numpy as np
-        torch = self.torch
+        torch, B = self.torch, self.B
         s.enc_done.synchronize()
-        ts = s.sizes_host.numpy().astype(np.uint32)
+        ts = s.sizes_host.numpy().astype(np.uint32).reshape(B, self.nt)
         with torch.cuda.stream(s.stream):
-            res = s.gather(s.out, int(ts.sum(dtype=np.int64)), ts, wait=False)
+            res = s.gather(s.out, self.stride, ts, wait=False)
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record()
-            self.hoh_ans.decode_tiles_async(s.out, s.out.numel(), self.W, self.H, self.t0, self.nt, s.sizes, s.dec,
-                                            self.status[i, 2:4], ctx=s.ctx, index=s.index, row0=self.y0)
+            self.hoh_ans.decode_tiles_images_async(s.out, B, self.stride, self.W, self.H, self.t0, self.nt, s.sizes,
+                                                   s.dec, self.status[i, 2 * B:4 * B], ctx=s.ctx, index=s.index)
             e2 = torch.cuda.Event(enable_timing=True)
             e2.record()
             s.events[-1] = s.events[-1] + (e1, e2)
             for q in res[2]:
-                q.wait()              # RCCL: the slot's stream (not the host) waits before reusing the blob
+                q.wait()              # RCCL: the slot's stream (not the host) waits before reusing the blobs
 
     def drain(self):
         self.torch.cuda.synchronize()
 
     def check(self, total):
         st = self.status[:total].cpu().numpy()
+        B = self.B
         for i in range(total):
-            self.hoh_ans.check_status(st[i, 0:2], "encode (step %d)" % i)
-            self.hoh_ans.check_status(st[i, 2:4], "decode (step %d)" % i)
+            for b in range(B):
+                self.hoh_ans.check_status(st[i, 2 * b:2 * b + 2], "encode (step %d image %d)" % (i, b))
+                self.hoh_ans.check_status(st[i, 2 * B + 2 * b:2 * B + 2 * b + 2], "decode (step %d image %d)" % (i, b))
 
     def reset(self, slots):
         for s in slots:
@@ -691,12 +703,36 @@ class GpuShardOps:
         return bool(self.torch.equal(s.dec, s.rgb))
 
 
-def sharded_leg(args, W, H, D, K, warm, seed0, rank, world, dev, torch, hoh_ans, hd):
+def shard_one_in_flight(ops, s, torch, hoh_ans, n=5):
+    """The dominant kernel's launch duration with ONE shard in flight on this rank (the N = 1
+    line's one-in-flight measurement, on the N > 1 path): n host-synchronous shard encodes of
+    slot s's first band (hoh_encode_tiles_async, B = 1) with the library's HIP-event stage timing
+    on the call's stream; the bytes are checked against the batched blob of that band."""
+    out = torch.empty(ops.stride, dtype=torch.uint8, device=ops.dev)
+    sizes = torch.empty(ops.nt, dtype=torch.int32, device=ops.dev)
+    st = torch.zeros(2, dtype=torch.int64, device=ops.dev)
+    rgb0 = s.rgb[:ops.band]
+    with torch.cuda.stream(s.stream):
+        s.ctx.profiling(True)
+        s.ctx.reset_stats()
+        for _ in range(n):
+            hoh_ans.encode_tiles_async(rgb0, ops.W, ops.H, ops.t0, ops.nt, out, sizes, st, ctx=s.ctx,
+                                       row0=ops.y0)
+            s.stream.synchronize()
+        iso = {k: v[0] / v[1] for k, v in s.ctx.kernel_stats().items() if v[1]}
+        s.ctx.profiling(False)
+    size = hoh_ans.check_status(st.cpu().numpy(), "one-in-flight shard encode")
+    same = bool(torch.equal(out[:size], s.out[:size])) and bool(torch.equal(sizes, s.sizes[:ops.nt]))
+    return iso, same
+
+
+def sharded_leg(args, W, H, D, B, K, warm, seed0, rank, world, dev, torch, hoh_ans, hd, one_in_flight=False):
     """One N > 1 leg (or its one-rank rehearsal, --sharded): returns a dict of its numbers; on
-    rank 0 the gathered file of slot 0 (seed seed0) is hashed."""
+    rank 0 the gathered file of slot 0's first image (seed seed0) is hashed, and every slot's
+    images' files of their last step against the reference choh's SHAs where known."""
     import numpy as np
     import torch.distributed as dist
-    ops = GpuShardOps(args, W, H, seed0, rank, world, dev, torch, hoh_ans, hd, max(K, warm, D))
+    ops = GpuShardOps(args, W, H, seed0, rank, world, dev, torch, hoh_ans, hd, max(K, warm, D), B)
     slots, el, lossless = hd.run_sharded_leg(ops, D, K, warm)
     t_enc = sum(ev[0].elapsed_time(ev[1]) for s in slots for ev in s.events) * 1e-3
     t_dec = sum(ev[-2].elapsed_time(ev[-1]) for s in slots for ev in s.events) * 1e-3
@@ -706,19 +742,26 @@ def sharded_leg(args, W, H, D, K, warm, seed0, rank, world, dev, torch, hoh_ans,
             a0, c0 = stats.get(k, (0.0, 0))
             stats[k] = (a0 + tot, c0 + cnt)
         s.ctx.profiling(False)
-    tt = torch.tensor([t_enc, t_dec], dtype=torch.float64, device=dev)
+    iso, iso_same = (None, None)
+    if one_in_flight:
+        iso, iso_same = shard_one_in_flight(ops, slots[0], torch, hoh_ans)
+    tt = torch.tensor([t_enc, t_dec, iso.get(DOM, 0.0) if iso else 0.0], dtype=torch.float64, device=dev)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    t_enc, t_dec = tt.tolist()
-    n_rank = int(slots[0].sizes_host.numpy().astype(np.int64).sum())
+    t_enc, t_dec, iso_dom = tt.tolist()
+    n_rank = int(slots[0].sizes_host.numpy().astype(np.int64)[:ops.nt].sum())
     nn = torch.tensor([n_rank], dtype=torch.int64, device=dev)
     dist.all_reduce(nn)
-    sha = None
-    if rank == 0:      # slot 0's file of its last step: header + tile table + every rank's blob
-        g = slots[0].gather
-        sha = hashlib.sha256(g.file[:g.total].cpu().numpy().tobytes()).hexdigest()
-    res = {"el": el, "K": K, "D": D, "lossless": lossless, "t_enc": t_enc, "t_dec": t_dec,
-           "comp_total": int(nn.item()), "sha": sha, "stats": stats, "rows": ops.rows,
-           "value": W * H * 3 * K / el / 1e6}
+    sha, shas = None, {}
+    if rank == 0:      # every slot's files of its last step: header + tile table + every rank's blob
+        for s in slots:
+            g = s.gather
+            for b, sd in enumerate(s.seeds):
+                shas[sd] = hashlib.sha256(g.files[b, :g.totals[b]].cpu().numpy().tobytes()).hexdigest()
+        sha = shas[seed0]
+    res = {"el": el, "K": K, "D": D, "B": B, "lossless": lossless, "t_enc": t_enc, "t_dec": t_dec,
+           "comp_total": int(nn.item()), "sha": sha, "shas": shas, "stats": stats, "rows": ops.rows,
+           "iso": iso, "iso_dom_ms_max": iso_dom if iso else None, "iso_same_bytes": iso_same,
+           "value": W * H * 3 * K * B / el / 1e6}
     del slots, ops
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
@@ -821,11 +864,10 @@ def main():
     if args.pmc_probe_speed >= 0:
         pmc_probe_speed(args)
         return
-    sharded0 = int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.sharded
     if args.batch <= 0:
-        args.batch = 1 if sharded0 else DEFAULT_BATCH
+        args.batch = DEFAULT_BATCH
     if args.inflight <= 0:
-        args.inflight = 20 if (sharded0 or args.batch == 1) else DEFAULT_SLOTS
+        args.inflight = 20 if args.batch == 1 else DEFAULT_SLOTS
     D = max(1, args.inflight)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -847,13 +889,13 @@ def main():
                 except Exception as e:      # reported, never invented
                     pmc_speed = {"error": repr(e)[:300]}
 
-    # hardware queues (HIP reads GPU_MAX_HW_QUEUES at runtime init).  The batched N = 1 path runs
-    # at HIP's default (4 queues: nothing is set); the single-image paths (--batch 1, and the N > 1
-    # path) keep one queue per in-flight image up to HW_QUEUE_CAP, past that shared evenly
+    # hardware queues (HIP reads GPU_MAX_HW_QUEUES at runtime init).  The batched paths (N = 1 and
+    # N > 1 alike) run at HIP's default (4 queues: nothing is set); the single-image path (--batch
+    # 1) keeps one queue per in-flight image up to HW_QUEUE_CAP, past that shared evenly
     # (docs/EXPERIMENTS.md, "in-flight sweep": more than ~20 queues per process cost 15-30%)
     if args.hw_queues > 0:
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, args.hw_queues))
-    elif sharded0 or args.batch == 1:
+    elif args.batch == 1:
         os.environ["GPU_MAX_HW_QUEUES"] = str(hw_queues_for(D))
 
     import torch
@@ -863,7 +905,7 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if sharded:
-        sharded_main(args, D, world, rank, dev, torch, hoh_ans, hd)
+        sharded_main(args, D, args.batch, world, rank, dev, torch, hoh_ans, hd)
     elif args.batch > 1 and args.batch_only:
         batch_main(args, D, args.batch, dev, torch, hoh_ans, hd)
     else:
@@ -880,7 +922,9 @@ def roofline_obj(kms, kavg, ratio, rows_raw, raw_total, K, el, pmc, B=1):
     achieved = alg / (kms * 1e-3) / 1e9 if kms else None
     pipeline_gbs = 2 * (1 + ratio) * raw_total * B * K / el / 1e9
     traffic = pmc.get(DOM, {}).get("hbm_bytes") if pmc else None
-    return {"bound": "hbm", "kernel": "k_rans_fast01 (" + DOM + ")",
+    # "bound" names what limits the kernel (its serial coder chain's latency, per "limiter"); the
+    # roofline it is priced against is HBM ("peak_resource"): there is no contraction for MFMA
+    return {"bound": "latency", "peak_resource": "hbm", "kernel": "k_rans_fast01 (" + DOM + ")",
             "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
             "traffic": traffic, "algorithmic_bytes": alg,
@@ -897,13 +941,22 @@ def roofline_obj(kms, kavg, ratio, rows_raw, raw_total, K, el, pmc, B=1):
             "pipeline_bytes_per_image": round(2 * (1 + ratio) * raw_total)}
 
 
-def sharded_main(args, D, world, rank, dev, torch, hoh_ans, hd):
+def strong_batch(W, H, world, B):
+    """Images per slot of the configs[3] leg: about as many pixels per GPU per step as the weak
+    line's B 8192^2 bands (16384^2 over N ranks: 2 images per slot at N = 1, 16 at N = 8)."""
+    rows = H // max(1, world)
+    return max(1, min(16, (B * 8192 * 8192) // (W * max(rows, 1))))
+
+
+def sharded_main(args, D, B, world, rank, dev, torch, hoh_ans, hd):
     """N > 1 (one process per GPU, RCCL), or --sharded at N = 1 (the same code on a one-rank
     group).  The line's value is the primary leg: weak scaling 8192 x (8192 N) by default (each
-    GPU always holds an 8192^2 band), or configs[3] with --strong.  Unless --strong or
-    --no-strong-leg, the same launch also runs configs[3] -- one 16384^2 image (seed 2, the
-    reference choh's golden file) sharded over the N ranks -- into detail.strong_16384_*, with
-    rank 0's gathered file hashed against tests/golden/golden_speed.json."""
+    GPU always holds an 8192^2 band of every image), or configs[3] with --strong.  Each rank runs
+    the N = 1 line's schedule -- D slots, each a batch of B images' bands per step through the
+    batched shard calls, at HIP's default hardware queues.  Unless --strong or --no-strong-leg, the
+    same launch also runs configs[3] -- 16384^2 images sharded over the N ranks, slot 0's first
+    image seed 2 (the reference choh's golden file) -- into detail.strong_16384_*, with rank 0's
+    gathered file hashed against tests/golden/golden_speed.json."""
     import torch.distributed as dist
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     if world == 1:
@@ -919,23 +972,38 @@ def sharded_main(args, D, world, rank, dev, torch, hoh_ans, hd):
     H = args.size if args.strong else args.size * world
     K, warm = args.steps, args.warmup
     seed0 = STRONG_SEED if (args.strong and W == STRONG_SIDE) else args.seed
-    p = sharded_leg(args, W, H, D, K, warm, seed0, rank, world, dev, torch, hoh_ans, hd)
+    Bp = strong_batch(W, H, world, B) if args.strong else B
+    p = sharded_leg(args, W, H, D, Bp, K, warm, seed0, rank, world, dev, torch, hoh_ans, hd, one_in_flight=True)
     strong = None
     if not args.strong and not args.no_strong_leg and STRONG_SIDE // 256 >= world:
         Ds = max(1, min(args.strong_inflight, D))
-        strong = sharded_leg(args, STRONG_SIDE, STRONG_SIDE, Ds, max(1, args.leg_steps), Ds, STRONG_SEED, rank, world,
-                             dev, torch, hoh_ans, hd)
+        Bs = strong_batch(STRONG_SIDE, STRONG_SIDE, world, B)
+        strong = sharded_leg(args, STRONG_SIDE, STRONG_SIDE, Ds, Bs, max(1, args.leg_steps), Ds, STRONG_SEED, rank,
+                             world, dev, torch, hoh_ans, hd)
+    bad = False
     if rank == 0:
         raw_total = W * H * 3
-        ratio = p["comp_total"] / raw_total
         kavg = {k: v[0] / v[1] for k, v in p["stats"].items() if v[1]}
-        roof = roofline_obj(None, kavg, ratio, W * p["rows"] * 3, raw_total, K, p["el"], None)
-        roof["avg_launch_ms_source"] = "not measured at N > 1 (one image in flight is an N = 1 leg)"
+        rows_raw = W * p["rows"] * 3
+        # the one-in-flight launch is the slowest rank's
+        ratio = p["comp_total"] / raw_total
+        roof = roofline_obj(p["iso_dom_ms_max"] or None, kavg, ratio, rows_raw, raw_total, K, p["el"], None, Bp)
+        roof["avg_launch_ms_source"] = ("HIP events on the encoder's stream, one shard (%dx%d band) in flight per "
+                                        "rank, 5 launches, max over ranks" % (W, p["rows"]))
+        roof["algorithmic_bytes_note"] = "(1 + r) x the band's raw bytes per launch (SURVEY 8(d) encode side)"
         gw = golden_speed_sha(W, H, seed0, args.noise) if args.strong else None
         if gw is None:
             gw = golden_sha(W, H, seed0, args.noise)
+        gb = golden_bench_shas(W, H, args.noise) if (W, H) == (8192, 8192) else {}
+        if gw is not None:
+            gb = dict(gb)
+            gb[seed0] = gw
+        checked = {sd: (h == gb[sd]) for sd, h in p["shas"].items() if sd in gb}
         detail = {
-            "inflight": D,
+            "slots": D,
+            "batch": Bp,
+            "inflight": D * Bp,
+            "hw_queues": hw_queue_note(),
             "warmup_requested": args.warmup,
             "latency_ms_enc": round(p["t_enc"] / K * 1e3, 3),
             "latency_ms_dec": round(p["t_dec"] / K * 1e3, 3),
@@ -944,8 +1012,12 @@ def sharded_main(args, D, world, rank, dev, torch, hoh_ans, hd):
             "lossless": p["lossless"],
             "file_sha256": p["sha"],
             "bit_exact_vs_reference": (p["sha"] == gw) if gw else None,
+            "slot_files_bit_exact": "%d of %d" % (sum(checked.values()), len(checked)),
+            "slot_files_checked_seeds": sorted(checked),
+            "one_in_flight_shard_bytes_equal_batched": p["iso_same_bytes"],
             "setup_steps": D,
             "kernel_avg_ms_under_load": {k: round(v, 4) for k, v in kavg.items()},
+            "kernel_avg_ms_one_in_flight_rank0": {k: round(v, 4) for k, v in (p["iso"] or {}).items()},
         }
         if strong is not None:
             g = golden_speed_sha(STRONG_SIDE, STRONG_SIDE, STRONG_SEED, args.noise)
@@ -953,14 +1025,16 @@ def sharded_main(args, D, world, rank, dev, torch, hoh_ans, hd):
                 "strong_16384_MBps": round(strong["value"], 1),
                 "strong_16384_ms_per_step": round(strong["el"] / strong["K"] * 1e3, 4),
                 "strong_16384_steps": strong["K"],
-                "strong_16384_inflight": strong["D"],
+                "strong_16384_slots": strong["D"],
+                "strong_16384_batch": strong["B"],
                 "strong_16384_lossless": strong["lossless"],
                 "strong_16384_file_sha256": strong["sha"],
                 "strong_16384_bit_exact_vs_reference": (strong["sha"] == g) if g else None,
-                "strong_16384_note": "BASELINE configs[3]: one 16384x16384 image (seed %d) sharded over the %d rank(s) "
-                                     "(strong scaling), RCCL gather of the sub-bitstreams to rank 0; sha256 of rank 0's "
-                                     "gathered file against the reference choh's (golden_speed.json)"
-                                     % (STRONG_SEED, world),
+                "strong_16384_note": "BASELINE configs[3]: 16384x16384 images (slot 0's first: seed %d) sharded over "
+                                     "the %d rank(s) (strong scaling), %d slots x %d images per step, RCCL gather of "
+                                     "the sub-bitstreams to rank 0; sha256 of rank 0's gathered file against the "
+                                     "reference choh's (golden_speed.json)"
+                                     % (STRONG_SEED, world, strong["D"], strong["B"]),
             })
         res = {
             "metric": metric_name(),
@@ -976,20 +1050,23 @@ def sharded_main(args, D, world, rank, dev, torch, hoh_ans, hd):
             "dtype": "u8",
             "data": "synthetic",
             "config": {
-                "workload": ("%dx%d synthetic RGB (gradient + triangular noise k=%d, seeds %d..%d: one image per "
-                             "slot), 256x256 tiles, choh -s0 encode + dhoh decode, %s, %d image(s) in flight per GPU"
-                             % (W, H, args.noise, seed0, seed0 + D - 1,
-                                "side index" if not args.no_index else "serial decode", D)),
-                "W": W, "H": H, "tiles": (W // 256) * (H // 256), "per_gpu": "%dx%d" % (W, p["rows"]),
+                "workload": ("%dx%d synthetic RGB (gradient + triangular noise k=%d, seeds %d..%d), 256x256 tiles, "
+                             "choh -s0 encode + dhoh decode, %s, %d slot(s) x a batch of %d images' bands per step "
+                             "(hoh_encode_tiles_images_async / hoh_decode_tiles_images_async) per GPU, %s hardware "
+                             "queues"
+                             % (W, H, args.noise, seed0, seed0 + D * Bp - 1,
+                                "side index" if not args.no_index else "serial decode", D, Bp, hw_queue_note())),
+                "W": W, "H": H, "tiles": (W // 256) * (H // 256), "per_gpu": "%dx%d" % (W, p["rows"]), "batch": Bp,
                 "parallelism": "tile rows sharded over %d GPU(s), RCCL gather to rank 0" % world,
             },
             "roofline": roof,
             "detail": detail,
         }
         print(json.dumps(res), flush=True)
+        bad = (not all(checked.values())) or detail.get("strong_16384_bit_exact_vs_reference") is False
     ok = p["lossless"] and (strong is None or strong["lossless"])
     dist.destroy_process_group()
-    if not ok:
+    if not ok or bad:
         sys.exit(3)
 
 

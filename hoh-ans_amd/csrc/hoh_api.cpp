@@ -203,6 +203,8 @@ void hoh_ctx_destroy(hoh_ctx* c) {
 
 void hoh_set_profiling(hoh_ctx* c, int on) { if (c) c->profiling = on; }
 
+void* hoh_ctx_stream(hoh_ctx* c) { return c ? (void*)c->own : nullptr; }
+
 int hoh_ctx_set_option(hoh_ctx* c, int option, int64_t value) {
   if (!c) return HOH_E_ARG;
   switch (option) {
@@ -252,7 +254,9 @@ extern "C" int hoh_debug_read(hoh_ctx* c, int which, void* dst, size_t bytes) {
   // 3: k_lzsort's posting lists of the last -s1..-s4 encode (per entry key | fingerprint << 32, first-pass entries,
   // u16 ranks: tools/scripts/lzsort_check.py); 4: the fingerprints + tile pixel words (k_lzfp)
   // 5: the per-tile kernel counters of the last encode (EncodeJob::dbg, [tile][64] u32)
-  const Buf& b = which == 0 ? c->matches : which == 3 ? c->lzs : which == 4 ? c->fpb : which == 5 ? c->dbg : c->lzspec;
+  // 6: the StreamInfo records of the last encode (tests/test_gpu_check_build.py: ladder bounds)
+  const Buf& b = which == 0 ? c->matches : which == 3 ? c->lzs : which == 4 ? c->fpb : which == 5 ? c->dbg
+               : which == 6 ? c->streams : c->lzspec;
   if (bytes > b.n || !b.p) return HOH_E_ARG;
   return hipMemcpy(dst, b.p, bytes, hipMemcpyDeviceToHost) == hipSuccess ? HOH_OK : HOH_E_HIP;
 }
@@ -590,6 +594,40 @@ int hoh_encode_tiles_async(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int s
   uint64_t total = 0;
   return encode_tiles_impl(c, d_rgb, W, H, t0, ntiles, d_out, cap, 0, 0, d_tile_sizes, &total, speed ? nullptr : idx,
                            pick(c, stream), speed, d_status);
+}
+
+// n images' shards per call (choh.cpp:464-500's tile loop over a band of tile rows, run over a
+// batch).  When the band is whole tile rows of 256 (H a multiple of 256), the n bands stacked in
+// d_rgb are the tile grid of one W x (n * rows) image, so every kernel covers all n bands' tiles in
+// one launch, exactly as hoh_encode_images_async stacks whole images; blob i gets its own layout
+// (k_layout: one workgroup per band) at d_out + i * stride.  Otherwise the bands run one after
+// another on the stream (same bytes).
+int hoh_encode_tiles_images_async(hoh_ctx* c, int n, const uint8_t* d_rgb, int W, int H, int speed, int t0,
+                                  int ntiles, uint8_t* d_out, size_t stride, uint32_t* d_tile_sizes, hoh_index* idx,
+                                  uint64_t* d_status, void* stream) {
+  if (!c || n <= 0 || !d_rgb || !d_out || !d_tile_sizes || !d_status || W <= 0 || H <= 0 || speed < 0 || speed > 4 ||
+      stride == 0)
+    return HOH_E_ARG;
+  int xt, yt, tw, th;
+  if (!hoh_tiling(W, H, &xt, &yt, &tw, &th)) return HOH_E_UNSUPPORTED;     // header-only files carry no tiles
+  if (t0 < 0 || ntiles <= 0 || t0 + ntiles > xt * yt || t0 % xt || ntiles % xt) return HOH_E_ARG;
+  const int y0 = (t0 / xt) * th, rows = std::min(H, (t0 + ntiles) / xt * th) - y0;
+  const size_t band = (size_t)W * rows * 3;
+  if (n == 1 || speed || !batch_stacks(W, H)) {
+    if (idx && n > 1) return HOH_E_UNSUPPORTED;      // a side index holds one shard here
+    for (int i = 0; i < n; i++) {
+      const int r = hoh_encode_tiles_async(c, d_rgb + i * band - (size_t)y0 * W * 3, W, H, speed, t0, ntiles,
+                                           d_out + i * stride, stride, d_tile_sizes + (size_t)i * ntiles, idx,
+                                           d_status + 2 * i, stream);
+      if (r) return r;
+    }
+    return HOH_OK;
+  }
+  if ((int64_t)rows * n > (1ll << 30) || (int64_t)ntiles * n > (1 << 24)) return HOH_E_ARG;
+  (void)hipSetDevice(c->device);
+  uint64_t total = 0;
+  return encode_tiles_impl(c, d_rgb, W, rows * n, 0, ntiles * n, d_out, stride, 0, 0, d_tile_sizes, &total, idx,
+                           pick(c, stream), 0, d_status, n, stride);
 }
 
 int hoh_encode_image_ix(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int speed, uint8_t* d_out,

@@ -17,6 +17,9 @@ int decode_tiles_impl(hoh_ctx* c, const uint8_t* d_blob, size_t size, int W, int
 int decode_tiles_async_impl(hoh_ctx* c, const uint8_t* d_blob, size_t size, int W, int H, int t0, int ntiles,
                             const uint32_t* d_sizes, uint8_t* d_rgb, const hoh_index* idx, uint64_t* d_status,
                             hipStream_t s);
+int decode_tiles_images_async_impl(hoh_ctx* c, int n, const uint8_t* d_blob, size_t stride, int W, int H, int t0,
+                                   int ntiles, const uint32_t* d_sizes, uint8_t* d_rgb, const hoh_index* idx,
+                                   uint64_t* d_status, hipStream_t s);
 int decode_stream_impl(hoh_ctx* c, const uint8_t* d_in, size_t size, size_t* bp, uint16_t* d_out, size_t cap,
                        size_t* n, hipStream_t s);
 int encode_streams_impl(hoh_ctx* c, const uint16_t* d_syms, const uint64_t* off, const uint32_t* cnt, int nstreams,
@@ -92,6 +95,16 @@ int hoh_decode_tiles_async(hoh_ctx* c, const uint8_t* d_blob, size_t size, int W
   (void)hipSetDevice(ctx_device(c));
   return decode_tiles_async_impl(c, d_blob, size, W, H, t0, ntiles, d_tile_sizes, d_rgb, idx, d_status,
                                  ctx_stream(c, stream));
+}
+
+int hoh_decode_tiles_images_async(hoh_ctx* c, int n, const uint8_t* d_blob, size_t stride, int W, int H, int t0,
+                                  int ntiles, const uint32_t* d_tile_sizes, uint8_t* d_rgb, const hoh_index* idx,
+                                  uint64_t* d_status, void* stream) {
+  if (!c || n <= 0 || !d_blob || !d_rgb || !d_tile_sizes || !d_status || W <= 0 || H <= 0 || stride == 0)
+    return HOH_E_ARG;
+  (void)hipSetDevice(ctx_device(c));
+  return decode_tiles_images_async_impl(c, n, d_blob, stride, W, H, t0, ntiles, d_tile_sizes, d_rgb, idx, d_status,
+                                        ctx_stream(c, stream));
 }
 
 int hoh_decode_image(hoh_ctx* c, const uint8_t* d_hoh, size_t size, uint8_t* d_rgb, size_t cap, int* W, int* H,

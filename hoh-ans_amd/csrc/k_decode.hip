@@ -146,7 +146,7 @@ __global__ __launch_bounds__(1024) void k_dtable(DecJob j) {
     const int xo = (g % j.xt) * j.tw, yo = (g / j.xt) * j.th;
     t.x0 = xo; t.y0 = yo;
     t.w = min(j.tw, j.W - xo); t.h = min(j.th, j.H - yo);
-    t.off = i == 0 ? 0 : (j.tsizes ? j.tsizes[i - 1] : 0);
+    t.off = i == 0 ? 0 : (j.tsizes ? j.tsizes[ib + i - 1] : 0);
     t.mode = 0; t.nmatch = 0; t.err = 0; t.pad = 0;
     tiles[i] = t;
   }
@@ -331,9 +331,14 @@ __device__ bool parse_stream(const DecJob& j, uint64_t& p, int sid, uint64_t out
   return true;
 }
 
-__global__ __launch_bounds__(64) void k_dparse(DecJob j) {
-  if (dec_abort(j)) return;
+__global__ __launch_bounds__(64) void k_dparse(DecJob job) {
+  if (dec_abort(job)) return;
   const int t = blockIdx.x, lane = threadIdx.x;
+  // a batch: every bound check of this tile's framing and streams stops at its own file's end
+  // (file i is [i * in_stride, (i + 1) * in_stride)), so a truncated file reads as corrupt instead
+  // of running on into the next file's bytes
+  DecJob j = job;
+  if (j.nimg > 1) j.size = min(job.size, (uint64_t)(t / j.img_tiles + 1) * j.in_stride);
   DecTile ti = j.tiles[t];
   uint64_t p = ti.off;
   bool ok = p + 4 <= j.size;
@@ -2521,6 +2526,52 @@ int decode_tiles_async_impl(hoh_ctx* c, const uint8_t* d_blob, size_t size, int 
     const int g = t0 + i, xo = (g % j.xt) * j.tw, yo = (g / j.xt) * j.th;
     as.bytes += (uint64_t)std::min(j.tw, W - xo) * std::min(j.th, H - yo) * 3;
   }
+  return decode_run(c, j, idx, s, &as);
+}
+
+// enqueue-only decode of n shards (tiles [t0, t0+ntiles) of n W x H images): blob i at
+// d_blob + i * stride, its tile sizes at d_sizes + i * ntiles (device), band i's RGB at
+// d_rgb + i * W * rows * 3.  Whole 256-row tile bands stack into one W x (n * rows) job (one
+// dtable workgroup per blob), as decode_images_async_impl stacks whole files; otherwise the
+// shards run one after another.  {status, band RGB bytes} per shard in d_status.
+int decode_tiles_images_async_impl(hoh_ctx* c, int n, const uint8_t* d_blob, size_t stride, int W, int H, int t0,
+                                   int ntiles, const uint32_t* d_sizes, uint8_t* d_rgb, const hoh_index* idx,
+                                   uint64_t* d_status, hipStream_t s) {
+  if (!((W >= 512 || H >= 512) && W >= 256 && H >= 256)) return 6;
+  const int xt = W / 256, yt = H / 256, th = (H + yt - 1) / yt;
+  if (t0 < 0 || ntiles <= 0 || t0 + ntiles > xt * yt || t0 % xt || ntiles % xt) return 1;
+  const int y0 = (t0 / xt) * th, rows = std::min(H, (t0 + ntiles) / xt * th) - y0;
+  const size_t band = (size_t)W * rows * 3;
+  if (n == 1 || !batch_stacks(W, H)) {
+    if (idx && n > 1) return 6;
+    for (int i = 0; i < n; i++) {
+      const int r = decode_tiles_async_impl(c, d_blob + i * stride, stride, W, H, t0, ntiles, d_sizes + (size_t)i * ntiles,
+                                            d_rgb + i * band - (size_t)y0 * W * 3, idx, d_status + 2 * i, s);
+      if (r) return r;
+    }
+    return 0;
+  }
+  if ((int64_t)rows * n > (1ll << 30) || (int64_t)ntiles * n > (1 << 24)) return 1;
+  DecJob j;
+  memset(&j, 0, sizeof(j));
+  j.W = W; j.H = rows * n;                        // the stack of the n bands
+  j.xt = xt; j.yt = rows * n / 256;
+  j.tw = (W + xt - 1) / xt; j.th = 256;
+  j.t0 = 0;
+  j.ntiles = ntiles * n;
+  j.nimg = n;
+  j.img_tiles = ntiles;
+  j.in_stride = stride;
+  j.prefix = 0;
+  j.in = d_blob;
+  j.size = (uint64_t)n * stride;
+  j.rgb = d_rgb;
+  j.tsizes = d_sizes;
+  AsyncDec as;
+  as.hdr[0] = as.hdr[1] = 0;
+  as.hl = 0;                                      // blobs have no header to check
+  as.status = d_status;
+  as.bytes = (uint64_t)band;
   return decode_run(c, j, idx, s, &as);
 }
 

@@ -62,6 +62,8 @@ def lib():
         L.hoh_reset_kernel_stats.argtypes = [vp]
         L.hoh_reset_kernel_stats.restype = None
         L.hoh_ctx_set_option.argtypes = [vp, C.c_int, C.c_int64]
+        L.hoh_ctx_stream.restype = vp
+        L.hoh_ctx_stream.argtypes = [vp]
         L.hoh_encode_bound.restype = sz
         L.hoh_encode_bound.argtypes = [C.c_int, C.c_int]
         L.hoh_encode_image.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, vp, sz, szp, szp, vp]
@@ -92,6 +94,10 @@ def lib():
             ("hoh_encode_tiles_async", [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, sz, vp, vp, vp,
                                         vp]),
             ("hoh_decode_tiles_async", [vp, vp, sz, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, vp]),
+            ("hoh_encode_tiles_images_async", [vp, C.c_int, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, sz,
+                                               vp, vp, vp, vp]),
+            ("hoh_decode_tiles_images_async", [vp, C.c_int, vp, sz, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp,
+                                               vp, vp]),
             ("hoh_mgpu_create", [C.POINTER(vp), C.c_int, ip]),
             ("hoh_mgpu_destroy", [vp]),
             ("hoh_mgpu_transport", [vp]),
@@ -174,6 +180,13 @@ class Context:
     def reset_stats(self):
         lib().hoh_reset_kernel_stats(self.h)
 
+    def own_stream(self, torch):
+        """The context's own HIP stream (hoh_ctx_stream) as a torch stream, for event fences."""
+        if getattr(self, "_own", None) is None:
+            self._own = torch.cuda.ExternalStream(int(lib().hoh_ctx_stream(self.h) or 0),
+                                                  device=torch.device("cuda", self.device))
+        return self._own
+
     def set_option(self, option, value):
         """hoh_ctx_set_option: e.g. set_option(OPT_NOIX_DECODER, NOIX_LANES)."""
         check(lib().hoh_ctx_set_option(self.h, option, value), "hoh_ctx_set_option")
@@ -202,20 +215,23 @@ def tiling(W, H):
 
 # ------------------------------------------------------------------ device-resident (torch) API
 
-def _stream_ptr(torch):
+def _stream_ptr(torch, ctx):
     """torch's current stream as the call's stream.  torch's default stream is handle 0, which the
     C ABI reads as "the context's own stream" (include/hoh_ans.h), a stream torch does not order
-    against: on it, torch's pending work is drained first (the call then sees the buffers torch
-    filled), and _after_call drains the library's work (torch then sees what the call wrote)."""
-    h = torch.cuda.current_stream().cuda_stream
-    if not h:
-        torch.cuda.synchronize()
-    return vp(h)
+    against; on it the call is fenced by events instead: the context's stream waits for the work
+    torch has queued on the default stream (the call then sees the buffers torch filled), and
+    _after_call makes the default stream wait for the call (torch then sees what it wrote).
+    Neither side blocks the host or any other stream."""
+    cur = torch.cuda.current_stream()
+    if not cur.cuda_stream:
+        ctx.own_stream(torch).wait_stream(cur)
+    return vp(cur.cuda_stream)
 
 
-def _after_call(torch):
-    if not torch.cuda.current_stream().cuda_stream:
-        torch.cuda.synchronize()
+def _after_call(torch, ctx):
+    cur = torch.cuda.current_stream()
+    if not cur.cuda_stream:
+        cur.wait_stream(ctx.own_stream(torch))
 
 
 class Index:
@@ -246,9 +262,9 @@ def encode_image(rgb_dev, W, H, out_dev=None, ctx=None, index=None, speed=0):
     n, printed = C.c_size_t(0), C.c_size_t(0)
     r = lib().hoh_encode_image_ix(ctx.h, vp(rgb_dev.data_ptr()), W, H, speed, vp(out_dev.data_ptr()),
                                   out_dev.numel(), C.byref(n), C.byref(printed),
-                                  index.h if index is not None else None, _stream_ptr(torch))
+                                  index.h if index is not None else None, _stream_ptr(torch, ctx))
     check(r, "hoh_encode_image")
-    _after_call(torch)
+    _after_call(torch, ctx)
     return out_dev, n.value, printed.value
 
 
@@ -263,9 +279,9 @@ def decode_image(hoh_dev, size, out_dev=None, ctx=None, index=None):
     w, h = C.c_int(), C.c_int()
     r = lib().hoh_decode_image_ix(ctx.h, vp(hoh_dev.data_ptr()), size, vp(out_dev.data_ptr()),
                                   out_dev.numel(), C.byref(w), C.byref(h),
-                                  index.h if index is not None else None, _stream_ptr(torch))
+                                  index.h if index is not None else None, _stream_ptr(torch, ctx))
     check(r, "hoh_decode_image")
-    _after_call(torch)
+    _after_call(torch, ctx)
     return out_dev, w.value, h.value
 
 
@@ -277,9 +293,9 @@ def encode_image_async(rgb_dev, W, H, out_dev, status_dev, ctx=None, index=None,
     ctx = ctx or default_ctx()
     r = lib().hoh_encode_image_async(ctx.h, vp(rgb_dev.data_ptr()), W, H, speed, vp(out_dev.data_ptr()),
                                      out_dev.numel(), index.h if index is not None else None,
-                                     vp(status_dev.data_ptr()), _stream_ptr(torch))
+                                     vp(status_dev.data_ptr()), _stream_ptr(torch, ctx))
     check(r, "hoh_encode_image_async")
-    _after_call(torch)
+    _after_call(torch, ctx)
 
 
 def decode_image_async(hoh_dev, size, W, H, out_dev, status_dev, ctx=None, index=None):
@@ -289,9 +305,9 @@ def decode_image_async(hoh_dev, size, W, H, out_dev, status_dev, ctx=None, index
     ctx = ctx or default_ctx()
     r = lib().hoh_decode_image_async(ctx.h, vp(hoh_dev.data_ptr()), size, W, H, vp(out_dev.data_ptr()),
                                      out_dev.numel(), index.h if index is not None else None,
-                                     vp(status_dev.data_ptr()), _stream_ptr(torch))
+                                     vp(status_dev.data_ptr()), _stream_ptr(torch, ctx))
     check(r, "hoh_decode_image_async")
-    _after_call(torch)
+    _after_call(torch, ctx)
 
 
 def encode_images_async(rgb_dev, n, W, H, out_dev, stride, status_dev, ctx=None, index=None, speed=0):
@@ -303,9 +319,9 @@ def encode_images_async(rgb_dev, n, W, H, out_dev, stride, status_dev, ctx=None,
     assert out_dev.numel() >= n * stride and rgb_dev.numel() >= n * W * H * 3 and status_dev.numel() >= 2 * n
     r = lib().hoh_encode_images_async(ctx.h, n, vp(rgb_dev.data_ptr()), W, H, speed, vp(out_dev.data_ptr()), stride,
                                       index.h if index is not None else None, vp(status_dev.data_ptr()),
-                                      _stream_ptr(torch))
+                                      _stream_ptr(torch, ctx))
     check(r, "hoh_encode_images_async")
-    _after_call(torch)
+    _after_call(torch, ctx)
 
 
 def decode_images_async(hoh_dev, n, stride, W, H, out_dev, status_dev, ctx=None, index=None):
@@ -315,9 +331,9 @@ def decode_images_async(hoh_dev, n, stride, W, H, out_dev, status_dev, ctx=None,
     assert hoh_dev.numel() >= n * stride and out_dev.numel() >= n * W * H * 3 and status_dev.numel() >= 2 * n
     r = lib().hoh_decode_images_async(ctx.h, n, vp(hoh_dev.data_ptr()), stride, W, H, vp(out_dev.data_ptr()),
                                       index.h if index is not None else None, vp(status_dev.data_ptr()),
-                                      _stream_ptr(torch))
+                                      _stream_ptr(torch, ctx))
     check(r, "hoh_decode_images_async")
-    _after_call(torch)
+    _after_call(torch, ctx)
 
 
 def check_status(status, what):
@@ -338,9 +354,9 @@ def encode_tiles(rgb_dev, W, H, t0, ntiles, out_dev, sizes_dev, ctx=None, index=
     base = rgb_dev.data_ptr() - row0 * W * 3
     r = lib().hoh_encode_tiles_speed(ctx.h, vp(base), W, H, speed, t0, ntiles, vp(out_dev.data_ptr()),
                                      out_dev.numel(), vp(sizes_dev.data_ptr()), C.byref(n),
-                                     index.h if index is not None else None, _stream_ptr(torch))
+                                     index.h if index is not None else None, _stream_ptr(torch, ctx))
     check(r, "hoh_encode_tiles")
-    _after_call(torch)
+    _after_call(torch, ctx)
     return n.value
 
 
@@ -351,9 +367,9 @@ def decode_tiles(blob_dev, size, W, H, t0, tile_sizes, out_dev, ctx=None, index=
     ts = np.ascontiguousarray(tile_sizes, dtype=np.uint32)
     base = out_dev.data_ptr() - row0 * W * 3
     r = lib().hoh_decode_tiles(ctx.h, vp(blob_dev.data_ptr()), size, W, H, t0, ts.size, _p(ts), vp(base),
-                               index.h if index is not None else None, _stream_ptr(torch))
+                               index.h if index is not None else None, _stream_ptr(torch, ctx))
     check(r, "hoh_decode_tiles")
-    _after_call(torch)
+    _after_call(torch, ctx)
 
 
 def encode_tiles_async(rgb_dev, W, H, t0, ntiles, out_dev, sizes_dev, status_dev, ctx=None, index=None, row0=0,
@@ -365,9 +381,9 @@ def encode_tiles_async(rgb_dev, W, H, t0, ntiles, out_dev, sizes_dev, status_dev
     base = rgb_dev.data_ptr() - row0 * W * 3
     r = lib().hoh_encode_tiles_async(ctx.h, vp(base), W, H, speed, t0, ntiles, vp(out_dev.data_ptr()),
                                      out_dev.numel(), vp(sizes_dev.data_ptr()), index.h if index is not None else None,
-                                     vp(status_dev.data_ptr()), _stream_ptr(torch))
+                                     vp(status_dev.data_ptr()), _stream_ptr(torch, ctx))
     check(r, "hoh_encode_tiles_async")
-    _after_call(torch)
+    _after_call(torch, ctx)
 
 
 def decode_tiles_async(blob_dev, size, W, H, t0, ntiles, sizes_dev, out_dev, status_dev, ctx=None, index=None, row0=0):
@@ -378,9 +394,41 @@ def decode_tiles_async(blob_dev, size, W, H, t0, ntiles, sizes_dev, out_dev, sta
     base = out_dev.data_ptr() - row0 * W * 3
     r = lib().hoh_decode_tiles_async(ctx.h, vp(blob_dev.data_ptr()), size, W, H, t0, ntiles, vp(sizes_dev.data_ptr()),
                                      vp(base), index.h if index is not None else None, vp(status_dev.data_ptr()),
-                                     _stream_ptr(torch))
+                                     _stream_ptr(torch, ctx))
     check(r, "hoh_decode_tiles_async")
-    _after_call(torch)
+    _after_call(torch, ctx)
+
+
+def encode_tiles_images_async(rgb_dev, n, W, H, t0, ntiles, out_dev, stride, sizes_dev, status_dev, ctx=None,
+                              index=None, speed=0):
+    """Enqueue-only encode of the same shard (tiles [t0, t0+ntiles), whole tile rows) of n images
+    (hoh_encode_tiles_images_async): rgb_dev holds the n bands back to back, blob i goes to
+    out_dev + i*stride, its tile sizes to sizes_dev[i*ntiles:(i+1)*ntiles] (int32/uint32, device),
+    {status, blob size} per shard to status_dev (2n int64)."""
+    import torch
+    ctx = ctx or default_ctx()
+    assert out_dev.numel() >= n * stride and sizes_dev.numel() >= n * ntiles and status_dev.numel() >= 2 * n
+    r = lib().hoh_encode_tiles_images_async(ctx.h, n, vp(rgb_dev.data_ptr()), W, H, speed, t0, ntiles,
+                                            vp(out_dev.data_ptr()), stride, vp(sizes_dev.data_ptr()),
+                                            index.h if index is not None else None, vp(status_dev.data_ptr()),
+                                            _stream_ptr(torch, ctx))
+    check(r, "hoh_encode_tiles_images_async")
+    _after_call(torch, ctx)
+
+
+def decode_tiles_images_async(blob_dev, n, stride, W, H, t0, ntiles, sizes_dev, out_dev, status_dev, ctx=None,
+                              index=None):
+    """Inverse of encode_tiles_images_async: n blobs (tile sizes on the device) -> n bands back to
+    back in out_dev; {status, band RGB bytes} per shard in status_dev."""
+    import torch
+    ctx = ctx or default_ctx()
+    assert blob_dev.numel() >= n * stride and sizes_dev.numel() >= n * ntiles and status_dev.numel() >= 2 * n
+    r = lib().hoh_decode_tiles_images_async(ctx.h, n, vp(blob_dev.data_ptr()), stride, W, H, t0, ntiles,
+                                            vp(sizes_dev.data_ptr()), vp(out_dev.data_ptr()),
+                                            index.h if index is not None else None, vp(status_dev.data_ptr()),
+                                            _stream_ptr(torch, ctx))
+    check(r, "hoh_decode_tiles_images_async")
+    _after_call(torch, ctx)
 
 
 def file_prefix(W, H, tile_sizes):
@@ -405,9 +453,9 @@ def synth_rgb_dev(W, H, seed=1, noise=4, ctx=None, device="cuda", row0=0):
     import torch
     ctx = ctx or default_ctx()
     t = torch.empty(W * H * 3, dtype=torch.uint8, device=device)
-    check(lib().hoh_synth_rgb_rows(ctx.h, vp(t.data_ptr()), W, row0, H, seed, noise, _stream_ptr(torch)),
+    check(lib().hoh_synth_rgb_rows(ctx.h, vp(t.data_ptr()), W, row0, H, seed, noise, _stream_ptr(torch, ctx)),
           "hoh_synth_rgb_rows")
-    _after_call(torch)
+    _after_call(torch, ctx)
     return t
 
 
@@ -417,9 +465,9 @@ def natural_rgb_dev(W, H, seed=1, ctx=None, device="cuda", row0=0):
     import torch
     ctx = ctx or default_ctx()
     t = torch.empty(W * H * 3, dtype=torch.uint8, device=device)
-    check(lib().hoh_natural_rgb_rows(ctx.h, vp(t.data_ptr()), W, row0, H, seed, _stream_ptr(torch)),
+    check(lib().hoh_natural_rgb_rows(ctx.h, vp(t.data_ptr()), W, row0, H, seed, _stream_ptr(torch, ctx)),
           "hoh_natural_rgb_rows")
-    _after_call(torch)
+    _after_call(torch, ctx)
     return t
 
 

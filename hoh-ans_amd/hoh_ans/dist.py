@@ -112,6 +112,73 @@ class FileGather:
         return self.file, total
 
 
+class BatchGather:
+    """FileGather for B images at once (bench.py's batched N > 1 schedule: every rank encodes the
+    same band of B images per step, hoh_encode_tiles_images_async).  Blob i of this rank lies at
+    blob[i*stride:]; tile_sizes is a (B, ntiles) array of this rank's tile sizes.  ONE all_gather
+    carries all B images' tile sizes, then ONE batch of point-to-point operations moves every
+    (rank, image) blob straight into its place in image i's file on rank 0 (row i of `files`,
+    behind hoh_file_prefix).  Returns (files, totals, requests) on rank 0 -- files is a (B, cap)
+    uint8 tensor, totals the B file sizes -- and (None, [0]*B, requests) elsewhere; with wait=True
+    the requests are waited on and the third element is omitted."""
+
+    def __init__(self, W, H, B, device, group=None):
+        self.W, self.H, self.B, self.device, self.group = W, H, B, device, group
+        self.files = None
+        self.totals = [0] * B
+
+    def __call__(self, blob, stride, tile_sizes, wait=True):
+        import torch
+        import torch.distributed as dist
+        B = self.B
+        rank = dist.get_rank(self.group)
+        world = dist.get_world_size(self.group)
+        counts = shard_counts(self.W, self.H, world)
+        ts = np.asarray(tile_sizes, dtype=np.int64).reshape(B, -1)
+        if ts.shape[1] != counts[rank]:
+            raise RuntimeError("rank %d holds %d tile sizes per image, its shard has %d tiles"
+                               % (rank, ts.shape[1], counts[rank]))
+        per = [s.reshape(B, c) for s, c in zip(gather_sizes(ts.reshape(-1), self.device, self.group,
+                                                               [c * B for c in counts]), counts)]
+        bsz = [[int(per[r][i].sum(dtype=np.int64)) for i in range(B)] for r in range(world)]
+        if max(bsz[rank]) > stride:
+            raise RuntimeError("a blob is larger than the stride")
+        ranks = dist.get_process_group_ranks(self.group) if self.group is not None else list(range(world))
+        if rank != 0:
+            ops = [dist.P2POp(dist.isend, blob[i * stride:i * stride + bsz[rank][i]], ranks[0], self.group)
+                   for i in range(B) if bsz[rank][i]]
+            reqs = dist.batch_isend_irecv(ops) if ops else []
+            if wait:
+                for q in reqs:
+                    q.wait()
+                return None, [0] * B
+            return None, [0] * B, reqs
+        prefixes = [file_prefix(self.W, self.H, np.concatenate([per[r][i] for r in range(world)])) for i in range(B)]
+        totals = [len(prefixes[i]) + sum(bsz[r][i] for r in range(world)) for i in range(B)]
+        need = max(totals)
+        if self.files is None or self.files.shape[1] < need:
+            self.files = torch.empty((B, need + need // 16), dtype=torch.uint8, device=self.device)
+        ops = []
+        for i in range(B):
+            pl = len(prefixes[i])
+            self.files[i, :pl] = torch.frombuffer(bytearray(prefixes[i]), dtype=torch.uint8).to(self.device)
+            off = pl + bsz[0][i]
+            for r in range(1, world):
+                if bsz[r][i]:
+                    ops.append(dist.P2POp(dist.irecv, self.files[i, off:off + bsz[r][i]], ranks[r], self.group))
+                off += bsz[r][i]
+        reqs = dist.batch_isend_irecv(ops) if ops else []
+        for i in range(B):
+            pl = len(prefixes[i])
+            self.files[i, pl:pl + bsz[0][i]] = blob[i * stride:i * stride + bsz[0][i]]
+        self.totals = totals
+        if not wait:
+            return self.files, totals, reqs
+        for q in reqs:
+            q.wait()
+        return self.files, totals
+
+
 def run_pipeline(nslots, total, enqueue, finish):
     """Single-thread pipeline over `nslots` in-flight slots: step i goes to slot i % nslots.
     enqueue(slot, i) enqueues step i's device work without waiting on the host; finish(slot, i)

@@ -45,6 +45,10 @@ typedef struct hoh_ctx hoh_ctx;
 int hoh_ctx_create(hoh_ctx** ctx, int device);
 void hoh_ctx_destroy(hoh_ctx* ctx);
 const char* hoh_strerror(int code);
+/* The context's own HIP stream (what a NULL `stream` argument means), as void*: callers that
+ * order their own streams against it with events (the Python mirror fences torch's default
+ * stream this way). */
+void* hoh_ctx_stream(hoh_ctx* ctx);
 const char* hoh_version(void);
 /* Number of device allocations (hipMalloc) the library has made so far, process-wide.  Contexts
  * keep grow-only workspaces, so repeated calls of one shape allocate nothing after the first. */
@@ -134,8 +138,12 @@ int hoh_decode_image_async(hoh_ctx* ctx, const uint8_t* d_hoh, size_t size, int 
  * (payload positions are absolute in the batch buffer), so a decode with it needs the same n and
  * stride (else HOH_E_ARG).  The batch runs as one job when its tiles stack -- H a multiple of 256,
  * so the n images are the 256-row tile grid of one n*H image -- at -s0;
- * otherwise the images run one after another on the stream (without a side index when n > 1:
- * HOH_E_UNSUPPORTED). */
+ * otherwise tiled images run one after another on the stream (without a side index when n > 1:
+ * HOH_E_UNSUPPORTED).  Untiled shapes (header-only files) return HOH_E_UNSUPPORTED for
+ * any n, as in the single-image async calls: use hoh_encode_image / hoh_decode_image.  The decoder
+ * bounds every parse of file i by [i*stride, (i+1)*stride) (a truncated file reads as corrupt) and
+ * reads n*stride bytes of d_hoh at most; in a one-job batch an error in any file marks every
+ * image's status. */
 int hoh_encode_images_async(hoh_ctx* ctx, int n, const uint8_t* d_rgb, int W, int H, int speed, uint8_t* d_out,
                             size_t stride, hoh_index* idx, uint64_t* d_status, void* stream);
 int hoh_decode_images_async(hoh_ctx* ctx, int n, const uint8_t* d_hoh, size_t stride, int W, int H, uint8_t* d_rgb,
@@ -176,6 +184,25 @@ int hoh_encode_tiles_async(hoh_ctx* ctx, const uint8_t* d_rgb, int W, int H, int
 int hoh_decode_tiles_async(hoh_ctx* ctx, const uint8_t* d_blob, size_t size, int W, int H, int t0, int ntiles,
                            const uint32_t* d_tile_sizes, uint8_t* d_rgb, const hoh_index* idx, uint64_t* d_status,
                            void* stream);
+/* Batched shards (multi-GPU with several images in flight per GPU): the same tile band
+ * [t0, t0+ntiles) of n W x H images per call.  The band must be whole tile rows (t0 and ntiles
+ * multiples of x_tiles, else HOH_E_ARG).  d_rgb holds the n bands back to back (band i = rows
+ * [y0, y1) of image i at d_rgb + i*W*(y1-y0)*3 -- NOT the image base as in the single-shard
+ * calls); blob i is written at / read from d_blob + i*stride, its tile sizes at
+ * d_tile_sizes + i*ntiles (device u32); d_status holds {status, blob size} (encode) or {status,
+ * band RGB bytes} (decode) per shard.  When H is a multiple of 256 the n bands stack into one
+ * tile grid and every kernel covers all n shards per launch (as hoh_encode_images_async does for
+ * whole images); otherwise the shards run one after another on the stream.  Blobs are
+ * byte-identical to n single-shard calls'.  -s0 stacks; -s>=1 runs shard after shard.  A side
+ * index serves the batch it was recorded for (same n and stride).  The decoder bounds every parse
+ * of blob i by [i*stride, (i+1)*stride) and reads n*stride bytes of d_blob at most; in a one-job
+ * batch an error in any blob marks every shard's status. */
+int hoh_encode_tiles_images_async(hoh_ctx* ctx, int n, const uint8_t* d_rgb, int W, int H, int speed, int t0,
+                                  int ntiles, uint8_t* d_blob, size_t stride, uint32_t* d_tile_sizes, hoh_index* idx,
+                                  uint64_t* d_status, void* stream);
+int hoh_decode_tiles_images_async(hoh_ctx* ctx, int n, const uint8_t* d_blob, size_t stride, int W, int H, int t0,
+                                  int ntiles, const uint32_t* d_tile_sizes, uint8_t* d_rgb, const hoh_index* idx,
+                                  uint64_t* d_status, void* stream);
 /* Host: the .hoh prefix for a tiled image given every tile's size (choh.cpp:437-498):
  * magic, format, depth, varint W-1, H-1, x_tiles-1, y_tiles-1, n-1 varint sizes.  Returns the
  * prefix length, or 0 if cap is too small. */

@@ -219,3 +219,72 @@ def test_gloo_sharded_leg(tmp_path):
     for seed in (20, 21):
         want, _ = oracle.choh(synth.synth_rgb(W, H, seed=seed, noise=4))
         assert (tmp_path / ("leg_seed%d.hoh" % seed)).read_bytes() == want
+
+
+class _BatchCpuShardOps(_CpuShardOps):
+    """CPU stand-in for bench.py's batched GpuShardOps: a slot holds B images, a step encodes the
+    rank's band of all B (the oracle's encode_tile per tile, blob i at i * STRIDE) and
+    hd.BatchGather moves all of them to rank 0 with one size exchange and one batch of
+    point-to-point operations."""
+    B, STRIDE = 2, 2 << 20
+
+    def new_slot(self, k):
+        import torch
+        seeds = [self.seed0 + k * self.B + b for b in range(self.B)]
+        return {"seeds": seeds, "imgs": [synth.synth_rgb(self.W, self.H, seed=sd, noise=4) for sd in seeds],
+                "blob": torch.zeros(self.B * self.STRIDE, dtype=torch.uint8),
+                "g": self.hd.BatchGather(self.W, self.H, self.B, "cpu"), "ok": True}
+
+    def enqueue(self, s, i):
+        import torch
+        sizes = []
+        for b, img in enumerate(s["imgs"]):
+            tiles = []
+            for t in range(self.t0, self.t0 + self.nt):
+                x, y = (t % self.xt) * self.tw, (t // self.xt) * self.th
+                tiles.append(oracle.encode_tile(img[y:y + self.th, x:x + self.tw]))
+            cat = b"".join(tiles)
+            assert len(cat) <= self.STRIDE
+            s["blob"][b * self.STRIDE:b * self.STRIDE + len(cat)] = torch.frombuffer(bytearray(cat), dtype=torch.uint8)
+            sizes.append([len(t) for t in tiles])
+        s["sizes"] = np.array(sizes, np.uint32)
+
+    def finish(self, s, i):
+        res = s["g"](s["blob"], self.STRIDE, s["sizes"], wait=False)
+        for q in res[2]:
+            q.wait()
+        self.log.append(i)
+        if self.rank == 0:
+            s["files"] = [res[0][b, :res[1][b]].numpy().tobytes() for b in range(self.B)]
+            s["ok"] = s["ok"] and all(np.array_equal(oracle.dhoh(f), img) for f, img in zip(s["files"], s["imgs"]))
+
+
+def _batch_leg_worker(rank, world, port, outdir):
+    import torch.distributed as dist
+    from hoh_ans import dist as hd
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ops = _BatchCpuShardOps(W, H, rank, world, 40)
+        slots, el, ok = hd.run_sharded_leg(ops, 2, 3, 1)
+        assert ok and el > 0
+        assert ops.log == [0, 1, 2]
+        if rank == 0:
+            for s in slots:
+                for sd, f in zip(s["seeds"], s["files"]):
+                    with open(os.path.join(outdir, "batch_seed%d.hoh" % sd), "wb") as fh:
+                        fh.write(f)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_batched_sharded_leg(tmp_path):
+    """bench.py's batched N > 1 schedule on two gloo ranks: 2 slots x 2 images, BatchGather;
+    every image's gathered file equals the single-process choh -s0 file and decodes losslessly"""
+    world = 2
+    mp.spawn(_batch_leg_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for seed in (40, 41, 42, 43):
+        want, _ = oracle.choh(synth.synth_rgb(W, H, seed=seed, noise=4))
+        assert (tmp_path / ("batch_seed%d.hoh" % seed)).read_bytes() == want, seed

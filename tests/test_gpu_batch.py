@@ -138,3 +138,59 @@ def test_batch_index_layout_checked(hoh):
     assert torch.equal(out2[:sizes[0]], out[:sizes[0]])
     assert torch.equal(out2[2 * small:2 * small + sizes[2]], out[2 * stride:2 * stride + sizes[2]])
     ctx.close()
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_batch_untiled_shape_unsupported(hoh, n):
+    """untiled shapes (header-only files) are refused by the batched calls for any n,
+    as by the single-image async calls (include/hoh_ans.h); the synchronous call encodes them"""
+    import torch
+    W, H = 320, 200
+    ctx = hoh.Context(0)
+    rgb = torch.zeros(n * W * H * 3, dtype=torch.uint8, device="cuda")
+    stride = hoh.lib().hoh_encode_bound(W, H)
+    out = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(2 * n, dtype=torch.int64, device="cuda")
+    with pytest.raises(hoh.HohError) as e:
+        hoh.encode_images_async(rgb, n, W, H, out, stride, st, ctx=ctx)
+    assert e.value.code == 6
+    with pytest.raises(hoh.HohError) as e:
+        hoh.decode_images_async(out, n, stride, W, H, rgb, st, ctx=ctx)
+    assert e.value.code == 6
+    f, m, _ = hoh.encode_image(rgb[:W * H * 3], W, H, ctx=ctx)
+    assert m == 10                                 # the header only (choh.cpp:508-520): 6 + 2 varints
+    ctx.close()
+
+
+def test_batch_truncated_file_reads_corrupt(hoh):
+    """A file cut short by the batch stride must read as corrupt: the decoder bounds file i's parse
+    by [i*stride, (i+1)*stride) and never runs on into file i+1's bytes."""
+    import torch
+    W, H = 1024, 512
+    ctx = hoh.Context(0)
+    img = W * H * 3
+    rgb = torch.empty(2 * img, dtype=torch.uint8, device="cuda")
+    rgb[:img] = hoh.synth_rgb_dev(W, H, 3, 8, ctx=ctx)      # the larger file
+    rgb[img:] = hoh.synth_rgb_dev(W, H, 4, 2, ctx=ctx)
+    stride = hoh.lib().hoh_encode_bound(W, H)
+    out = torch.zeros(2 * stride, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(4, dtype=torch.int64, device="cuda")
+    hoh.encode_images_async(rgb, 2, W, H, out, stride, st, ctx=ctx)
+    s0, s1 = [hoh.check_status(x, "enc") for x in st.cpu().numpy().reshape(2, 2)]
+    assert s0 > s1 + 64
+    for cut in (s0 - 1, s0 - 40, (s0 + s1) // 2):
+        tight = max(cut, s1)
+        buf = torch.zeros(2 * tight, dtype=torch.uint8, device="cuda")
+        buf[:tight] = out[:tight]                          # file 0 truncated to `tight` bytes
+        buf[tight:tight + s1] = out[stride:stride + s1]    # file 1 right behind it
+        dec = torch.zeros(2 * img, dtype=torch.uint8, device="cuda")
+        ds = torch.full((4,), -1, dtype=torch.int64, device="cuda")
+        hoh.decode_images_async(buf, 2, tight, W, H, dec, ds, ctx=ctx)
+        codes = ds.cpu().numpy().reshape(2, 2)[:, 0]
+        assert codes[0] == 7, (cut, codes)
+    # the same files at a stride that holds both decode
+    dec = torch.zeros(2 * img, dtype=torch.uint8, device="cuda")
+    ds = torch.full((4,), -1, dtype=torch.int64, device="cuda")
+    hoh.decode_images_async(out, 2, stride, W, H, dec, ds, ctx=ctx)
+    assert all(int(c) == 0 for c in ds.cpu().numpy()[0::2]) and torch.equal(dec, rgb)
+    ctx.close()

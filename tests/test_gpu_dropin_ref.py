@@ -12,7 +12,8 @@ the flow of entropy_roundtrip_test.sh:1-11 and the layer round trip with those b
   * the reference decoder must read the drop-in's stream back too (one stream: Q1 does not bite),
     except the single-symbol table it cannot read (Q6);
   * layer_roundtrip_test must print "Layer roundtrip: OK" and exit 0 through the GPU;
-  * choh's files and printed sizes must equal the reference binary's, tiled at -s0..-s2.
+  * choh's files and printed sizes must equal the reference binary's, tiled at -s0..-s4 (with the
+    RGB and palette colour modes) and header-only.
 The inputs are repository files (the reference encodes its own source text; that file is not
 kept here), plus byte patterns that reach the stored fallback and a single-symbol table (Q6)."""
 import os
@@ -89,10 +90,28 @@ def test_layer_roundtrip_flow():
 
 
 def _choh_cases():
-    # (name, W, H, speed): tiled images (768x512: 3x2 tiles of 256; 1024^2: 4x4) at -s0 and -s1,
-    # plus an untiled one (header only)
+    # (name, W, H, speed): tiled images (768x512: 3x2 tiles of 256; 1024^2: 4x4) at -s0..-s4, plus
+    # an untiled one (header only).  -s3/-s4 take choh.cpp:265-325's RGB colour-mode
+    # branch (layer_encode per R, G, B plane with cruncher 3/4) and seek distances 12/14
+    # (choh.cpp:132-137); "palette" tiles hold <= 256 colours (palette_encode, choh.cpp:48-102, Q15)
     return [("synth", 768, 512, 0), ("synth", 768, 512, 1), ("natural", 1024, 1024, 0),
-            ("natural", 1024, 1024, 1), ("synth", 768, 512, 2), ("synth", 320, 200, 0)]
+            ("natural", 1024, 1024, 1), ("synth", 768, 512, 2), ("synth", 320, 200, 0),
+            ("synth", 768, 512, 3), ("natural", 768, 512, 3), ("natural", 768, 512, 4),
+            ("palette", 512, 256, 3), ("palette", 512, 256, 4), ("natural", 768, 512, 2)]
+
+
+def _image(kind, W, H):
+    import hoh_ans.natural as nat
+    from hoh_ans import synth
+    if kind == "synth":
+        return synth.synth_rgb(W, H, seed=3, noise=4)
+    if kind == "natural":
+        return nat.natural_rgb(W, H, 1)
+    rs = np.random.RandomState(21)                 # test_gpu_search.py's palette image
+    pal = np.stack([rs.randint(0, 256, 40), np.full(40, 9), rs.randint(0, 256, 40)], 1).astype(np.uint8)
+    img = synth.synth_rgb(W, H, 10, 3)
+    img[:, W // 2:] = pal[rs.randint(0, 40, (H, W - W // 2))]
+    return img
 
 
 @pytest.mark.parametrize("case", _choh_cases(), ids=lambda c: "%s-%dx%d-s%d" % c)
@@ -101,10 +120,8 @@ def test_choh_through_dropins(tmp_path, case):
     which calls layer_encode (layer_encode.hpp:11-20) per plane and encode_entropy for the LZ and
     palette streams) compiled unchanged against the drop-ins and run on the GPU: its file and
     printed size must equal the reference binary's (oracle/_ref/choh, same source, no drop-ins)."""
-    import hoh_ans.natural as nat
-    from hoh_ans import synth
     kind, W, H, speed = case
-    img = synth.synth_rgb(W, H, seed=3, noise=4) if kind == "synth" else nat.natural_rgb(W, H, 1)
+    img = _image(kind, W, H)
     src = tmp_path / "in.rgb"
     src.write_bytes(np.ascontiguousarray(img, dtype=np.uint8).tobytes())
     outs = {}
