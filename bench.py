@@ -14,9 +14,10 @@ One step = one pass of the hot path over one batch of the workload, inputs resid
   N > 1: weak scaling (default) -- the images are 8192 x (8192*N) and rank r owns a band of tile
          rows (8192^2 pixels per GPU per image).  --strong: configs[3], 16384x16384 images sharded
          over the N GPUs.  A step is: encode the shard of B images (hoh_encode_tiles_images_async:
-         every kernel covers the B bands' tiles), gather every shard to rank 0 over RCCL (one
-         all-gather of the B images' tile sizes, point-to-point blobs straight into rank 0's B
-         files behind their header + tile table: byte-identical to a 1-GPU encode), and decode the
+         every kernel covers the B bands' tiles), gather each image's shards over RCCL to its root
+         rank b % N (one all-gather of the B images' tile sizes, point-to-point blobs straight
+         into the root's file behind its header + tile table: byte-identical to a 1-GPU encode;
+         the roots spread the blobs over every xGMI link), and decode the
          B bands (hoh_decode_tiles_images_async, tile sizes read on the device).
 value = raw RGB bytes of the step's images x K / max-over-ranks(time of the K steps) / 1e6.
 
@@ -614,7 +615,8 @@ class GpuShardOps:
     encodes them in one batched call (hoh_encode_tiles_images_async: every kernel covers the B
     bands' tiles, tile sizes and statuses stay on the device), copies the tile sizes to pinned host
     memory behind an event and, when the step finishes, all-gathers the B images' sizes once, sends
-    the B blobs to rank 0 (each straight into its place in its file behind hoh_file_prefix) and
+    the B blobs to their files' root ranks (image b's file on rank b % N, each blob straight into
+    its place behind hoh_file_prefix: hoh_ans.dist.BatchGather) and
     decodes the B bands (hoh_decode_tiles_images_async, tile sizes read on the device) on the slot's
     stream.  The same D slots x B images schedule as the N = 1 line, at HIP's default queues."""
 
@@ -728,8 +730,9 @@ def shard_one_in_flight(ops, s, torch, hoh_ans, n=5):
 
 def sharded_leg(args, W, H, D, B, K, warm, seed0, rank, world, dev, torch, hoh_ans, hd, one_in_flight=False):
     """One N > 1 leg (or its one-rank rehearsal, --sharded): returns a dict of its numbers; on
-    rank 0 the gathered file of slot 0's first image (seed seed0) is hashed, and every slot's
-    images' files of their last step against the reference choh's SHAs where known."""
+    rank 0 the SHA of slot 0's first image's gathered file (seed seed0) is reported, and every slot's
+    images' files of their last step against the reference choh's SHAs where known (each file is
+    assembled on its root rank, hoh_ans.dist.BatchGather, and hashed there)."""
     import numpy as np
     import torch.distributed as dist
     ops = GpuShardOps(args, W, H, seed0, rank, world, dev, torch, hoh_ans, hd, max(K, warm, D), B)
@@ -751,13 +754,17 @@ def sharded_leg(args, W, H, D, B, K, warm, seed0, rank, world, dev, torch, hoh_a
     n_rank = int(slots[0].sizes_host.numpy().astype(np.int64)[:ops.nt].sum())
     nn = torch.tensor([n_rank], dtype=torch.int64, device=dev)
     dist.all_reduce(nn)
-    sha, shas = None, {}
-    if rank == 0:      # every slot's files of its last step: header + tile table + every rank's blob
-        for s in slots:
-            g = s.gather
-            for b, sd in enumerate(s.seeds):
-                shas[sd] = hashlib.sha256(g.files[b, :g.totals[b]].cpu().numpy().tobytes()).hexdigest()
-        sha = shas[seed0]
+    # every slot's files of its last step (header + tile table + every rank's blob), hashed on the
+    # rank that assembled each (image b of a slot on rank b % world), collected on every rank
+    mine = {}
+    for s in slots:
+        g = s.gather
+        for b in g.own:
+            mine[s.seeds[b]] = hashlib.sha256(g.files[g.row(b), :g.totals[b]].cpu().numpy().tobytes()).hexdigest()
+    allh = [None] * world
+    dist.all_gather_object(allh, mine)
+    shas = {k: v for d in allh for k, v in d.items()}
+    sha = shas.get(seed0)
     res = {"el": el, "K": K, "D": D, "B": B, "lossless": lossless, "t_enc": t_enc, "t_dec": t_dec,
            "comp_total": int(nn.item()), "sha": sha, "shas": shas, "stats": stats, "rows": ops.rows,
            "iso": iso, "iso_dom_ms_max": iso_dom if iso else None, "iso_same_bytes": iso_same,
@@ -994,10 +1001,10 @@ def sharded_main(args, D, B, world, rank, dev, torch, hoh_ans, hd):
         gw = golden_speed_sha(W, H, seed0, args.noise) if args.strong else None
         if gw is None:
             gw = golden_sha(W, H, seed0, args.noise)
-        gb = golden_bench_shas(W, H, args.noise) if (W, H) == (8192, 8192) else {}
+        gb = dict(golden_bench_shas(W, H, args.noise))  # 8192^2 seeds 1..40; 8192 x 8192N seeds 1..4
         if gw is not None:
-            gb = dict(gb)
             gb[seed0] = gw
+        gw = gb.get(seed0)
         checked = {sd: (h == gb[sd]) for sd, h in p["shas"].items() if sd in gb}
         detail = {
             "slots": D,
@@ -1032,7 +1039,7 @@ def sharded_main(args, D, B, world, rank, dev, torch, hoh_ans, hd):
                 "strong_16384_bit_exact_vs_reference": (strong["sha"] == g) if g else None,
                 "strong_16384_note": "BASELINE configs[3]: 16384x16384 images (slot 0's first: seed %d) sharded over "
                                      "the %d rank(s) (strong scaling), %d slots x %d images per step, RCCL gather of "
-                                     "the sub-bitstreams to rank 0; sha256 of rank 0's gathered file against the "
+                                     "the sub-bitstreams to each image's root rank; sha256 of the gathered file against the "
                                      "reference choh's (golden_speed.json)"
                                      % (STRONG_SEED, world, strong["D"], strong["B"]),
             })
@@ -1057,7 +1064,8 @@ def sharded_main(args, D, B, world, rank, dev, torch, hoh_ans, hd):
                              % (W, H, args.noise, seed0, seed0 + D * Bp - 1,
                                 "side index" if not args.no_index else "serial decode", D, Bp, hw_queue_note())),
                 "W": W, "H": H, "tiles": (W // 256) * (H // 256), "per_gpu": "%dx%d" % (W, p["rows"]), "batch": Bp,
-                "parallelism": "tile rows sharded over %d GPU(s), RCCL gather to rank 0" % world,
+                "parallelism": "tile rows sharded over %d GPU(s), RCCL gather of each image's shards to its "
+                               "root rank (image b of a step on rank b %% N)" % world,
             },
             "roofline": roof,
             "detail": detail,

@@ -473,6 +473,7 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   j.dbg = (uint32_t*)c->dbg.p;
   if (hipMemsetAsync(j.dbg, 0, (size_t)ntiles * 64 * 4, s) != hipSuccess) return HOH_E_HIP;
 #endif
+  j.exp = (uint32_t)HOH_KNOB(EXP, 0);   // measurement what-ifs (tools/scripts): 0 in the product
   j.gerr = (uint32_t*)c->misc.p;
   j.total = (uint64_t*)((uint8_t*)c->misc.p + 8);
   j.ntrial = (uint32_t*)((uint8_t*)c->misc.p + 16);

@@ -219,6 +219,7 @@ struct EncodeJob {
   Checkpoint* ckpt;
   uint32_t* gerr;         // global error word
   uint32_t* dbg;          // measurement builds only (HOH_DEBUG_READ): [tile][64] counters, else null
+  uint32_t exp;           // measurement what-ifs (knob EXP, knob builds only; 0 in the product): output invalid
   uint64_t* total;        // total bytes of the tile blob
   uint32_t* tile_sizes;   // out: per tile bytes (may be null)
   uint8_t* out;           // output: [prefix bytes][tile size table][tiles]

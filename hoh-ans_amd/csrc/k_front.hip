@@ -538,7 +538,7 @@ __global__ __launch_bounds__(NT) void k_front256(EncodeJob j) {
   uint64_t* cand = j.candbits + (size_t)t * (j.npix_cap / 64);
   const uint8_t* img = j.rgb + ((size_t)y0 * j.W + x0) * 3;
   const size_t pitch = (size_t)j.W * 3;
-  const bool lz = j.speed == 0;
+  const bool lz = j.speed == 0 && !(j.exp & 2);     // what-if EXP & 2 (measurement): no LZ screen
   uint32_t* ring = pring[wv];
   // pixel (x = 64k + lane, y) of the tile: one unaligned dword that never leaves the tile (x = 0
   // reads its own 3 bytes + the next pixel's first, others the previous pixel's last byte + theirs)

@@ -210,7 +210,9 @@ __device__ __forceinline__ void rans_fast_body(const EncodeJob& j, int nplane, S
   const uint32_t n = st.n;
   const PbShape g{31u - st.pb, 1u << st.pb, 32u - st.pb};
   const char* tb = (const char*)j.tab_fast;
-  const uint32_t tbase = sid * (uint32_t)(HOH_FAST_RANGE * sizeof(EncFast));
+  // what-if EXP & 1 (measurement, output invalid): the 64 lanes' tables of block 0 for every
+  // wave, so every table gather hits L2
+  const uint32_t tbase = ((j.exp & 1) ? (uint32_t)lane : sid) * (uint32_t)(HOH_FAST_RANGE * sizeof(EncFast));
   Coder c;
   c.xh = 0; c.xl = 1u << 31; c.mask = 0; c.slot = 0;
   c.slab = j.slabs + st.slab_off;

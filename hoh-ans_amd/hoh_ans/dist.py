@@ -117,15 +117,29 @@ class BatchGather:
     same band of B images per step, hoh_encode_tiles_images_async).  Blob i of this rank lies at
     blob[i*stride:]; tile_sizes is a (B, ntiles) array of this rank's tile sizes.  ONE all_gather
     carries all B images' tile sizes, then ONE batch of point-to-point operations moves every
-    (rank, image) blob straight into its place in image i's file on rank 0 (row i of `files`,
-    behind hoh_file_prefix).  Returns (files, totals, requests) on rank 0 -- files is a (B, cap)
-    uint8 tensor, totals the B file sizes -- and (None, [0]*B, requests) elsewhere; with wait=True
-    the requests are waited on and the third element is omitted."""
+    (rank, image) blob straight into its place in image i's file behind hoh_file_prefix.
+
+    Image i's file is assembled on its root rank root(i) = i % world (every image is still one
+    gather of its sub-bitstreams): with B >= world each rank roots B / world files, so the blobs of
+    a step spread over all the xGMI links instead of converging on rank 0's (at N = 8 that is an
+    eighth of the bytes per link).  After a call: `own` lists the images this rank roots, `files`
+    holds their files (row k = image own[k]) and `totals[i]` the size of every file (all ranks
+    know them).  Returns (files, totals, requests) -- files None on a rank that roots nothing --
+    or, with wait=True, (files, totals) after waiting."""
 
     def __init__(self, W, H, B, device, group=None):
         self.W, self.H, self.B, self.device, self.group = W, H, B, device, group
         self.files = None
         self.totals = [0] * B
+        self.own = []
+
+    @staticmethod
+    def root(i, world):
+        return i % world
+
+    def row(self, i):
+        """row of image i in `files` (this rank must root it)"""
+        return self.own.index(i)
 
     def __call__(self, blob, stride, tile_sizes, wait=True):
         import torch
@@ -144,39 +158,43 @@ class BatchGather:
         if max(bsz[rank]) > stride:
             raise RuntimeError("a blob is larger than the stride")
         ranks = dist.get_process_group_ranks(self.group) if self.group is not None else list(range(world))
-        if rank != 0:
-            ops = [dist.P2POp(dist.isend, blob[i * stride:i * stride + bsz[rank][i]], ranks[0], self.group)
-                   for i in range(B) if bsz[rank][i]]
-            reqs = dist.batch_isend_irecv(ops) if ops else []
-            if wait:
-                for q in reqs:
-                    q.wait()
-                return None, [0] * B
-            return None, [0] * B, reqs
-        prefixes = [file_prefix(self.W, self.H, np.concatenate([per[r][i] for r in range(world)])) for i in range(B)]
+        self.own = [i for i in range(B) if self.root(i, world) == rank]
+        prefixes = {i: file_prefix(self.W, self.H, np.concatenate([per[r][i] for r in range(world)]))
+                    for i in range(B)}
         totals = [len(prefixes[i]) + sum(bsz[r][i] for r in range(world)) for i in range(B)]
-        need = max(totals)
-        if self.files is None or self.files.shape[1] < need:
-            self.files = torch.empty((B, need + need // 16), dtype=torch.uint8, device=self.device)
+        files = None
+        if self.own:
+            need = max(totals[i] for i in self.own)
+            if self.files is None or self.files.shape[0] < len(self.own) or self.files.shape[1] < need:
+                self.files = torch.empty((len(self.own), need + need // 16), dtype=torch.uint8, device=self.device)
+            files = self.files
         ops = []
         for i in range(B):
+            rt = self.root(i, world)
+            if rt != rank:
+                if bsz[rank][i]:
+                    ops.append(dist.P2POp(dist.isend, blob[i * stride:i * stride + bsz[rank][i]], ranks[rt],
+                                          self.group))
+                continue
+            k = self.own.index(i)
             pl = len(prefixes[i])
-            self.files[i, :pl] = torch.frombuffer(bytearray(prefixes[i]), dtype=torch.uint8).to(self.device)
-            off = pl + bsz[0][i]
-            for r in range(1, world):
-                if bsz[r][i]:
-                    ops.append(dist.P2POp(dist.irecv, self.files[i, off:off + bsz[r][i]], ranks[r], self.group))
+            files[k, :pl] = torch.frombuffer(bytearray(prefixes[i]), dtype=torch.uint8).to(self.device)
+            off = pl
+            for r in range(world):
+                if r != rank and bsz[r][i]:
+                    ops.append(dist.P2POp(dist.irecv, files[k, off:off + bsz[r][i]], ranks[r], self.group))
                 off += bsz[r][i]
         reqs = dist.batch_isend_irecv(ops) if ops else []
-        for i in range(B):
-            pl = len(prefixes[i])
-            self.files[i, pl:pl + bsz[0][i]] = blob[i * stride:i * stride + bsz[0][i]]
+        for i in self.own:                      # this rank's own blob of the images it roots
+            k = self.own.index(i)
+            off = len(prefixes[i]) + sum(bsz[r][i] for r in range(rank))
+            files[k, off:off + bsz[rank][i]] = blob[i * stride:i * stride + bsz[rank][i]]
         self.totals = totals
         if not wait:
-            return self.files, totals, reqs
+            return files, totals, reqs
         for q in reqs:
             q.wait()
-        return self.files, totals
+        return files, totals
 
 
 def run_pipeline(nslots, total, enqueue, finish):

@@ -3,7 +3,9 @@ oracle/ref/Makefile) on the deterministic 8192^2 synthetic image of each seed be
 flight (seeds 1..40, noise 4: slot k holds seed 1 + k, or seeds 1 + k*B .. with --batch B).  bench.py compares every slot's file
 with these after the timed region.  ~7 s per seed on one core (run in parallel here).
 
-    python tests/golden/make_golden_bench.py [--size S] [--seeds A B] [--jobs J]   (needs /root/reference)
+    python tests/golden/make_golden_bench.py [--size S] [--height H] [--seeds A B] [--jobs J]   (needs /root/reference)
+
+--height (default S) makes the weak-scaling images of bench.py's N > 1 line (8192 x 8192 N).
 """
 import argparse
 import hashlib
@@ -25,12 +27,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--size", type=int, default=8192)
     ap.add_argument("--seeds", type=int, nargs=2, default=[1, 20])
+    ap.add_argument("--height", type=int, default=0)
     ap.add_argument("--noise", type=int, default=4)
     ap.add_argument("--jobs", type=int, default=6)
     a = ap.parse_args()
     exe = O.ref_bin("choh")
     assert exe, "reference choh not built (oracle/ref/Makefile)"
-    W = H = a.size
+    W = a.size
+    H = a.height or a.size
     d = tempfile.mkdtemp(dir="/tmp")
 
     def one(seed):
@@ -50,9 +54,10 @@ def main():
         recs = list(ex.map(one, range(a.seeds[0], a.seeds[1] + 1)))
     path = os.path.join(HERE, "golden_bench.json")
     out = json.load(open(path)) if os.path.exists(path) else {"files": []}
-    keys = {(r["spec"]["W"], r["spec"]["seed"], r["spec"]["noise"]) for r in recs}
-    out["files"] = [f for f in out["files"] if (f["spec"]["W"], f["spec"]["seed"], f["spec"]["noise"]) not in keys] + recs
-    out["files"].sort(key=lambda f: (f["spec"]["W"], f["spec"]["seed"]))
+    key = lambda f: (f["spec"]["W"], f["spec"]["H"], f["spec"]["seed"], f["spec"]["noise"])  # noqa: E731
+    keys = {key(r) for r in recs}
+    out["files"] = [f for f in out["files"] if key(f) not in keys] + recs
+    out["files"].sort(key=key)
     out["generator"] = "tests/golden/make_golden_bench.py (reference choh built by oracle/ref/Makefile)"
     json.dump(out, open(path, "w"), indent=1)
     for r in recs:

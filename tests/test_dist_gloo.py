@@ -254,9 +254,9 @@ class _BatchCpuShardOps(_CpuShardOps):
         for q in res[2]:
             q.wait()
         self.log.append(i)
-        if self.rank == 0:
-            s["files"] = [res[0][b, :res[1][b]].numpy().tobytes() for b in range(self.B)]
-            s["ok"] = s["ok"] and all(np.array_equal(oracle.dhoh(f), img) for f, img in zip(s["files"], s["imgs"]))
+        g = s["g"]                                  # image b's file is assembled on rank b % world
+        s["files"] = {b: res[0][g.row(b), :res[1][b]].numpy().tobytes() for b in g.own}
+        s["ok"] = s["ok"] and all(np.array_equal(oracle.dhoh(f), s["imgs"][b]) for b, f in s["files"].items())
 
 
 def _batch_leg_worker(rank, world, port, outdir):
@@ -270,19 +270,19 @@ def _batch_leg_worker(rank, world, port, outdir):
         slots, el, ok = hd.run_sharded_leg(ops, 2, 3, 1)
         assert ok and el > 0
         assert ops.log == [0, 1, 2]
-        if rank == 0:
-            for s in slots:
-                for sd, f in zip(s["seeds"], s["files"]):
-                    with open(os.path.join(outdir, "batch_seed%d.hoh" % sd), "wb") as fh:
-                        fh.write(f)
+        for s in slots:                             # every rank writes the files it roots
+            for b, f in s["files"].items():
+                with open(os.path.join(outdir, "batch_seed%d.hoh" % s["seeds"][b]), "wb") as fh:
+                    fh.write(f)
         dist.barrier()
     finally:
         dist.destroy_process_group()
 
 
 def test_gloo_batched_sharded_leg(tmp_path):
-    """bench.py's batched N > 1 schedule on two gloo ranks: 2 slots x 2 images, BatchGather;
-    every image's gathered file equals the single-process choh -s0 file and decodes losslessly"""
+    """bench.py's batched N > 1 schedule on two gloo ranks: 2 slots x 2 images, BatchGather (image
+    b of a slot assembled on rank b % 2); every image's gathered file equals the single-process
+    choh -s0 file and decodes losslessly"""
     world = 2
     mp.spawn(_batch_leg_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     for seed in (40, 41, 42, 43):

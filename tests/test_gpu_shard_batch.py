@@ -165,3 +165,15 @@ def test_default_stream_fences(hoh):
             assert hashlib.sha256(got[i * stride:i * stride + n].cpu().numpy().tobytes()).hexdigest() == want[sd]
         assert all(int(x) == 0 for x in ds.cpu().numpy()[0::2]) and same, rep
     ctx.close()
+
+
+def test_weak_scaling_image_golden(hoh):
+    """bench.py's N = 2 weak-scaling image (8192 x 16384, seed 1) as 2 batched shards of 2 images
+    (seeds 1, 2): the assembled files equal the reference choh's (golden_bench.json, made by
+    make_golden_bench.py --height 16384)"""
+    g = json.load(open(os.path.join(HERE, "golden", "golden_bench.json")))
+    want = {r["spec"]["seed"]: (r["out"]["len"], r["out"]["sha256"]) for r in g["files"]
+            if (r["spec"]["W"], r["spec"]["H"], r["spec"]["noise"], r["spec"]["speed"]) == (8192, 16384, 4, 0)}
+    files = _run(hoh, 8192, 16384, 2, [1, 2], False)
+    for sd, f in zip((1, 2), files):
+        assert (len(f), hashlib.sha256(f).hexdigest()) == want[sd], sd
