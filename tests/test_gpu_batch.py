@@ -76,7 +76,7 @@ def test_batch_8192_vs_reference_goldens(hoh):
     import torch
     g = json.load(open(os.path.join(HERE, "golden", "golden_bench.json")))
     want = {r["spec"]["seed"]: (r["out"]["len"], r["out"]["sha256"]) for r in g["files"]
-            if (r["spec"]["W"], r["spec"]["noise"], r["spec"]["speed"]) == (8192, 4, 0)}
+            if (r["spec"]["W"], r["spec"]["H"], r["spec"]["noise"], r["spec"]["speed"]) == (8192, 8192, 4, 0)}
     seeds = [1, 2, 3, 4]
     ctx = hoh.Context(0)
     W = H = 8192

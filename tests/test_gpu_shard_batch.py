@@ -88,7 +88,7 @@ def test_batched_shards_8192_vs_reference_goldens(hoh):
     """4 ranks x a batch of 3 bench seeds at 8192^2: assembled files == the reference choh's"""
     g = json.load(open(os.path.join(HERE, "golden", "golden_bench.json")))
     want = {r["spec"]["seed"]: (r["out"]["len"], r["out"]["sha256"]) for r in g["files"]
-            if (r["spec"]["W"], r["spec"]["noise"], r["spec"]["speed"]) == (8192, 4, 0)}
+            if (r["spec"]["W"], r["spec"]["H"], r["spec"]["noise"], r["spec"]["speed"]) == (8192, 8192, 4, 0)}
     seeds = [5, 6, 7]
     files = _run(hoh, 8192, 8192, 4, seeds, True)
     for sd, f in zip(seeds, files):
@@ -141,7 +141,7 @@ def test_default_stream_fences(hoh):
     W = H = 8192
     g = json.load(open(os.path.join(HERE, "golden", "golden_bench.json")))
     want = {r["spec"]["seed"]: r["out"]["sha256"] for r in g["files"]
-            if (r["spec"]["W"], r["spec"]["noise"], r["spec"]["speed"]) == (8192, 4, 0)}
+            if (r["spec"]["W"], r["spec"]["H"], r["spec"]["noise"], r["spec"]["speed"]) == (8192, 8192, 4, 0)}
     ctx = hoh.Context(0)
     stride = hoh.lib().hoh_encode_bound(W, H)
     img = W * H * 3

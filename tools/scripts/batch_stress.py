@@ -28,7 +28,7 @@ img = W * H * 3
 L = hoh.lib()
 stride = L.hoh_encode_bound(W, H)
 g = json.load(open(os.path.join(ROOT, "tests", "golden", "golden_bench.json")))
-gold = {r["spec"]["seed"]: r["out"]["sha256"] for r in g["files"] if (r["spec"]["W"], r["spec"]["noise"]) == (8192, 4)}
+gold = {r["spec"]["seed"]: r["out"]["sha256"] for r in g["files"] if (r["spec"]["W"], r["spec"]["H"], r["spec"]["noise"]) == (8192, 8192, 4)}
 
 
 class Slot:
