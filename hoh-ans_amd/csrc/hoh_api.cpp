@@ -404,6 +404,12 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   if (speed) {
     nsym = sym_total_s(ntiles, j.npix_cap, j.lz_cap);
     nslab = slab_total_s(ntiles, j.npix_cap, j.lz_cap);
+    // the trial pool (EncodeJob::tpool_*): half a plane's words per plane -- a kept trial takes
+    // its word bound (k_tables' whi), a compressed plane ~1/4 of that; when it runs out the
+    // remaining trials count only and their winners are encoded again (same bytes)
+    j.tpool_off = nslab;
+    j.tpool_words = HOH_KNOB(TRIAL_POOL, 1) ? (size_t)ntiles * HOH_NPLANE_S * (j.npix_cap / 2) : 0;
+    nslab += j.tpool_words;
   }
   const size_t nck = speed ? 1 : S * (j.npix_cap / HOH_SEG + 2);
   int e = HOH_OK;
@@ -477,6 +483,7 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   j.gerr = (uint32_t*)c->misc.p;
   j.total = (uint64_t*)((uint8_t*)c->misc.p + 8);
   j.ntrial = (uint32_t*)((uint8_t*)c->misc.p + 16);
+  j.tpool_head = (unsigned long long*)((uint8_t*)c->misc.p + 24);
   j.tile_sizes = d_tile_sizes;
   j.out = d_out;
   j.cap = cap;

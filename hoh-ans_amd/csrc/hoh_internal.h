@@ -88,7 +88,9 @@ struct StreamInfo {
   uint32_t ckpt_off;      // index of the first checkpoint of this stream
   uint32_t drop;          // coded but not part of the file (losing colour mode)
   uint32_t clip;          // nonzero: only the first clip bytes go to the file (Q15 prefix)
-  uint32_t sizeonly;      // rANS state chain only: words counted, none stored (2: pruned, words = wlo)
+  uint32_t sizeonly;      // rANS state chain only: words counted, none stored (2: pruned, words = wlo;
+                          //   3: a kept trial that stores its words in the trial pool; 4: the
+                          //   layer's final stream whose words a stored trial already holds)
   uint32_t hist_src;      // 0: count the symbols; k + 1: the histogram of stream k
   uint32_t wlo, whi;      // size-only trials: bounds on words (k_tables, from the code length)
 };
@@ -220,6 +222,11 @@ struct EncodeJob {
   uint32_t* gerr;         // global error word
   uint32_t* dbg;          // measurement builds only (HOH_DEBUG_READ): [tile][64] counters, else null
   uint32_t exp;           // measurement what-ifs (knob EXP, knob builds only; 0 in the product): output invalid
+  // -s>=1: the ladder trials k_prune_s keeps that could win the layer (KS_VAR + p*8 + 2..7) store
+  // their words in a pool of the slab arena (sizeonly 3), so the winner is not encoded a second
+  // time: words [tpool_off, tpool_off + tpool_words) of slabs, bump-allocated through *tpool_head
+  uint64_t tpool_off, tpool_words;
+  unsigned long long* tpool_head;
   uint64_t* total;        // total bytes of the tile blob
   uint32_t* tile_sizes;   // out: per tile bytes (may be null)
   uint8_t* out;           // output: [prefix bytes][tile size table][tiles]

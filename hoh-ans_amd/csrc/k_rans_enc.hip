@@ -68,15 +68,22 @@ struct Coder {
   uint32_t widx;
   uint32_t* slab;
   uint32_t* win;
+  uint32_t lost;          // trials (KIND 3): words not written (size-only lanes: all of them;
+                          //   storing lanes: any past the slab's start), counted
+  bool keep;              // trials (KIND 3): this lane stores its words
 };
 
-// copy the window's emitted words to the slab (backwards, rans64 order)
+// copy the window's emitted words to the slab (backwards, rans64 order); GUARD (stored ladder
+// trials, whose slab is sized by the word bound): a word that would land before the slab's start
+// is counted in c.lost instead of written
+template <bool GUARD = false>
 __device__ __forceinline__ void flush_win(Coder& c) {
   uint32_t m = c.mask;
   const uint32_t shift = WIN - c.slot;
   while (m) {
     const uint32_t t = __builtin_clz(m) - shift;
-    c.slab[--c.widx] = c.win[t];
+    if (!GUARD || (c.keep && c.widx)) c.slab[--c.widx] = c.win[t];
+    else c.lost++;
     m &= ~(0x80000000u >> (t + shift));
   }
   c.mask = 0;
@@ -164,7 +171,9 @@ __device__ __forceinline__ void stepg(Coder& c, const EncFast& e, const PbShape&
   if (!SO) c.slot++;
 }
 
-// KIND 0: prob_bits 15 (step15); 1: any prob_bits 12..19; 2: the same, size only
+// KIND 0: prob_bits 15 (step15); 1: any prob_bits 12..19; 2: the same, size only; 3: the ladder
+// trials of one launch (KIND 1's steps; a lane stores its words when its trial holds a pool slab,
+// sizeonly 3, and only counts them otherwise -- one instruction stream for both kinds of lane)
 template <int KIND>
 __device__ __forceinline__ void stepk(Coder& c, const EncFast& e, const PbShape& g) {
   if (KIND == 0) step15(c, e);
@@ -178,10 +187,12 @@ __device__ __forceinline__ void ckpt(const Coder& c, Checkpoint* ck, uint32_t k)
   ck[k] = p;
 }
 
+template <int KIND>
+__device__ __forceinline__ void rans_fast_run(const EncodeJob& j, uint32_t sid, const StreamInfo& st);
+
 // One lane per stream, 64 streams per wave, one wave per workgroup: block blk of a launch.
 template <int KIND>
 __device__ __forceinline__ void rans_fast_body(const EncodeJob& j, int nplane, SidMap ma, int na, SidMap mb, int blk) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int lane = threadIdx.x;
   // the chain is the critical path of an image: win issue arbitration against co-resident waves
 #ifndef CHAIN_PRIO
@@ -207,6 +218,17 @@ __device__ __forceinline__ void rans_fast_body(const EncodeJob& j, int nplane, S
   // size-only trial
   if ((KIND == 2) != (st.sizeonly != 0) || (KIND != 2 && (KIND == 0) != (st.pb == 15))) return;
   if (st.sizeonly == 2) return;            // pruned trial (k_prune_s): its words are set
+  // trials: the storing chain for every lane when the pool is on (storing and counting lanes share
+  // a wave: two kinds of chain in one wave would run one after the other)
+  if (KIND == 2 && j.tpool_words) rans_fast_run<3>(j, sid, st);
+  else rans_fast_run<KIND>(j, sid, st);
+}
+
+template <int KIND>
+__device__ __forceinline__ void rans_fast_run(const EncodeJob& j, uint32_t sid, const StreamInfo& st) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  constexpr bool GUARD = KIND == 3;
+  const int lane = threadIdx.x;
   const uint32_t n = st.n;
   const PbShape g{31u - st.pb, 1u << st.pb, 32u - st.pb};
   const char* tb = (const char*)j.tab_fast;
@@ -214,16 +236,18 @@ __device__ __forceinline__ void rans_fast_body(const EncodeJob& j, int nplane, S
   // wave, so every table gather hits L2
   const uint32_t tbase = ((j.exp & 1) ? (uint32_t)lane : sid) * (uint32_t)(HOH_FAST_RANGE * sizeof(EncFast));
   Coder c;
-  c.xh = 0; c.xl = 1u << 31; c.mask = 0; c.slot = 0;
-  c.slab = j.slabs + st.slab_off;
-  c.widx = st.slab_cap;
+  c.xh = 0; c.xl = 1u << 31; c.mask = 0; c.slot = 0; c.lost = 0;
+  c.keep = !GUARD || st.sizeonly == 3;
+  const uint32_t cap = c.keep ? st.slab_cap : 0u;
+  c.slab = j.slabs + (c.keep ? st.slab_off : 0);
+  c.widx = cap;
   c.win = (uint32_t*)(lds + threadIdx.x * WIN_PITCH * 4);
   Checkpoint* ck = j.ckpt ? j.ckpt + st.ckpt_off : nullptr;
   const uint16_t* sp = j.sym + st.sym_off;
   // prologue: the top n % 32 symbols one at a time (descending); the rest is whole windows
   const uint32_t r = n & 31, nb = (n - r) / 8;   // nb 8-symbol blocks, a multiple of 4
   for (uint32_t i = n; i > n - r; i--) stepk<KIND>(c, ent(tb, tbase + (uint32_t)sp[i - 1] * 16u), g);
-  if (KIND != 2) flush_win(c);
+  if (KIND != 2) flush_win<GUARD>(c);
   if (((nb * 8) % HOH_SEG) == 0 && nb * 8 < n) ckpt(c, ck, nb * 8 / HOH_SEG);
   if (nb) {
     // table entries gathered 16 steps ahead (two 8-symbol blocks per buffer): with several images
@@ -256,7 +280,7 @@ __device__ __forceinline__ void rans_fast_body(const EncodeJob& j, int nplane, S
       if (p >= 2) { look(eA, h, l); if (p >= 3) syms(p - 3, h, l); }
       run(eB, p - 1);
       if (p >= 3) { look(eB, h, l); if (p >= 4) syms(p - 4, h, l); }
-      if (KIND != 2) flush_win(c);
+      if (KIND != 2) flush_win<GUARD>(c);
     }
   }
   if (KIND == 2) {                         // size only: the emitted words + the two flushed ones
@@ -264,10 +288,18 @@ __device__ __forceinline__ void rans_fast_body(const EncodeJob& j, int nplane, S
     j.streams[sid].widx_end = 0;
     return;
   }
-  flush_win(c);
+  flush_win<GUARD>(c);
+  if (GUARD && (!c.keep || c.lost || c.widx < 2)) {
+    // a counting lane, or a storing one whose bound failed (counted only: its winner is encoded
+    // again); the emitted words + the two flushed ones
+    j.streams[sid].words = cap - c.widx + c.lost + 2;
+    j.streams[sid].widx_end = 0;
+    if (c.keep) j.streams[sid].sizeonly = 1;
+    return;
+  }
   c.slab[--c.widx] = c.xh;                 // Rans64EncFlush: lo at the lower address
   c.slab[--c.widx] = c.xl;
-  j.streams[sid].words = st.slab_cap - c.widx;
+  j.streams[sid].words = cap - c.widx;
   j.streams[sid].widx_end = c.widx;
 }
 

@@ -1907,8 +1907,23 @@ __global__ __launch_bounds__(64) void k_prune_s(EncodeJob j) {
       if (lo[ks[a]] <= U) need |= 1u << ks[a];
   }
   for (int k = 0; k < 8; k++) {
-    if ((need >> k) & 1) j.trials[atomicAdd(j.ntrial, 1u)] = (uint32_t)(t * SPT_S + KS_VAR + p * 8 + k);
-    else { v[k].sizeonly = 2; v[k].words = v[k].wlo; }
+    if ((need >> k) & 1) {
+      j.trials[atomicAdd(j.ntrial, 1u)] = (uint32_t)(t * SPT_S + KS_VAR + p * 8 + k);
+      // a trial that can become the layer's final stream (k >= 2, k_choose_s) stores its words
+      // in the trial pool when there is room: whi bounds them (k_tables; tests/
+      // test_gpu_check_build.py), and the chain stops storing, never writes, past the slab
+      if (k >= 2 && j.tpool_words) {
+        const uint64_t cap = (uint64_t)v[k].whi + 64;
+        const uint64_t o = atomicAdd(j.tpool_head, (unsigned long long)cap);
+        if (o + cap <= j.tpool_words) {
+          v[k].slab_off = j.tpool_off + o;
+          v[k].slab_cap = (uint32_t)cap;
+          v[k].sizeonly = 3;
+        }
+      }
+    } else {
+      v[k].sizeonly = 2; v[k].words = v[k].wlo;
+    }
   }
 #ifdef HOH_DEBUG_READ
   if (j.dbg) atomicAdd(&j.dbg[(size_t)t * 64 + 40 + __popc(need)], 1u);   // planes by trials kept (lzscan_stats.py)
@@ -1926,17 +1941,17 @@ __global__ __launch_bounds__(64) void k_choose_s(EncodeJob j) {
   const StreamInfo* st = j.streams + (size_t)t * SPT_S;
   const uint64_t n = (uint64_t)ti.w * ti.h;
   uint64_t possible = (pi.depth * n + (pi.depth * n) % 8 + 1024) / 8;
-  uint32_t valid = 0, fin = 0, fin_pb = 0;
+  uint32_t valid = 0, fin = 0, fin_pb = 0, fin_k = 0;
   const uint64_t sm = st[KS_MED + p].size;
   if (sm < possible) { possible = sm; valid = 1; }
   const StreamInfo* v = st + KS_VAR + p * 8;
   const uint64_t t1 = v[0].size, t2 = v[1].size;
   if (t1 < t2) {
     if (t1 < possible) possible = t1;                                 // not swapped (Q14)
-    for (int k = 2; k < 5; k++) if (v[k].size < possible) { possible = v[k].size; valid = 1; fin = 1; fin_pb = v[k].pb; }
+    for (int k = 2; k < 5; k++) if (v[k].size < possible) { possible = v[k].size; valid = 1; fin = 1; fin_pb = v[k].pb; fin_k = k; }
   } else {
     if (t2 < possible) possible = t2;
-    for (int k = 5; k < 8; k++) if (v[k].size < possible) { possible = v[k].size; valid = 1; fin = 1; fin_pb = v[k].pb; }
+    for (int k = 5; k < 8; k++) if (v[k].size < possible) { possible = v[k].size; valid = 1; fin = 1; fin_pb = v[k].pb; fin_k = k; }
   }
   pi.possible = (uint32_t)possible;
   pi.valid = valid;
@@ -1951,6 +1966,13 @@ __global__ __launch_bounds__(64) void k_choose_s(EncodeJob j) {
     f.slab_off = plane_slab_off_s(j, t, p);                          // the MED stream's slab: unused now
     f.slab_cap = j.npix_cap + 8;
     f.mode = SM_EMPTY; f.words = 0; f.size = 0; f.err = 0; f.fast = 1;   // k_tables decides
+    const StreamInfo& w = v[fin_k];
+    if (w.sizeonly == 3) {
+      // the winning trial stored its words: the same symbols, prob_bits and table, so they are
+      // this stream's words (the final chain launch skips it; k_tables rebuilds the header)
+      f.slab_off = w.slab_off; f.slab_cap = w.slab_cap; f.words = w.words; f.widx_end = w.widx_end;
+      f.sizeonly = 4;
+    }
     j.streams[(size_t)t * SPT_S + KS_FIN + p] = f;
   }
 }

@@ -4,7 +4,7 @@
 # hit: 64 shared tables), 2 (no LZ screen in k_front256), 3 (both).  ms/image, encode / both.
 set -e
 cd "$(dirname "$0")/../.."
-for e in 0 1 2 3; do
+for e in ${EXPS:-0 1 2 3}; do
   echo "EXP=$e"
   HOH_LIB=hoh-ans_amd/lib/libhohgpu_check.so HOH_EXP=$e HOH_QUIET=1 timeout -k 10 120 \
     python3 tools/scripts/batch_pipe.py 4 8 40 enc,both
