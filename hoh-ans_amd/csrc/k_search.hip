@@ -1553,10 +1553,12 @@ void k_lzscan(EncodeJob j, int limit, int rp, int nseg_req, int hls) {
       const uint32_t b = 1 + 64 * c + lane;
       fv[c] = b <= bm && !post ? F[q - b] : 0u;
     }
+    // what-if EXP & 16 (measurement, output invalid): no vertical search
+    const uint32_t kmv = (j.exp & 16) ? 0u : kmax;
 #pragma unroll
     for (int c = 0; c < LZS_VB; c++) {
       const uint32_t k = 1 + 64 * c + lane;
-      fw[c] = k <= kmax && k * w > bm ? FT[cbase - k] : 0u;           // FT[x * h + y - k] = F[q - k * w]
+      fw[c] = k <= kmv && k * w > bm ? FT[cbase - k] : 0u;            // FT[x * h + y - k] = F[q - k * w]
     }
     if (rp) fill_to(q >= reach ? q - reach : 0u, q + 260);
     // horizontal: b = 1 .. min(limit, q), longest first, then the smallest b.  Each batch's hits
@@ -1664,7 +1666,7 @@ void k_lzscan(EncodeJob j, int limit, int rp, int nseg_req, int hls) {
     [[maybe_unused]] const uint64_t tv0 = LZS_T();
     LZS_DBG(10, (uint32_t)(tv0 - tp0));
     // vertical (lz.hpp:54-74): whole rows up to 65536 back, strictly longer only
-    if ((best >> 17) < 259) {
+    if ((best >> 17) < 259 && kmv) {
       uint32_t vmine = 0;
       auto vchunk = [&](uint32_t k, uint32_t fk) {
         const uint32_t b = k * w;
