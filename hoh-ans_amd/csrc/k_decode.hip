@@ -61,6 +61,7 @@ struct DecJob {
   int blk_ok;                   // plane_cap holds the blocked layout of a 256-wide tile
   int nimg, img_tiles;          // batch (hoh_decode_images_async): nimg files of img_tiles tiles, the
   uint64_t in_stride;           //   image their stack, file i at in + i * in_stride (nimg <= 1: one file)
+  uint32_t exp;                 // measurement what-ifs (knob EXP, knob builds only; 0 in the product)
 };
 
 __device__ __forceinline__ uint64_t rd_varint(const uint8_t* b, uint64_t& p) {
@@ -575,7 +576,7 @@ __global__ __launch_bounds__(DR_T) DRANS_ATTR void k_drans(DecJob j, int nstream
   // dec_abort through the dynamic area (read before the barrier that follows the table clear)
   if (threadIdx.x == 0) wtot[0] = *(volatile const uint32_t*)j.gerr;
   __syncthreads();
-  if (wtot[0]) return;
+  if (wtot[0] || (j.exp & 32)) return;     // what-if EXP & 32 (measurement, output invalid): no rANS decode
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int sid = blockIdx.x;
   const DecStream d = j.streams[sid];
@@ -1664,7 +1665,7 @@ __device__ __forceinline__ void dunpred_fast_tile(const DecJob& j, const DecTile
 
 __global__ __launch_bounds__(64) DUNF_ATTR void k_dunpred_fast(DecJob j) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  if (dec_abort(j)) return;
+  if (dec_abort(j) || (j.exp & 64)) return;   // what-if EXP & 64 (measurement, output invalid)
   const int t = blockIdx.x;
   const DecTile ti = j.tiles[t];
   if (ti.err || !unpred_fast(j, t, ti)) return;
@@ -2634,6 +2635,7 @@ static uint32_t dl_budget() {
 static int dl_wg_per_cu() { return std::max(1, HOH_KNOB(DL_WG, 4)); }
 
 static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s, const AsyncDec* as) {
+  j.exp = (uint32_t)HOH_KNOB(EXP, 0);
   j.npix_cap = (uint32_t)(((size_t)j.tw * j.th + 63) / 64 * 64);
   j.lz_cap = (uint32_t)((j.npix_cap / 4 + j.npix_cap / 255 + 16 + 7) / 8 * 8);
   {
