@@ -557,6 +557,9 @@ __device__ __forceinline__ uint32_t dstep(uint32_t bk, uint32_t sy, uint32_t bma
 #ifndef DRANS_WPE
 #define DRANS_WPE 4
 #endif
+#ifndef DR_LINE
+#define DR_LINE 64    // symbols a thread stores at once (64: a whole 128-B line of its row)
+#endif
 #ifndef DUNF_WPE
 #define DUNF_WPE 0
 #endif
@@ -675,9 +678,11 @@ __global__ __launch_bounds__(DR_T) DRANS_ATTR void k_drans(DecJob j, int nstream
       const uint64_t szal = j.size & ~3ull;
       uint32_t tailw = 0;
       for (uint64_t q = szal; q < j.size; q++) tailw |= (uint32_t)j.in[q] << (8 * (q & 3));
-      auto fetch4 = [&](uint32_t k, uint32_t* o) {           // words k .. k+3
+      // words k .. k+3 as the 5 file dwords that hold them (aligned when they land in the ring, so a
+      // fetch issued a group ahead is not awaited at once: aligning it at issue put the load's
+      // whole latency, and the line stores before it, in front of every group's steps)
+      auto fetch5 = [&](uint32_t k, uint32_t* A) {
         const uint64_t a = (P & ~3ull) + (uint64_t)k * 4;
-        uint32_t A[5];
         if (a + 20 <= szal) {
           typedef uint32_t u4a __attribute__((ext_vector_type(4), aligned(4)));
           const u4a v = *(const u4a*)(j.in + a);
@@ -690,21 +695,19 @@ __global__ __launch_bounds__(DR_T) DRANS_ATTR void k_drans(DecJob j, int nstream
             A[e] = b + 4 <= szal ? *(const uint32_t*)(j.in + b) : (b == szal ? tailw : 0u);
           }
         }
-#pragma unroll
-        for (int e = 0; e < 4; e++) o[e] = __builtin_amdgcn_alignbyte(A[e + 1], A[e], al);
       };
-      auto put4 = [&](uint32_t k, const uint32_t* o) {
+      auto put4 = [&](uint32_t k, const uint32_t* A) {
 #pragma unroll
-        for (int e = 0; e < 4; e++) rg[((k + e) & (DR_RW - 1)) * DR_T] = o[e];
+        for (int e = 0; e < 4; e++) rg[((k + e) & (DR_RW - 1)) * DR_T] = __builtin_amdgcn_alignbyte(A[e + 1], A[e], al);
       };
-      uint32_t fill = wi, pend[4];
+      uint32_t fill = wi, pend[5];
       bool hp = true;                                        // pend holds words fill .. fill+3
       {
-        uint32_t t0[4], t1[4];
-        fetch4(fill, t0); fetch4(fill + 4, t1);
+        uint32_t t0[5], t1[5];
+        fetch5(fill, t0); fetch5(fill + 4, t1);
         put4(fill, t0); put4(fill + 4, t1);
         fill += 8;
-        fetch4(fill, pend);                                  // lands at the first group
+        fetch5(fill, pend);                                  // lands at the first group
       }
       // LDS byte addresses (dynamic area at 0): tables at 0 and 2 * DR_NB * 4, this lane's ring
       // slot s at DR_FIXED + tid*4 + s*1024
@@ -714,19 +717,19 @@ __global__ __launch_bounds__(DR_T) DRANS_ATTR void k_drans(DecJob j, int nstream
       uint4* o4 = d.blk ? (uint4*)(out + (sg >> 6) * BLK_BAND) + (sg & 63) + ((((sg & 63) + 7) >> 3) * 64)
                         : (uint4*)(out + s0);
       const uint32_t ostride = d.blk ? 64u : 1u;
-      for (uint32_t g4 = 0; g4 < DSEG / 64; g4++) {
-        uint32_t pk[32];                                     // 64 symbols: one whole 128-B line
+      for (uint32_t g4 = 0; g4 < DSEG / DR_LINE; g4++) {
+        uint32_t pk[DR_LINE / 2];                            // DR_LINE symbols of the lane's row
 #pragma unroll
-        for (int gi = 0; gi < 4; gi++) {
+        for (int gi = 0; gi < DR_LINE / 16; gi++) {
           // land the words fetched a group ago (fill + 4 - wi <= DR_RW held when they were
           // issued, so no unread word is overwritten)
           if (hp) { put4(fill, pend); fill += 4; }
           while (fill - wi < 8) {                            // a lane that read fast: fetch now
-            uint32_t t[4];
-            fetch4(fill, t); put4(fill, t); fill += 4;
+            uint32_t t[5];
+            fetch5(fill, t); put4(fill, t); fill += 4;
           }
           hp = fill + 4 - wi <= DR_RW;
-          if (hp) fetch4(fill, pend);
+          if (hp) fetch5(fill, pend);
 #pragma unroll
           for (int u = 0; u < 16; u += 2) {
             const uint32_t w0 = lds_u32(DR_FIXED + (t4 | ((wi & (DR_RW - 1)) << 10)));
@@ -739,7 +742,8 @@ __global__ __launch_bounds__(DR_T) DRANS_ATTR void k_drans(DecJob j, int nstream
         // the lane's whole 128-B line at once: 32-B pieces from 64 lanes 512 B apart left
         // partial lines for the memory side (WRITE_SIZE 1.6x the residual bytes)
 #pragma unroll
-        for (int e = 0; e < 8; e++) o4[(8 * g4 + e) * ostride] = make_uint4(pk[4 * e], pk[4 * e + 1], pk[4 * e + 2], pk[4 * e + 3]);
+        for (int e = 0; e < DR_LINE / 8; e++)
+          o4[((DR_LINE / 8) * g4 + e) * ostride] = make_uint4(pk[4 * e], pk[4 * e + 1], pk[4 * e + 2], pk[4 * e + 3]);
       }
       if (xh != (uint32_t)(want >> 32) || xl != (uint32_t)want || wi > d.words) bad = true;
       continue;
