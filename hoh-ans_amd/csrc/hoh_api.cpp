@@ -397,6 +397,8 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   j.gen_stride = 512;
   j.hdr_cap = HOH_HDR_CAP;
   const size_t S = (size_t)ntiles * j.spt;
+  // the chains address every stream's table by a 32-bit offset from one base (k_rans_enc.hip)
+  if (S * HOH_FAST_STRIDE * sizeof(EncFast) > 0xffffffffull) return HOH_E_UNSUPPORTED;
   // arenas: [tile][3] planes, [tile][3] LZ streams, [tile] indexed plane (hoh_internal.h); the
   // -s>=1 layout is in hoh_internal.h too
   size_t nsym = (size_t)ntiles * 3 * (j.npix_cap + j.lz_cap) + (size_t)ntiles * j.npix_cap;
@@ -449,7 +451,7 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   if ((e = ensure(c->streams, S * sizeof(StreamInfo)))) return e;
   if ((e = ensure(c->tiles, (size_t)ntiles * sizeof(TileInfo)))) return e;
   if ((e = ensure(c->hdr, S * HOH_HDR_CAP))) return e;
-  if ((e = ensure(c->tab_fast, S * HOH_FAST_RANGE * sizeof(EncFast)))) return e;
+  if ((e = ensure(c->tab_fast, S * HOH_FAST_STRIDE * sizeof(EncFast)))) return e;
   if ((e = ensure(c->tab_gen, S * 512 * sizeof(EncGen)))) return e;
   if ((e = ensure(c->slabs, nslab * 4))) return e;
   if ((e = ensure(c->misc, 64 + (size_t)nimg * 16))) return e;   // gerr, total | batch: img_total[n], img_err[n]
@@ -777,7 +779,8 @@ int encode_streams_impl(hoh_ctx* c, const uint16_t* d_syms, const uint64_t* off,
   // ladder) takes the tuned chain k_rans_fast (k_tables may still hand a stream back), the rest
   // the reference reciprocal step (k_rans_gen)
   const bool fast = pb >= 7 && pb <= 19 && range <= HOH_FAST_RANGE;
-  if (fast && (e = ensure(c->tab_fast, (size_t)nstreams * HOH_FAST_RANGE * sizeof(EncFast)))) return e;
+  if (fast && (size_t)nstreams * HOH_FAST_STRIDE * sizeof(EncFast) > 0xffffffffull) return HOH_E_UNSUPPORTED;
+  if (fast && (e = ensure(c->tab_fast, (size_t)nstreams * HOH_FAST_STRIDE * sizeof(EncFast)))) return e;
   std::vector<StreamInfo> st((size_t)nstreams);
   for (int i = 0; i < nstreams; i++) {
     memset(&st[i], 0, sizeof(StreamInfo));

@@ -19,6 +19,11 @@ static inline int hoh_knob_env(const char* name, int def) { const char* e = gete
 #define HOH_WAVE 64
 #define HOH_HDR_CAP 1600          // bytes reserved per stream for varints + meta + table
 #define HOH_FAST_RANGE 512        // LDS-table fast encoder handles range <= 512 at prob_bits 15
+// entries per stream of the fast encoder's table (a skew of 2-16 entries against the L1 sets
+// measured no different: profiles/r06/ab_chain_placement_and_table_skew.txt)
+#ifndef HOH_FAST_STRIDE
+#define HOH_FAST_STRIDE HOH_FAST_RANGE
+#endif
 #define HOH_SEG 256               // decode checkpoint spacing (symbols)
 #define HOH_MAX_TILE_W 65535
 #define HOH_LZ_WINDOW 64          // -s0 seek distance 6 -> 1 << 6 pixels back (choh.cpp:125, lz.hpp:20)
@@ -212,7 +217,7 @@ struct EncodeJob {
   StreamInfo* streams;    // [ntiles * SK_PER_TILE]
   TileInfo* tiles;        // [ntiles]
   uint8_t* hdr;           // [stream][HOH_HDR_CAP]
-  EncFast* tab_fast;      // [stream][512]
+  EncFast* tab_fast;      // [stream][HOH_FAST_STRIDE]
   EncGen* tab_gen;        // [stream][gen_stride] (generic streams)
   uint32_t gen_stride;    // entries per stream in tab_gen (>= range)
   uint32_t hdr_cap;       // bytes per stream in hdr

@@ -193,7 +193,7 @@ __device__ __forceinline__ void rans_fast_run(const EncodeJob& j, uint32_t sid, 
 // One lane per stream, 64 streams per wave, one wave per workgroup: block blk of a launch.
 template <int KIND>
 __device__ __forceinline__ void rans_fast_body(const EncodeJob& j, int nplane, SidMap ma, int na, SidMap mb, int blk) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   // the chain is the critical path of an image: win issue arbitration against co-resident waves
 #ifndef CHAIN_PRIO
 #define CHAIN_PRIO 3
@@ -228,13 +228,13 @@ template <int KIND>
 __device__ __forceinline__ void rans_fast_run(const EncodeJob& j, uint32_t sid, const StreamInfo& st) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   constexpr bool GUARD = KIND == 3;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   const uint32_t n = st.n;
   const PbShape g{31u - st.pb, 1u << st.pb, 32u - st.pb};
   const char* tb = (const char*)j.tab_fast;
   // what-if EXP & 1 (measurement, output invalid): the 64 lanes' tables of block 0 for every
   // wave, so every table gather hits L2
-  const uint32_t tbase = ((j.exp & 1) ? (uint32_t)lane : sid) * (uint32_t)(HOH_FAST_RANGE * sizeof(EncFast));
+  const uint32_t tbase = ((j.exp & 1) ? (uint32_t)lane : sid) * (uint32_t)(HOH_FAST_STRIDE * sizeof(EncFast));
   Coder c;
   c.xh = 0; c.xl = 1u << 31; c.mask = 0; c.slot = 0; c.lost = 0;
   c.keep = !GUARD || st.sizeonly == 3;
@@ -315,9 +315,13 @@ __global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane, SidMa
 // The pb-15 plane chains and, in otherwise idle blocks of the same chip-wide grid, the LZ
 // streams (prob_bits 10): one launch, so the short LZ chains run beside the long ones instead of
 // after them (-0.2 ms per image encoded alone).
-__global__ __launch_bounds__(64) void k_rans_fast01(EncodeJob j, int np0, SidMap a0, int na0, SidMap b0, int nblk0,
-                                                    int np1, SidMap a1, int na1, SidMap b1, int nblk1, int rot) {
-  const int blk = (int)((blockIdx.x + gridDim.x - rot) % gridDim.x);
+#ifndef CHAIN_WAVES
+#define CHAIN_WAVES 1
+#endif
+__global__ __launch_bounds__(64 * CHAIN_WAVES) void k_rans_fast01(EncodeJob j, int np0, SidMap a0, int na0, SidMap b0,
+                                                                  int nblk0, int np1, SidMap a1, int na1, SidMap b1,
+                                                                  int nblk1, int rot) {
+  const int blk = (int)((blockIdx.x + gridDim.x - rot) % gridDim.x) * CHAIN_WAVES + (int)(threadIdx.x >> 6);
   if (blk < nblk0) rans_fast_body<0>(j, np0, a0, na0, b0, blk);
   else if (blk - nblk0 < nblk1) rans_fast_body<1>(j, np1, a1, na1, b1, blk - nblk0);
 }
@@ -405,19 +409,23 @@ static std::atomic<unsigned> g_rot{0};
 
 // LDS requested per chain workgroup (isolation: at most 160 / this many chains per CU; knob
 // CHAIN_LDS_KB), never less than the lanes' output windows (WIN_PITCH dwords per lane)
-static size_t chain_lds() {
-  const int kb = HOH_KNOB(CHAIN_LDS_KB, 56);
-  const size_t want = (size_t)(kb > 160 ? 160 : kb) * 1024, win = (size_t)WIN_PITCH * 4 * 64;
+#ifndef CHAIN_LDS_DEF
+#define CHAIN_LDS_DEF (CHAIN_WAVES == 1 ? 56 : 81)
+#endif
+static size_t chain_lds(int waves = 1) {
+  const int kb = HOH_KNOB(CHAIN_LDS_KB, CHAIN_LDS_DEF);
+  const size_t want = (size_t)(kb > 160 ? 160 : kb) * 1024, win = (size_t)WIN_PITCH * 4 * 64 * waves;
   return want < win ? win : want;
 }
 
 void launch_rans_fast01(const EncodeJob& j, hipStream_t s, int np0, SidMap a0, int na0, SidMap b0, int np1, SidMap a1,
                         int na1, SidMap b1) {
   const int nblk0 = (np0 + 63) / 64, nblk1 = (np1 + 63) / 64;
-  const int grid = std::max(nblk0 + nblk1, 1024);
-  const int rot = (int)((g_rot.fetch_add(1) * 8u * (unsigned)((nblk0 + nblk1 + 7) / 8)) % (unsigned)grid);
-  hipLaunchKernelGGL(k_rans_fast01, dim3(grid), dim3(64), chain_lds(), s, j, np0, a0, na0, b0, nblk0, np1, a1, na1, b1,
-                     nblk1, rot);
+  const int nwg = (nblk0 + nblk1 + CHAIN_WAVES - 1) / CHAIN_WAVES;
+  const int grid = std::max(nwg, 1024 / CHAIN_WAVES);
+  const int rot = (int)((g_rot.fetch_add(1) * 8u * (unsigned)((nwg + 7) / 8)) % (unsigned)grid);
+  hipLaunchKernelGGL(k_rans_fast01, dim3(grid), dim3(64 * CHAIN_WAVES), chain_lds(CHAIN_WAVES), s, j, np0, a0, na0, b0,
+                     nblk0, np1, a1, na1, b1, nblk1, rot);
 }
 
 void launch_rans_fast(const EncodeJob& j, int nplane, hipStream_t s, SidMap a, int na, SidMap b, int kind) {

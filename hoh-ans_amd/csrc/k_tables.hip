@@ -217,7 +217,7 @@ __global__ __launch_bounds__(64) void k_tables(EncodeJob j, SidMap sm) {
       }
       e.f = f ? f : 1;
       e.c = c;
-      j.tab_fast[(size_t)s * HOH_FAST_RANGE + i] = e;
+      j.tab_fast[(size_t)s * HOH_FAST_STRIDE + i] = e;
     } else {
       EncGen g;                                           // rans64.hpp:167-247
       g.freq = f;
