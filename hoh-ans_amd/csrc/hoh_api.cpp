@@ -397,8 +397,9 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   j.gen_stride = 512;
   j.hdr_cap = HOH_HDR_CAP;
   const size_t S = (size_t)ntiles * j.spt;
-  // the chains address every stream's table by a 32-bit offset from one base (k_rans_enc.hip)
-  if (S * HOH_FAST_STRIDE * sizeof(EncFast) > 0xffffffffull) return HOH_E_UNSUPPORTED;
+  // the -s0 chains address every stream's table by a 32-bit offset from one base (k_rans_enc.hip;
+  // the -s>=1 ones by 64-bit addresses)
+  if (!speed && S * HOH_FAST_STRIDE * sizeof(EncFast) > 0xffffffffull) return HOH_E_UNSUPPORTED;
   // arenas: [tile][3] planes, [tile][3] LZ streams, [tile] indexed plane (hoh_internal.h); the
   // -s>=1 layout is in hoh_internal.h too
   size_t nsym = (size_t)ntiles * 3 * (j.npix_cap + j.lz_cap) + (size_t)ntiles * j.npix_cap;
@@ -606,6 +607,11 @@ int hoh_encode_tiles_async(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int s
                            pick(c, stream), speed, d_status);
 }
 
+// tiles per -s>=1 stack (measurement knob SPEED_STACK_TILES; ~8 MB of workspace per tile): 1024
+// = one 8192^2 image, which fills the device alone (stacks of two measured 3-6 % slower in the
+// pipelined speed legs, profiles/r06/speed_batches.txt); small images stack up to it
+static int speed_stack() { return HOH_KNOB(SPEED_STACK_TILES, 1024); }
+
 // n images' shards per call (choh.cpp:464-500's tile loop over a band of tile rows, run over a
 // batch).  When the band is whole tile rows of 256 (H a multiple of 256), the n bands stacked in
 // d_rgb are the tile grid of one W x (n * rows) image, so every kernel covers all n bands' tiles in
@@ -623,8 +629,8 @@ int hoh_encode_tiles_images_async(hoh_ctx* c, int n, const uint8_t* d_rgb, int W
   if (t0 < 0 || ntiles <= 0 || t0 + ntiles > xt * yt || t0 % xt || ntiles % xt) return HOH_E_ARG;
   const int y0 = (t0 / xt) * th, rows = std::min(H, (t0 + ntiles) / xt * th) - y0;
   const size_t band = (size_t)W * rows * 3;
-  if (n == 1 || speed || !batch_stacks(W, H)) {
-    if (idx && n > 1) return HOH_E_UNSUPPORTED;      // a side index holds one shard here
+  if (n == 1 || !batch_stacks(W, H)) {
+    if (idx && n > 1 && !speed) return HOH_E_UNSUPPORTED;      // a side index holds one shard here
     for (int i = 0; i < n; i++) {
       const int r = hoh_encode_tiles_async(c, d_rgb + i * band - (size_t)y0 * W * 3, W, H, speed, t0, ntiles,
                                            d_out + i * stride, stride, d_tile_sizes + (size_t)i * ntiles, idx,
@@ -635,9 +641,22 @@ int hoh_encode_tiles_images_async(hoh_ctx* c, int n, const uint8_t* d_rgb, int W
   }
   if ((int64_t)rows * n > (1ll << 30) || (int64_t)ntiles * n > (1 << 24)) return HOH_E_ARG;
   (void)hipSetDevice(c->device);
-  uint64_t total = 0;
-  return encode_tiles_impl(c, d_rgb, W, rows * n, 0, ntiles * n, d_out, stride, 0, 0, d_tile_sizes, &total, idx,
-                           pick(c, stream), 0, d_status, n, stride);
+  if (speed && idx) idx->nstreams = 0;                 // -s>=1 files get no side index
+  // -s>=1 workspaces are ~8 MB per tile: stacks of at most speed_stack() tiles, one after another
+  const int per = speed ? std::max(1, speed_stack() / ntiles) : n;
+  for (int i0 = 0; i0 < n; i0 += per) {
+    const int k = std::min(per, n - i0);
+    uint64_t total = 0;
+    const int r = k == 1 ? hoh_encode_tiles_async(c, d_rgb + i0 * band - (size_t)y0 * W * 3, W, H, speed, t0, ntiles,
+                                                  d_out + i0 * stride, stride, d_tile_sizes + (size_t)i0 * ntiles,
+                                                  nullptr, d_status + 2 * i0, stream)
+                         : encode_tiles_impl(c, d_rgb + i0 * band, W, rows * k, 0, ntiles * k, d_out + i0 * stride,
+                                             stride, 0, 0, d_tile_sizes + (size_t)i0 * ntiles, &total,
+                                             speed ? nullptr : idx, pick(c, stream), speed, d_status + 2 * i0, k,
+                                             stride);
+    if (r) return r;
+  }
+  return HOH_OK;
 }
 
 int hoh_encode_image_ix(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int speed, uint8_t* d_out,
@@ -701,9 +720,9 @@ int hoh_encode_images_async(hoh_ctx* c, int n, const uint8_t* d_rgb, int W, int 
   int xt, yt, tw, th;
   if (!hoh_tiling(W, H, &xt, &yt, &tw, &th)) return HOH_E_UNSUPPORTED;
   const size_t img_bytes = (size_t)W * H * 3;
-  if (n == 1 || speed || !batch_stacks(W, H)) {
+  if (n == 1 || !batch_stacks(W, H)) {
     // one image after another on the stream (same bytes); a side index holds one image only
-    if (idx && n > 1) return HOH_E_UNSUPPORTED;
+    if (idx && n > 1 && !speed) return HOH_E_UNSUPPORTED;
     for (int i = 0; i < n; i++) {
       const int r = hoh_encode_image_async(c, d_rgb + i * img_bytes, W, H, speed, d_out + i * stride, stride, idx,
                                            d_status + 2 * i, stream);
@@ -720,10 +739,20 @@ int hoh_encode_images_async(hoh_ctx* c, int n, const uint8_t* d_rgb, int W, int 
   hb[hl++] = (uint8_t)(yt - 1);
   if (stride < hl) return HOH_E_CAP;
   launch_put_bytes(d_out, hb, (int)hl, s, n, stride);
-  uint64_t total = 0;
-  const int r = encode_tiles_impl(c, d_rgb, W, H * n, 0, xt * yt * n, d_out, stride, hl, 1, nullptr, &total, idx, s,
-                                  0, d_status, n, stride);
-  return r;
+  if (speed && idx) idx->nstreams = 0;                 // -s>=1 files get no side index
+  // -s>=1 workspaces are ~8 MB per tile: stacks of at most speed_stack() tiles, one after another
+  const int per = speed ? std::max(1, speed_stack() / (xt * yt)) : n;
+  for (int i0 = 0; i0 < n; i0 += per) {
+    const int k = std::min(per, n - i0);
+    uint64_t total = 0;
+    const int r = k == 1 ? encode_tiles_impl(c, d_rgb + i0 * img_bytes, W, H, 0, xt * yt, d_out + i0 * stride, stride,
+                                             hl, 1, nullptr, &total, nullptr, s, speed, d_status + 2 * i0)
+                         : encode_tiles_impl(c, d_rgb + i0 * img_bytes, W, H * k, 0, xt * yt * k, d_out + i0 * stride,
+                                             stride, hl, 1, nullptr, &total, speed ? nullptr : idx, s, speed,
+                                             d_status + 2 * i0, k, stride);
+    if (r) return r;
+  }
+  return HOH_OK;
 }
 
 int hoh_encode_image(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int speed, uint8_t* d_out, size_t cap,
@@ -779,7 +808,6 @@ int encode_streams_impl(hoh_ctx* c, const uint16_t* d_syms, const uint64_t* off,
   // ladder) takes the tuned chain k_rans_fast (k_tables may still hand a stream back), the rest
   // the reference reciprocal step (k_rans_gen)
   const bool fast = pb >= 7 && pb <= 19 && range <= HOH_FAST_RANGE;
-  if (fast && (size_t)nstreams * HOH_FAST_STRIDE * sizeof(EncFast) > 0xffffffffull) return HOH_E_UNSUPPORTED;
   if (fast && (e = ensure(c->tab_fast, (size_t)nstreams * HOH_FAST_STRIDE * sizeof(EncFast)))) return e;
   std::vector<StreamInfo> st((size_t)nstreams);
   for (int i = 0; i < nstreams; i++) {

@@ -254,6 +254,13 @@ inline int batch_stacks(int W, int H) { return (W >= 512 || H >= 512) && W >= 25
 
 // the image of tile t and the base of its file in out
 __host__ __device__ inline int tile_img(const EncodeJob& j, int t) { return j.nimg > 1 ? t / j.img_tiles : 0; }
+// a batch image's file is written only when it fits its stride and none of its tiles failed
+__device__ __forceinline__ bool file_ok(const EncodeJob& j, int t) {
+  if (*j.gerr) return false;
+  if (j.nimg <= 1) return *j.total <= j.cap;
+  const int img = tile_img(j, t);
+  return j.img_total[img] <= j.out_stride && !j.img_err[img];
+}
 
 // arena offsets (elements / words): [tile][3] planes, [tile][3] LZ streams, [tile] indexed plane
 __host__ __device__ inline size_t idx_plane_off(const EncodeJob& j, int t) {

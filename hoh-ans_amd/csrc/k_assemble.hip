@@ -135,14 +135,6 @@ __global__ __launch_bounds__(1024) void k_layout(EncodeJob j) {
   }
 }
 
-// a batch image's file is written only when it fits its stride and none of its tiles failed
-__device__ __forceinline__ bool file_ok(const EncodeJob& j, int t) {
-  if (*j.gerr) return false;
-  if (j.nimg <= 1) return *j.total <= j.cap;
-  const int img = tile_img(j, t);
-  return j.img_total[img] <= j.out_stride && !j.img_err[img];
-}
-
 __global__ __launch_bounds__(64) void k_tilebytes(EncodeJob j) {
   const int t = blockIdx.x * 64 + threadIdx.x;
   if (t >= j.ntiles || !file_ok(j, t)) return;

@@ -187,11 +187,13 @@ __device__ __forceinline__ void ckpt(const Coder& c, Checkpoint* ck, uint32_t k)
   ck[k] = p;
 }
 
-template <int KIND>
+template <int KIND, bool WIDE>
 __device__ __forceinline__ void rans_fast_run(const EncodeJob& j, uint32_t sid, const StreamInfo& st);
 
 // One lane per stream, 64 streams per wave, one wave per workgroup: block blk of a launch.
-template <int KIND>
+// WIDE: each lane's table through its own 64-bit address (jobs whose tables pass 4 GB: batched
+// -s>=1 encodes); otherwise 32-bit offsets from one scalar base (the -s0 chains)
+template <int KIND, bool WIDE = false>
 __device__ __forceinline__ void rans_fast_body(const EncodeJob& j, int nplane, SidMap ma, int na, SidMap mb, int blk) {
   const int lane = threadIdx.x & 63;
   // the chain is the critical path of an image: win issue arbitration against co-resident waves
@@ -220,21 +222,22 @@ __device__ __forceinline__ void rans_fast_body(const EncodeJob& j, int nplane, S
   if (st.sizeonly == 2) return;            // pruned trial (k_prune_s): its words are set
   // trials: the storing chain for every lane when the pool is on (storing and counting lanes share
   // a wave: two kinds of chain in one wave would run one after the other)
-  if (KIND == 2 && j.tpool_words) rans_fast_run<3>(j, sid, st);
-  else rans_fast_run<KIND>(j, sid, st);
+  if (KIND == 2 && j.tpool_words) rans_fast_run<3, WIDE>(j, sid, st);
+  else rans_fast_run<KIND, WIDE>(j, sid, st);
 }
 
-template <int KIND>
+template <int KIND, bool WIDE>
 __device__ __forceinline__ void rans_fast_run(const EncodeJob& j, uint32_t sid, const StreamInfo& st) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   constexpr bool GUARD = KIND == 3;
   const int lane = threadIdx.x & 63;
   const uint32_t n = st.n;
   const PbShape g{31u - st.pb, 1u << st.pb, 32u - st.pb};
-  const char* tb = (const char*)j.tab_fast;
   // what-if EXP & 1 (measurement, output invalid): the 64 lanes' tables of block 0 for every
   // wave, so every table gather hits L2
-  const uint32_t tbase = ((j.exp & 1) ? (uint32_t)lane : sid) * (uint32_t)(HOH_FAST_STRIDE * sizeof(EncFast));
+  const uint32_t tsid = (j.exp & 1) ? (uint32_t)lane : sid;
+  const char* tb = (const char*)j.tab_fast + (WIDE ? (size_t)tsid * (HOH_FAST_STRIDE * sizeof(EncFast)) : 0);
+  const uint32_t tbase = WIDE ? 0u : tsid * (uint32_t)(HOH_FAST_STRIDE * sizeof(EncFast));
   Coder c;
   c.xh = 0; c.xl = 1u << 31; c.mask = 0; c.slot = 0; c.lost = 0;
   c.keep = !GUARD || st.sizeonly == 3;
@@ -309,7 +312,7 @@ __global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane, SidMa
   // the grid covers every CU; the working blocks are a window rotated per launch so that the
   // chains of images in flight land on different CUs instead of sharing the first ones
   const int blk = (int)((blockIdx.x + gridDim.x - rot) % gridDim.x);
-  if (blk < nblk) rans_fast_body<KIND>(j, nplane, ma, na, mb, blk);
+  if (blk < nblk) rans_fast_body<KIND, true>(j, nplane, ma, na, mb, blk);
 }
 
 // The pb-15 plane chains and, in otherwise idle blocks of the same chip-wide grid, the LZ
@@ -334,9 +337,9 @@ __global__ __launch_bounds__(64) void k_rans_fast_s(EncodeJob j, int np0, SidMap
                                                     int np2, SidMap a2, int na2, int nblk2,
                                                     int np1, SidMap a1, int na1, int nblk1) {
   const int blk = (int)blockIdx.x;
-  if (blk < nblk0) rans_fast_body<0>(j, np0, a0, na0, b0, blk);
-  else if (blk - nblk0 < nblk2) rans_fast_body<2>(j, np2, a2, na2, SidMap{0, 0}, blk - nblk0);
-  else if (blk - nblk0 - nblk2 < nblk1) rans_fast_body<1>(j, np1, a1, na1, SidMap{0, 0}, blk - nblk0 - nblk2);
+  if (blk < nblk0) rans_fast_body<0, true>(j, np0, a0, na0, b0, blk);
+  else if (blk - nblk0 < nblk2) rans_fast_body<2, true>(j, np2, a2, na2, SidMap{0, 0}, blk - nblk0);
+  else if (blk - nblk0 - nblk2 < nblk1) rans_fast_body<1, true>(j, np1, a1, na1, SidMap{0, 0}, blk - nblk0 - nblk2);
 }
 
 // Generic: one lane per stream, rans64.hpp:262-278 verbatim (64x64 high product).

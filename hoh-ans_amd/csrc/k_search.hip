@@ -2006,16 +2006,20 @@ __device__ void place_layer(const EncodeJob& j, int t, int p, uint64_t off, uint
   st[(pi.perm_final ? KS_MED : KS_FIN) + p].drop = 1;
 }
 
+// One workgroup per file (k_layout's batch scheme): blockIdx.x = the image of a batch, its tiles
+// [tb, te), its file at img * out_stride; else the one file / shard blob
 __global__ __launch_bounds__(1024) void k_layout_s(EncodeJob j) {
   __shared__ uint64_t part[1024];
   __shared__ uint64_t tot_size, tot_vlen;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, img = blockIdx.x;
+  const int tb = j.nimg > 1 ? img * j.img_tiles : 0, te = j.nimg > 1 ? tb + j.img_tiles : j.ntiles;
+  const uint64_t fbase = j.nimg > 1 ? (uint64_t)img * j.out_stride : 0;
   if (tid == 0) { tot_size = 0; tot_vlen = 0; }
   __syncthreads();
-  for (int base = 0; base < j.ntiles; base += 1024) {
+  for (int base = tb; base < te; base += 1024) {
     const int t = base + tid;
     uint64_t sz = 0, vl = 0;
-    if (t < j.ntiles) {
+    if (t < te) {
       TileInfo ti = j.tiles[t];
       StreamInfo* st = j.streams + (size_t)t * SPT_S;
       const PlaneInfo* pi = j.pinfo + (size_t)t * HOH_NPLANE_S;
@@ -2043,13 +2047,13 @@ __global__ __launch_bounds__(1024) void k_layout_s(EncodeJob j) {
         else s64 += 1 + hoh_varint_len(L1) + hoh_varint_len(pi[c2].size) + L1 + pi[c2].size + pi[c3].size;
         ti.chmap = ch1 | (c2 << 4) | (c3 << 8);
       }
-      if (bad) atomicOr(j.gerr, bad << 8);
+      if (bad) atomicOr(j.nimg > 1 ? j.img_err + img : j.gerr, j.nimg > 1 ? bad : bad << 8);
       ti.lz_bytes = lzb;
       ti.size = (uint32_t)s64;
       j.tiles[t] = ti;
       sz = s64;
       if (j.tile_sizes) j.tile_sizes[t] = (uint32_t)s64;
-      if (j.write_table && t + 1 < j.ntiles) vl = hoh_varint_len(s64);
+      if (j.write_table && t + 1 < te) vl = hoh_varint_len(s64);
     }
     if (sz) atomicAdd((unsigned long long*)&tot_size, (unsigned long long)sz);
     if (vl) atomicAdd((unsigned long long*)&tot_vlen, (unsigned long long)vl);
@@ -2057,12 +2061,12 @@ __global__ __launch_bounds__(1024) void k_layout_s(EncodeJob j) {
   __syncthreads();
   const uint64_t first = j.prefix + tot_vlen;
   uint64_t carry_s = 0, carry_v = 0;
-  for (int base = 0; base < j.ntiles; base += 1024) {
+  for (int base = tb; base < te; base += 1024) {
     const int t = base + tid;
     uint64_t sz = 0, vl = 0;
-    if (t < j.ntiles) {
+    if (t < te) {
       sz = j.tiles[t].size;
-      if (j.write_table && t + 1 < j.ntiles) vl = hoh_varint_len(sz);
+      if (j.write_table && t + 1 < te) vl = hoh_varint_len(sz);
     }
     part[tid] = sz;
     __syncthreads();
@@ -2074,9 +2078,9 @@ __global__ __launch_bounds__(1024) void k_layout_s(EncodeJob j) {
     for (int o = 1; o < 1024; o <<= 1) { const uint64_t u = tid >= o ? part[tid - o] : 0; __syncthreads(); part[tid] += u; __syncthreads(); }
     const uint64_t ev = part[tid] - vl, chunk_v = part[1023];
     __syncthreads();
-    if (t < j.ntiles) {
+    if (t < te) {
       TileInfo ti = j.tiles[t];
-      ti.off = first + carry_s + es;
+      ti.off = fbase + first + carry_s + es;
       ti.pad = (uint32_t)(j.prefix + carry_v + ev);
       j.tiles[t] = ti;
       StreamInfo* st = j.streams + (size_t)t * SPT_S;
@@ -2111,20 +2115,25 @@ __global__ __launch_bounds__(1024) void k_layout_s(EncodeJob j) {
     carry_s += chunk_s;
     carry_v += chunk_v;
   }
-  if (tid == 0) *j.total = first + tot_size;
+  if (tid == 0) {
+    if (j.nimg > 1) j.img_total[img] = first + tot_size;
+    else *j.total = first + tot_size;
+  }
 }
 
 // fixed bytes: tile framing (choh.cpp:115-116, :328, :351-356), LZ flags (lz.hpp:98) and every
 // placed layer's header (layer_encode.hpp:57, :276-297 or :320-325), clipped to its limit
 __global__ __launch_bounds__(64) void k_tilebytes_s(EncodeJob j) {
   const int t = blockIdx.x * 64 + threadIdx.x;
-  if (t >= j.ntiles || *j.total > j.cap || *j.gerr) return;
+  if (t >= j.ntiles || !file_ok(j, t)) return;
   const TileInfo ti = j.tiles[t];
   uint8_t* o = j.out + ti.off;
   o[0] = 0; o[1] = 0;
   o[2] = (uint8_t)ti.mode;
   o[3] = 0x03;
-  if (j.write_table && t + 1 < j.ntiles) hoh_write_varint(j.out, ti.pad, ti.size);
+  const int img = tile_img(j, t);
+  const bool last = j.nimg > 1 ? (t + 1) % j.img_tiles == 0 : t + 1 == j.ntiles;
+  if (j.write_table && !last) hoh_write_varint(j.out + (j.nimg > 1 ? (uint64_t)img * j.out_stride : 0), ti.pad, ti.size);
   if (ti.flags & TF_GREY) return;
   const PlaneInfo* pi = j.pinfo + (size_t)t * HOH_NPLANE_S;
   const uint32_t ch1 = ti.chmap & 15, c2 = (ti.chmap >> 4) & 15, c3 = (ti.chmap >> 8) & 15;
@@ -2263,7 +2272,7 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, v
   launch_rans_gen(j, j.ntiles * HOH_NPLANE_S, s, fin);
   launch_finalize(j, j.ntiles * HOH_NPLANE_S, s, fin);
   mark(mc, "rans_enc_final");
-  hipLaunchKernelGGL(k_layout_s, dim3(1), dim3(1024), 0, s, j);
+  hipLaunchKernelGGL(k_layout_s, dim3(j.nimg > 1 ? j.nimg : 1), dim3(1024), 0, s, j);
   hipLaunchKernelGGL(k_tilebytes_s, dim3((j.ntiles + 63) / 64), dim3(64), 0, s, j);
   launch_streambytes(j, S, s);
   mark(mc, "assemble");
