@@ -540,8 +540,9 @@ def extra_legs(args, slots, W, H, D, B, stride, status, torch, hoh_ans, hd):
 def speed_legs(args, slots, nat, W, H, D, B, stride, status, torch, hoh_ans, hd):
     """BASELINE configs[4] at the search speeds: the natural-statistic image (seed --seed in every
     slot) encoded at choh -s1..-s4 (full predictor search, layer_encode.hpp:122-319, and the
-    seek-distance LZ, lz.hpp:32-95 at 10..14), D slots of B images in flight (a slot's B images run
-    one after another at -s>=1: hoh_encode_images_async batches -s0 only), encode only (-s>=1
+    seek-distance LZ, lz.hpp:32-95 at 10..14), D slots of B images in flight (at -s>=1
+    hoh_encode_images_async stacks up to 1024 tiles per job: one 8192^2 image, which fills the
+    device alone -- stacks of two measured 3-6 % slower here), encode only (-s>=1
     layers are undecodable by construction), one set-up pass per slot, then
     --speed-leg-steps timed steps.  EVERY image's last file is SHA-compared with the reference
     choh's (golden_natural.json); one image at a time: the best of 3 synchronous encodes on slot 0."""

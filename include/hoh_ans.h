@@ -137,8 +137,10 @@ int hoh_decode_image_async(hoh_ctx* ctx, const uint8_t* d_hoh, size_t size, int 
  * Files are byte-identical to the single-image calls'.  One side index serves the whole batch
  * (payload positions are absolute in the batch buffer), so a decode with it needs the same n and
  * stride (else HOH_E_ARG).  The batch runs as one job when its tiles stack -- H a multiple of 256,
- * so the n images are the 256-row tile grid of one n*H image -- at -s0;
- * otherwise tiled images run one after another on the stream (without a side index when n > 1:
+ * so the n images are the 256-row tile grid of one n*H image; at -s1..-s4 (whose workspace is ~8 MB
+ * per tile) as stacks of up to 1024 tiles (one 8192^2 image, or 64 of 1024^2) one after another,
+ * and no side index (idx, if given, is emptied as in the single-image calls); otherwise tiled
+ * images run one after another on the stream (without a side index when n > 1 at -s0:
  * HOH_E_UNSUPPORTED).  Untiled shapes (header-only files) return HOH_E_UNSUPPORTED for
  * any n, as in the single-image async calls: use hoh_encode_image / hoh_decode_image.  The decoder
  * bounds every parse of file i by [i*stride, (i+1)*stride) (a truncated file reads as corrupt) and
@@ -193,7 +195,7 @@ int hoh_decode_tiles_async(hoh_ctx* ctx, const uint8_t* d_blob, size_t size, int
  * band RGB bytes} (decode) per shard.  When H is a multiple of 256 the n bands stack into one
  * tile grid and every kernel covers all n shards per launch (as hoh_encode_images_async does for
  * whole images); otherwise the shards run one after another on the stream.  Blobs are
- * byte-identical to n single-shard calls'.  -s0 stacks; -s>=1 runs shard after shard.  A side
+ * byte-identical to n single-shard calls'.  -s1..-s4 stack up to 1024 tiles per job.  A side
  * index serves the batch it was recorded for (same n and stride).  The decoder bounds every parse
  * of blob i by [i*stride, (i+1)*stride) and reads n*stride bytes of d_blob at most; in a one-job
  * batch an error in any blob marks every shard's status. */
