@@ -348,12 +348,17 @@ __global__ __launch_bounds__(64 * LZ_SEG) void k_lz(EncodeJob j) {
 // One 256-thread workgroup per tile; the nuke bitmap is built in LDS from the match list, then the plane is walked in
 // 256-pixel blocks with a block-wide rank of the kept pixels.
 __device__ __forceinline__ void nuke_tile(const EncodeJob& j, int t, uint32_t* nk_bits, uint32_t* wsum, bool in_lds);
+// 2048-pixel blocks, eight pixels per thread: 16-B plane loads and stores (below)
+#define NK_B 2048
+template <int NPM>
+__device__ __forceinline__ void nuke_tile_v(const EncodeJob& j, int t, uint32_t* nk_bits, uint32_t* wsum,
+                                            uint16_t (*nkbuf)[NK_B + 16]);
 
 // nuke bitmap + removed-count histograms in LDS need (npix_cap/32 + 1 + slots*512) words; a
 // single tile too large for that (untiled images over ~1.1 M px: the LDS holds 160 KB) takes the
 // same walk with the match list searched per pixel and the counts subtracted in global memory.
 __host__ __device__ static inline int nuke_slots(const EncodeJob& j) { return j.speed ? 2 * HOH_NPLANE_S : 4; }
-#define NK_LDS_MAX (160 * 1024 - 256)
+#define NK_LDS_MAX (160 * 1024 - 256 - 2 * (NK_B + 16) * 2)   // beside the staging buffers
 
 // A small grid strides over the tiles (most have no match): a launch over every tile dispatches
 // ~1000 idle workgroups, which waits for free CUs when other images are in flight.
@@ -372,6 +377,15 @@ void k_nuke(EncodeJob j, int in_lds) {
   extern __shared__ uint32_t nk_bits[];                  // npix_cap / 32 words, then the counts
   __shared__ uint32_t wsum[4];
   for (int t = blockIdx.x; t < j.ntiles; t += gridDim.x) nuke_tile(j, t, nk_bits, wsum, in_lds != 0);
+}
+// the 16-B walk (nuke_tile_v): NPM planes at most (-s0: 4, -s>=1: 12)
+template <int NPM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPM > 4 ? 4 : NUKE_WPE, NPM > 4 ? 4 : NUKE_WPE)))
+void k_nuke_v(EncodeJob j) {
+  extern __shared__ uint32_t nk_bits[];
+  __shared__ uint32_t wsum[4];
+  __shared__ __attribute__((aligned(16))) uint16_t nkbuf[2][NK_B + 16];
+  for (int t = blockIdx.x; t < j.ntiles; t += gridDim.x) nuke_tile_v<NPM>(j, t, nk_bits, wsum, nkbuf);
 }
 
 // matches are disjoint and in increasing position order (the greedy scan of k_lz / k_lzscan):
@@ -477,6 +491,135 @@ __device__ __forceinline__ void nuke_tile(const EncodeJob& j, int t, uint32_t* n
   __syncthreads();
 }
 
+// The LDS-bitmap walk in 2048-pixel blocks: thread i takes pixels 8i .. 8i+7 of the block, every
+// plane's eight values in one 16-B load; the kept ones are ranked once per block (eight bits of
+// the nuke bitmap per thread, one block scan), and each plane's kept values are staged in LDS at
+// their destination's offset from the 16-B line below it, so they leave as 16-B stores too (the
+// first and last partial lines element by element).  Two staging buffers alternate: one barrier
+// per plane.  (The 256-pixel walk of nuke_tile moved one u16 per thread per plane behind two
+// barriers a block: 2.3 GB in 1.4 ms per natural 8192^2 -s4 launch, twelve planes a tile.)
+// In place: a block's writes land below its own end, and every block reads its values first.
+template <int NPM>
+__device__ __forceinline__ void nuke_tile_v(const EncodeJob& j, int t, uint32_t* nk_bits, uint32_t* wsum,
+                                            uint16_t (*nkbuf)[NK_B + 16]) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const TileInfo ti = j.tiles[t];
+  const uint32_t nm = ti.nmatch;
+  if (nm == 0 || (ti.flags & TF_OVERFLOW) || nm > j.lz_cap) return;
+  const uint32_t npix = (uint32_t)ti.w * ti.h, nwords = (npix + 31) / 32;
+  const uint32_t* mt = j.matches + (size_t)t * 3 * (j.lz_cap + 1);
+  const int nslots = nuke_slots(j);
+  uint32_t* nh = nk_bits + j.npix_cap / 32 + 1;          // removed counts, [slot][512]
+  for (uint32_t i = tid; i < nwords + 1; i += 256) nk_bits[i] = 0;
+  for (uint32_t i = tid; i < (uint32_t)nslots * 512; i += 256) nh[i] = 0;
+  __syncthreads();
+  for (uint32_t m = tid; m < nm; m += 256) {             // one thread per match (disjoint)
+    const uint32_t a = mt[3 * m], e = a + mt[3 * m + 1];
+    for (uint32_t p = a; p < e; p++) atomicOr(&nk_bits[p >> 5], 1u << (p & 31));
+  }
+  __syncthreads();
+  const bool grey = ti.flags & TF_GREY, pal = !grey && (ti.flags & TF_PALETTE_CAND);
+  // slot k (< nslots <= NPM): -s0 the MED planes G R' B' (+ indexed); -s>=1 the six MED planes,
+  // then the six searched planes.  The pointers are recomputed where used (scalar arithmetic), not
+  // held: twelve plane and twelve histogram pointers overflowed the scalar registers.
+  uint32_t pres = 0;
+  for (int k = 0; k < nslots; k++) {
+    const int p = k % HOH_NPLANE_S;
+    if (!grey && (p < 3 || (p == 3 && pal) || (p >= 4 && j.speed >= 3))) pres |= 1u << k;
+  }
+  if (pres == 0) return;
+  auto plane = [&](int k) -> uint16_t* {
+    const int p = k % HOH_NPLANE_S;
+    return j.sym + ((k < HOH_NPLANE_S || !j.speed) ? med_plane_off(j, t, p) : fin_plane_off(j, t, p));
+  };
+  auto histo = [&](int k) -> uint32_t* {
+    const int p = k % HOH_NPLANE_S;
+    return j.hist + (size_t)(t * j.spt + ((k < HOH_NPLANE_S || !j.speed) ? med_kind(j, p) : KS_FIN + p)) * 512;
+  };
+  uint32_t outc = 0;
+  for (uint32_t base = 0; base < npix; base += NK_B) {
+    const uint32_t p0 = base + 8 * (uint32_t)tid;
+    const bool full = p0 + 8 <= npix;
+    uint4 v[NPM];
+#pragma unroll
+    for (int k = 0; k < NPM; k++) {
+      v[k] = make_uint4(0, 0, 0, 0);
+      if ((pres >> k) & 1) {
+        const uint16_t* rk = plane(k);
+        if (full) v[k] = *(const uint4*)(rk + p0);
+        else if (p0 < npix) {
+          uint16_t e[8];
+#pragma unroll
+          for (int i = 0; i < 8; i++) e[i] = p0 + i < npix ? rk[p0 + i] : 0;
+          v[k] = make_uint4(e[0] | e[1] << 16, e[2] | e[3] << 16, e[4] | e[5] << 16, e[6] | e[7] << 16);
+        }
+      }
+    }
+    const uint32_t valid = p0 >= npix ? 0u : full ? 0xffu : (1u << (npix - p0)) - 1u;
+    const uint32_t nk8 = (nk_bits[p0 >> 5] >> (p0 & 31)) & valid;   // p0 % 8 == 0: one word
+    const uint32_t keep = valid & ~nk8, cnt = (uint32_t)__popc(keep);
+    if (nk8) {                                           // removed values: counted in LDS, applied once below
+#pragma unroll
+      for (int k = 0; k < NPM; k++)
+        if ((pres >> k) & 1) {
+          const uint32_t w4[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+          for (int i = 0; i < 8; i++)
+            if ((nk8 >> i) & 1) atomicAdd(&nh[k * 512 + ((w4[i >> 1] >> (16 * (i & 1))) & 0xffffu)], 1u);
+        }
+    }
+    // block exclusive scan of the kept counts
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(incl, o);
+      if (lane >= o) incl += u;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    uint32_t before = incl - cnt, tot = 0;
+    for (int q = 0; q < 4; q++) { const uint32_t c = wsum[q]; if (q < wv) before += c; tot += c; }
+    // global dest outc + i <-> staging slot (outc & 7) + i; 16-B line c of the staging buffer is
+    // global elements a0 + 8c .. a0 + 8c + 7 (a0 = outc & ~7)
+    const uint32_t sk = (outc & 7u) + before, a0 = outc & ~7u, lo = outc & 7u, hi = lo + tot;
+    const uint32_t nln = (hi + 7) / 8;
+    uint32_t bsel = 0;                                   // alternates per present plane (slots skip)
+#pragma unroll
+    for (int k = 0; k < NPM; k++) {
+      if ((pres >> k) & 1) {
+        uint16_t* b = nkbuf[bsel];
+        bsel ^= 1;
+        uint16_t* rk = plane(k);
+        const uint32_t w4[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+        uint32_t s = sk;
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+          if ((keep >> i) & 1) b[s++] = (uint16_t)(w4[i >> 1] >> (16 * (i & 1)));
+        __syncthreads();                                 // also: the other buffer's reads are done
+        for (uint32_t c = tid; c < nln; c += 256) {
+          const uint32_t e0 = 8 * c;
+          if (e0 >= lo && e0 + 8 <= hi) {
+            *(uint4*)(rk + a0 + e0) = *(const uint4*)(b + e0);
+          } else {
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+              if (e0 + i >= lo && e0 + i < hi) rk[a0 + e0 + i] = b[e0 + i];
+          }
+        }
+      }
+    }
+    outc += tot;
+    __syncthreads();                                     // wsum and the staging buffers are reused
+  }
+  for (int k = 0; k < NPM; k++)
+    if ((pres >> k) & 1) {
+      uint32_t* hk = histo(k);
+      for (uint32_t i = tid; i < 512; i += 256)
+        if (nh[k * 512 + i]) hk[i] -= nh[k * 512 + i];   // this tile's histograms: one writer
+    }
+  __syncthreads();
+}
+
 void launch_lz(const EncodeJob& j, hipStream_t s) {
   hipLaunchKernelGGL(k_lz, dim3(j.ntiles), dim3(64 * LZ_SEG), 0, s, j);
 }
@@ -485,5 +628,7 @@ void launch_nuke(const EncodeJob& j, hipStream_t s) {
   // one workgroup per tile (natural images: most tiles have copies); tiles without copies leave
   const size_t lds = ((size_t)j.npix_cap / 32 + 1 + (size_t)nuke_slots(j) * 512) * 4;
   const bool in_lds = lds <= NK_LDS_MAX;
-  hipLaunchKernelGGL(k_nuke, dim3(j.ntiles), dim3(256), in_lds ? lds : 0, s, j, (int)in_lds);
+  if (!in_lds) hipLaunchKernelGGL(k_nuke, dim3(j.ntiles), dim3(256), 0, s, j, 0);
+  else if (j.speed) hipLaunchKernelGGL(k_nuke_v<2 * HOH_NPLANE_S>, dim3(j.ntiles), dim3(256), lds, s, j);
+  else hipLaunchKernelGGL(k_nuke_v<4>, dim3(j.ntiles), dim3(256), lds, s, j);
 }

@@ -1169,28 +1169,61 @@ __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring,
 // the same fingerprint as q and before it is in q's group, before q, in descending order when
 // walked back from q's rank -- so k_lzscan visits only equal-hash positions of q's window, back
 // distances ascending, instead of every fingerprint of the window (lz.hpp:32-50 at seek 11..14).
-// Two stable counting-sort passes (LSD, 8-bit digits) of pos | hash << 16 per tile, one 256-thread
-// workgroup per tile (small, so it schedules beside the predictor search it overlaps): per
-// 256-position chunk, a wave ranks its lanes by digit with 8 ballots, the 4 waves' per-digit counts
-// are prefix-summed in LDS, and each position lands at its digit's base + the counts of the waves
-// before + its rank in its wave (stable).
+// Two stable counting-sort passes (LSD, 8-bit digits) of the entries pos | hash << 16 |
+// fingerprint << 32, one 1024-thread workgroup per tile (tiles strided over a grid of one
+// workgroup per CU).  Both passes' digit counts come from one read of the fingerprints (LDS
+// histograms); then each pass runs over chunks of LZSORT_C entries: a chunk is ranked in LDS (each
+// wave a contiguous share of it, 64 at a time: ballot peers per digit, a wave-private running base
+// per digit, one scan over (digit, wave)), staged in digit order, and leaves as one contiguous run
+// per digit at the digit's running base -- whole lines, not one 8-byte store per line per wave
+// (round 5 scattered straight from registers: 16 waves x 256 digits of open lines per tile, ~140 B
+// of HBM traffic per position against ~28 stored).
 // j.lzs_hmask is 0xffff; a knobs build can narrow it (LZS_HMASK) so that hash collisions are the rule
 // (tools/scripts/r5_collide.sh: the files must not change)
 __device__ __forceinline__ uint32_t lzs_hash(uint32_t f, uint32_t hm) { return ((f * 0x9E3779B1u) >> 16) & hm; }
 #ifndef LZSORT_T
-#define LZSORT_T 1024         // threads per tile (one wave per contiguous share of the positions)
+#define LZSORT_T 1024         // threads per tile
 #endif
+#ifndef LZSORT_C
+#define LZSORT_C 4096         // entries per staged chunk (a wave ranks LZSORT_C / 16 of them)
+#endif
+#define LZSORT_W (LZSORT_T / 64)
+#define LZSORT_K (LZSORT_C / LZSORT_T)   // groups of 64 per wave and chunk
+#define LZSORT_RH (32 * LZSORT_T)         // positions whose ranks are built in LDS at a time (a word each)
+static_assert(LZSORT_C % LZSORT_T == 0, "whole groups per wave");
 __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j, int limit) {
-  // Stable LSD counting sort by the 16-bit hash, two 8-bit passes.  Each wave owns a contiguous
-  // quarter of the pass's input and ranks it alone (64 at a time: ballot peers per digit, a
-  // wave-private running base per digit), so a pass has two barriers, not three per 256
-  // positions; the bases come from one scan over (digit, wave).  The next 64 keys are loaded
-  // while the current 64 are ranked.
-  __shared__ uint32_t cnt[LZSORT_T / 64][256];                   // per wave: digit counts, then bases
+  // the sort's staging (a chunk's listed entries in digit order, then per wave its digit counts /
+  // bases), later half a tile's ranks (k_lzscan's R)
+  constexpr uint32_t UB = LZSORT_C + LZSORT_W * 128 > LZSORT_RH / 4 ? LZSORT_C + LZSORT_W * 128 : LZSORT_RH / 4;
+  __shared__ __attribute__((aligned(16))) uint64_t ubuf[UB];
+  uint64_t* buf = ubuf;
+  uint32_t (*cnt)[256] = (uint32_t(*)[256])(ubuf + LZSORT_C);
+  uint16_t* Rl = (uint16_t*)ubuf;
+  __shared__ uint32_t hg[2][256];                                // per pass: digit counts, then running output bases
+  __shared__ uint32_t cst[257];                                  // a chunk's digit starts in buf; [256]: its size
+  __shared__ uint32_t wt[LZSORT_W];                              // scans: totals of the waves
   __shared__ uint32_t inner[65536 / 32];                         // flat positions inside a run (unlisted)
   __shared__ uint32_t cbit[65536 / 32];                          // the candidate screen (below)
   __shared__ uint32_t s_nl, s_ncand;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // this lane's digit group among the 64: the lanes with the same digit
+  auto group = [&](bool valid, uint32_t d) -> uint64_t {
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+      const uint64_t m = __ballot((d >> b) & 1);
+      peers &= ((d >> b) & 1) ? m : ~m;
+    }
+    return peers;
+  };
+  auto wscan = [&](uint32_t v) -> uint32_t {                     // inclusive scan over the wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(v, o);
+      if (lane >= o) v += u;
+    }
+    return v;
+  };
   // tiles strided over the grid (a smaller grid keeps fewer tiles' scatter targets in L2 at once)
   for (int t = blockIdx.x; t < j.ntiles; t += gridDim.x) {
   __syncthreads();                                               // the previous tile done
@@ -1220,95 +1253,149 @@ __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j, int limit) {
       cbit[i >> 5] = (uint32_t)mc; cbit[(i >> 5) + 1] = (uint32_t)(mc >> 32);
     }
   }
+  if (tid < 512) hg[tid >> 8][tid & 255] = 0;
   if (tid == 0) s_ncand = 0;
-  const uint32_t quarter = ((n + LZSORT_T / 64 - 1) / (LZSORT_T / 64) + 63) & ~63u;
-  const uint32_t lo = min(n, (uint32_t)wv * quarter), hi = min(n, lo + quarter);
+  __syncthreads();
+  auto is_inner = [&](uint32_t pos) -> bool { return (inner[pos >> 5] >> (pos & 31)) & 1; };
+  // both passes' digit counts: every position for the first, the listed ones for the second
+  for (uint32_t c0 = 0; c0 < n; c0 += LZSORT_T) {
+    const uint32_t i = c0 + tid;
+    const bool valid = i < n, listed = valid && !is_inner(i);
+    const uint32_t h = valid ? lzs_hash(F[i], hm) : 0u, d0 = h & 255, d1 = h >> 8;
+    const uint64_t g0 = group(valid, d0), g1 = group(listed, d1);
+    if (valid && __popcll(g0 & lt) == 0) atomicAdd(&hg[0][d0], (uint32_t)__popcll(g0));
+    if (listed && __popcll(g1 & lt) == 0) atomicAdd(&hg[1][d1], (uint32_t)__popcll(g1));
+  }
+  __syncthreads();
+  {                                                              // -> each digit's first output slot
+    const uint32_t hh = (uint32_t)tid >> 8;
+    const uint32_t v = tid < 512 ? hg[hh][tid & 255] : 0u, incl = wscan(v);
+    if (tid < 512 && lane == 63) wt[wv] = incl;
+    __syncthreads();
+    if (tid < 512) {
+      uint32_t run = incl - v;
+      for (int w = (int)hh * 4; w < wv; w++) run += wt[w];
+      hg[hh][tid & 255] = run;
+      if (tid == 511) s_nl = run + v;                            // listed positions
+    }
+  }
   for (int pass = 0; pass < 2; pass++) {
     const uint32_t sh = 16 + 8 * pass;
-    // entries travel as key | fingerprint << 32 (the fingerprint read once, coalesced, here)
-    const uint64_t* in = pass ? T : nullptr;
     uint64_t* out = pass ? SF : T;
-    auto key_at = [&](uint32_t i) -> uint64_t {
-      if (i >= hi) return 0u;
-      if (pass) return in[i];
-      const uint32_t f = F[i];
-      return (uint64_t)f << 32 | (i | (lzs_hash(f, hm) << 16));
-    };
-    // the second pass lists the counted positions only; an unlisted one takes no slot
-    auto listed_of = [&](uint32_t i, uint32_t key) -> bool {
-      const uint32_t pos = key & 0xffffu;
-      return i < hi && (!pass || !((inner[pos >> 5] >> (pos & 31)) & 1));
-    };
-    // this lane's digit group among the 64: the lanes with the same digit
-    auto group = [&](bool valid, uint32_t d) -> uint64_t {
-      uint64_t peers = __ballot(valid);
+    uint32_t* gb = hg[pass];
+    for (uint32_t c0 = 0; c0 < n; c0 += LZSORT_C) {
+      // this wave's share of the chunk: LZSORT_K groups of 64 consecutive entries
+      const uint32_t b0 = c0 + (uint32_t)wv * (LZSORT_K * 64);
+      uint64_t ent[LZSORT_K], lp[LZSORT_K];
+      uint32_t dg[LZSORT_K];
+      bool ls[LZSORT_K], vd[LZSORT_K];
 #pragma unroll
-      for (int b = 0; b < 8; b++) {
-        const uint64_t m = __ballot((d >> b) & 1);
-        peers &= ((d >> b) & 1) ? m : ~m;
+      for (int k = 0; k < LZSORT_K; k++) {
+        const uint32_t i = b0 + 64 * k + lane;
+        vd[k] = i < n;
+        uint64_t e = 0;
+        if (vd[k]) {
+          if (pass) e = T[i];
+          else { const uint32_t f = F[i]; e = (uint64_t)f << 32 | (i | (lzs_hash(f, hm) << 16)); }
+        }
+        ent[k] = e;
+        dg[k] = ((uint32_t)e >> sh) & 255;
+        ls[k] = vd[k] && (!pass || !is_inner((uint32_t)e & 0xffffu));
       }
-      return peers;
-    };
 #pragma unroll
-    for (int k = 0; k < 4; k++) cnt[wv][lane + 64 * k] = 0;        // each wave its own row
-    __syncthreads();                                               // inner / the previous pass done
-    // 1. this wave's listed count per digit
-    uint64_t kn = key_at(lo + lane);
-    for (uint32_t i0 = lo; i0 < hi; i0 += 64) {
-      const uint32_t i = i0 + lane, key = (uint32_t)kn;
-      kn = key_at(i + 64);
-      const bool listed = listed_of(i, key);
-      const uint32_t d = (key >> sh) & 255;
-      const uint64_t lp = group(i < hi, d) & __ballot(listed);
-      if (listed && __popcll(lp & lt) == 0) cnt[wv][d] += (uint32_t)__popcll(lp);
+      for (int k = 0; k < 4; k++) cnt[wv][lane + 64 * k] = 0;    // each wave its own row
+#pragma unroll
+      for (int k = 0; k < LZSORT_K; k++) {
+        lp[k] = group(vd[k], dg[k]) & __ballot(ls[k]);
+        if (ls[k] && __popcll(lp[k] & lt) == 0) cnt[wv][dg[k]] += (uint32_t)__popcll(lp[k]);
+      }
+      __syncthreads();
+      // the chunk's bases in buf: digits in order, the waves in order inside a digit (thread d < 256)
+      {
+        uint32_t c[LZSORT_W], tot = 0;
+#pragma unroll
+        for (int w = 0; w < LZSORT_W; w++) { c[w] = tid < 256 ? cnt[w][tid] : 0u; tot += c[w]; }
+        const uint32_t incl = wscan(tot);
+        if (tid < 256 && lane == 63) wt[wv] = incl;
+        __syncthreads();
+        if (tid < 256) {
+          uint32_t run = incl - tot;
+          for (int w = 0; w < wv; w++) run += wt[w];
+          cst[tid] = run;
+          if (tid == 255) cst[256] = run + tot;
+#pragma unroll
+          for (int w = 0; w < LZSORT_W; w++) { cnt[w][tid] = run; run += c[w]; }
+        }
+      }
+      __syncthreads();
+      // stage in digit order (stable: waves, groups, lanes in order)
+#pragma unroll
+      for (int k = 0; k < LZSORT_K; k++) {
+        const uint32_t d = dg[k], o = cnt[wv][d] + (uint32_t)__popcll(lp[k] & lt);
+        if (ls[k] && __popcll(lp[k] & lt) == 0) cnt[wv][d] = o + (uint32_t)__popcll(lp[k]);   // the group's first
+        if (ls[k]) buf[o] = ent[k];
+      }
+      __syncthreads();
+      // each digit's run of the chunk, contiguous at the digit's running base
+      const uint32_t m = cst[256];
+      for (uint32_t e = tid; e < m; e += LZSORT_T) {
+        const uint64_t v = buf[e];
+        const uint32_t d = ((uint32_t)v >> sh) & 255, o = gb[d] + (e - cst[d]);
+        out[o] = v;
+      }
+      __syncthreads();
+      if (tid < 256) gb[tid] += cst[tid + 1] - cst[tid];
     }
-    __syncthreads();
-    // 2. bases: digits in order, the waves in order inside a digit (threads 0..255: digit tid)
-    {
-      const uint32_t d = (uint32_t)tid & 255u;
-      const bool dg = tid < 256;
-      uint32_t c[LZSORT_T / 64], tot = 0;
-#pragma unroll
-      for (int w = 0; w < LZSORT_T / 64; w++) { c[w] = dg ? cnt[w][d] : 0u; tot += c[w]; }
-      // exclusive scan of the 256 digit totals (thread d holds digit d)
-      uint32_t incl = tot;
+  }
+  __syncthreads();
+  // Ranks R (k_lzscan starts q's walk at R[q] - 1): a listed position's index in SF; a flat
+  // position inside its run the last listed position before it in its group, which is its run's
+  // start (every position between is inside the run, unlisted).  Built in LDS LZSORT_RH positions
+  // at a time from SF (read coalesced) and written out in 16-B pieces (scattered u16 stores cost a
+  // line each).  Run starts: thread i holds inner word i of the part; the last non-inner position
+  // at or before each inner one comes from its own word or, by a max-scan over the words, from an
+  // earlier word; before the part, from `carry` (the previous part's last run start's rank).
+  {
+    uint32_t carry = 0;
+    for (uint32_t h0 = 0; h0 < n; h0 += LZSORT_RH) {
+      const uint32_t hn = min((uint32_t)LZSORT_RH, n - h0);
+      for (uint32_t i = tid; i < s_nl; i += LZSORT_T) {
+        const uint32_t pos = (uint32_t)SF[i] & 0xffffu;
+        if (pos - h0 < hn) Rl[pos - h0] = (uint16_t)i;
+      }
+      const uint32_t wb = 32 * (uint32_t)tid;
+      const uint32_t iw = wb < hn ? inner[(h0 + wb) >> 5] : 0u;
+      const uint32_t non = wb < hn ? ~iw : 0u;                   // non-inner (listed or past n) positions
+      // inclusive max-scan of (last non-inner position + 1) over the words
+      uint32_t lp = non ? wb + 32u - (uint32_t)__builtin_clz(non) : 0u;
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t u = __shfl_up(incl, o);
-        if (lane >= o) incl += u;
+        const uint32_t u = __shfl_up(lp, o);
+        if (lane >= o) lp = max(lp, u);
       }
-      __syncthreads();                                             // every count read
-      if (dg && lane == 63) cnt[0][wv] = incl;                     // wave totals (digits 64wv..)
+      if (lane == 63) wt[wv] = lp;
+      const uint32_t lprev = __shfl_up(lp, 1);
       __syncthreads();
-      uint32_t run = incl - tot;
-      for (int w = 0; w < wv && w < 4; w++) run += cnt[0][w];
-      if (pass && tid == 255) s_nl = run + tot;                    // listed positions
-      __syncthreads();
-      if (dg) {
+      uint32_t ex = lane ? lprev : 0u, tot = 0;
 #pragma unroll
-        for (int w = 0; w < LZSORT_T / 64; w++) { cnt[w][d] = run; run += c[w]; }
+      for (int w = 0; w < LZSORT_W; w++) {
+        const uint32_t v = wt[w];
+        if (w < wv) ex = max(ex, v);
+        tot = max(tot, v);
       }
-    }
-    __syncthreads();
-    // 3. scatter in order: rank = the wave's running base of the digit + listed peers before
-    kn = key_at(lo + lane);
-    for (uint32_t i0 = lo; i0 < hi; i0 += 64) {
-      const uint64_t ent = kn;
-      const uint32_t i = i0 + lane, key = (uint32_t)ent;
-      kn = key_at(i + 64);
-      const bool valid = i < hi, listed = listed_of(i, key);
-      const uint32_t d = (key >> sh) & 255, pos = key & 0xffffu;
-      const uint64_t lp = group(valid, d) & __ballot(listed);
-      const uint32_t o = valid ? cnt[wv][d] + (uint32_t)__popcll(lp & lt) : 0u;
-      if (listed && __popcll(lp & lt) == 0) cnt[wv][d] = o + (uint32_t)__popcll(lp);   // the group's first
-      if (listed) {
-        out[o] = ent;
-        if (pass) R[pos] = (uint16_t)o;
-      } else if (valid) {
-        // the last listed position before it in its group: its run's start, or a hash-colliding
-        // position after that start (k_lzscan steps over its own run's start)
-        R[pos] = (uint16_t)(o - 1);
+      const uint32_t before = ex ? (uint32_t)Rl[ex - 1] : carry;
+      for (uint32_t m = iw; m; m &= m - 1) {
+        const uint32_t b = (uint32_t)__builtin_ctz(m);
+        const uint32_t nb = non & ((2u << b) - 1u);              // the word up to b (b = 31: all of it)
+        Rl[wb + b] = nb ? Rl[wb + 31 - __builtin_clz(nb)] : (uint16_t)before;
       }
+      carry = tot ? (uint32_t)Rl[tot - 1] : carry;
+      __syncthreads();
+      for (uint32_t e = 8 * (uint32_t)tid; e < hn; e += 8 * LZSORT_T) {
+        if (e + 8 <= hn) *(uint4*)(R + h0 + e) = *(const uint4*)(Rl + e);
+        else for (uint32_t i = e; i < hn; i++) R[h0 + i] = Rl[i];
+      }
+      __syncthreads();
     }
   }
   __syncthreads();
@@ -2184,11 +2271,15 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, v
   // a failed fork runs the LZ kernels on s itself (ordered), never unordered on the side stream
   // knob LZ_FORK=0: the LZ kernels on s itself (measurement)
   const int fork_ok = HOH_KNOB(LZ_FORK, 1);
+  // k_lzfp before the fork at the speeds whose LZ stream is the longer (knob LZFP_FIRST: up to
+  // that speed): alone it takes 0.6 ms, beside the predictor search's first kernels 2.6
+  const bool lzfp_first = j.speed <= HOH_KNOB(LZFP_FIRST, 0);
+  if (lzfp_first) hipLaunchKernelGGL(k_lzfp, dim3(16, j.ntiles), dim3(NT), 0, s, j);
   const bool fork = fork_ok && side.s && side.fork && side.join && hipEventRecord(side.fork, s) == hipSuccess &&
                     hipStreamWaitEvent(side.s, side.fork, 0) == hipSuccess;
   hipStream_t sl = fork ? side.s : s;
   {
-    hipLaunchKernelGGL(k_lzfp, dim3(16, j.ntiles), dim3(NT), 0, sl, j);
+    if (!lzfp_first) hipLaunchKernelGGL(k_lzfp, dim3(16, j.ntiles), dim3(NT), 0, sl, j);
     // the hash tables pay at -s1's window (1024); the longer windows of -s2..-s4 fill them and
     // take the global map when a tile's (half-full) map fits its share of tab_gen
     uint32_t mw = 1;
