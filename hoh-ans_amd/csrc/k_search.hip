@@ -2272,8 +2272,10 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, v
   // knob LZ_FORK=0: the LZ kernels on s itself (measurement)
   const int fork_ok = HOH_KNOB(LZ_FORK, 1);
   // k_lzfp before the fork at the speeds whose LZ stream is the longer (knob LZFP_FIRST: up to
-  // that speed): alone it takes 0.6 ms, beside the predictor search's first kernels 2.6
-  const bool lzfp_first = j.speed <= HOH_KNOB(LZFP_FIRST, 0);
+  // that speed): alone it takes 0.6 ms, beside the predictor search's first kernels 2.6.  Natural
+  // 8192^2 (profiles/r06b/ab_lzfp_first.txt): -s1 20.3 -> 18.9 ms, -s2 21.9 -> 20.4; at -s3 / -s4,
+  // where the search stream is the longer, +0.4 / +-0
+  const bool lzfp_first = j.speed <= HOH_KNOB(LZFP_FIRST, 2);
   if (lzfp_first) hipLaunchKernelGGL(k_lzfp, dim3(16, j.ntiles), dim3(NT), 0, s, j);
   const bool fork = fork_ok && side.s && side.fork && side.join && hipEventRecord(side.fork, s) == hipSuccess &&
                     hipStreamWaitEvent(side.s, side.fork, 0) == hipSuccess;
