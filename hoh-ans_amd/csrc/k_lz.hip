@@ -628,7 +628,10 @@ void launch_nuke(const EncodeJob& j, hipStream_t s) {
   // one workgroup per tile (natural images: most tiles have copies); tiles without copies leave
   const size_t lds = ((size_t)j.npix_cap / 32 + 1 + (size_t)nuke_slots(j) * 512) * 4;
   const bool in_lds = lds <= NK_LDS_MAX;
-  if (!in_lds) hipLaunchKernelGGL(k_nuke, dim3(j.ntiles), dim3(256), 0, s, j, 0);
-  else if (j.speed) hipLaunchKernelGGL(k_nuke_v<2 * HOH_NPLANE_S>, dim3(j.ntiles), dim3(256), lds, s, j);
+  // -s0 (three or four planes): the 16-B walk (natural 8192^2 encode 7.78 -> 7.67 ms); -s>=1
+  // (twelve planes): the 256-pixel walk, whose six waves per SIMD beat the 16-B walk's twelve
+  // staged planes per block (1.42 against 1.64 ms alone per natural -s4 launch,
+  // profiles/r06b/bench_closing.json speed_roofline_s4)
+  if (!in_lds || j.speed) hipLaunchKernelGGL(k_nuke, dim3(j.ntiles), dim3(256), in_lds ? lds : 0, s, j, (int)in_lds);
   else hipLaunchKernelGGL(k_nuke_v<4>, dim3(j.ntiles), dim3(256), lds, s, j);
 }

@@ -1181,17 +1181,17 @@ __global__ __launch_bounds__(NT) void k_lzcand(EncodeJob j, int limit, int ring,
 // j.lzs_hmask is 0xffff; a knobs build can narrow it (LZS_HMASK) so that hash collisions are the rule
 // (tools/scripts/r5_collide.sh: the files must not change)
 __device__ __forceinline__ uint32_t lzs_hash(uint32_t f, uint32_t hm) { return ((f * 0x9E3779B1u) >> 16) & hm; }
-#ifndef LZSORT_T
-#define LZSORT_T 1024         // threads per tile
-#endif
-#ifndef LZSORT_C
-#define LZSORT_C 4096         // entries per staged chunk (a wave ranks LZSORT_C / 16 of them)
-#endif
-#define LZSORT_W (LZSORT_T / 64)
-#define LZSORT_K (LZSORT_C / LZSORT_T)   // groups of 64 per wave and chunk
-#define LZSORT_RH (32 * LZSORT_T)         // positions whose ranks are built in LDS at a time (a word each)
-static_assert(LZSORT_C % LZSORT_T == 0, "whole groups per wave");
+// LZSORT_T threads per tile workgroup, chunks of LZSORT_C entries (a wave ranks LZSORT_C / (T / 64)
+// of them).  Two shapes: 1024 / 4096 (one workgroup per CU) where the LZ stream is the longer one
+// (-s1/-s2), 512 / 2048 at -s3/-s4, where the predictor search beside it is the longer one and
+// gets half of each CU's waves back (natural 8192^2 -s4 31.6 -> 30.8 ms; at -s1 the 1024 shape is
+// 1.6 ms faster: profiles/r06b/ab_lzsort_512.txt)
+template <int LZSORT_T, int LZSORT_C>
 __global__ __launch_bounds__(LZSORT_T) void k_lzsort(EncodeJob j, int limit) {
+  constexpr int LZSORT_W = LZSORT_T / 64;
+  constexpr int LZSORT_K = LZSORT_C / LZSORT_T;                  // groups of 64 per wave and chunk
+  constexpr int LZSORT_RH = 32 * LZSORT_T;                       // positions whose ranks are built in LDS at a time (a word each)
+  static_assert(LZSORT_C % LZSORT_T == 0, "whole groups per wave");
   // the sort's staging (a chunk's listed entries in digit order, then per wave its digit counts /
   // bases), later half a tile's ranks (k_lzscan's R)
   constexpr uint32_t UB = LZSORT_C + LZSORT_W * 128 > LZSORT_RH / 4 ? LZSORT_C + LZSORT_W * 128 : LZSORT_RH / 4;
@@ -2296,7 +2296,9 @@ void encode_speed_s(const EncodeJob& j, hipStream_t s, const SideStream& side, v
       // by 1.4-1.7 ms at -s1..-s4 (k_lzsort 5.2 -> 3.7 ms at -s1; tools/scripts/r5_ab_lzsort.sh)
       const int sgk = HOH_KNOB(LZSORT_GRID, 0);                      // 0: the CU count
       const int sg = sgk > 0 ? sgk : j.cus > 0 ? j.cus : 256;
-      hipLaunchKernelGGL(k_lzsort, dim3(sg > 0 && sg < j.ntiles ? sg : j.ntiles), dim3(LZSORT_T), 0, sl, j, limit);
+      const dim3 grid(sg > 0 && sg < j.ntiles ? sg : j.ntiles);
+      if (j.speed >= HOH_KNOB(LZSORT_HALF_SPEED, 3)) hipLaunchKernelGGL((k_lzsort<512, 2048>), grid, dim3(512), 0, sl, j, limit);
+      else hipLaunchKernelGGL((k_lzsort<1024, 4096>), grid, dim3(1024), 0, sl, j, limit);
     } else {
       hipLaunchKernelGGL(k_lzcand, dim3(j.ntiles), dim3(NT), lds, sl, j, limit, lring, mode, mw, HOH_KNOB(LZC_NOWALK, 0));
     }
