@@ -2588,8 +2588,9 @@ static uint32_t lz_xrow() { return (uint32_t)HOH_KNOB(LZ_XROW, LZ_XROW); }
 // k_drans_lanes' ~400) but holds a whole CU per 12 chains; k_drans_lanes packs up to 64 chains per
 // workgroup into compact tables and fills the device when several decodes run at once.  So an
 // adaptive decode that has the device to itself takes k_drans_multi, one that finds another
-// context's no-index chain kernel still in flight takes k_drans_lanes.  HOH_NOIX_WAVE: one wave
-// per stream (k_drans_wave, the round-2 decoder).
+// context's no-index chain kernel still in flight, or whose plane chains need more than one round
+// of k_drans_multi (batches, 16384^2), takes k_drans_lanes.  HOH_NOIX_WAVE: one wave per stream
+// (k_drans_wave, the round-2 decoder).
 
 // Contexts' completion events per device, to count the no-index decodes in flight beside this one.
 static std::mutex g_noix_mu;
@@ -2702,7 +2703,10 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
     uint32_t* rounds = tbytes + S;                           // S + 1 words
     hipLaunchKernelGGL(k_dmlist, dim3((S + 255) / 256), dim3(256), 0, s, j, S, mlist);
     const int pin = ctx_noix(c);
-    const bool multi = pin == HOH_NOIX_MULTI || (pin != HOH_NOIX_LANES && !noix_busy(w, ctx_device(c)));
+    // k_drans_multi only while the plane chains fit one round of it (12 per CU: one 8192^2 image);
+    // a batch of eight took 8 rounds, 50 ms, where k_drans_lanes takes two (profiles/r06b/noix_pipeline_prof.txt)
+    const bool one_round = 3 * j.ntiles <= DM_MS * ctx_cus(c);
+    const bool multi = pin == HOH_NOIX_MULTI || (pin != HOH_NOIX_LANES && one_round && !noix_busy(w, ctx_device(c)));
     if (multi) {
       // one workgroup per CU (its LDS is a whole CU's), rounds of DM_MS streams per workgroup
       const int nmax = std::min(S, 6 * j.ntiles);
