@@ -2633,11 +2633,13 @@ static int noix_busy(DecWork& w, int dev) {
 }
 // k_drans_lanes: LDS table budget per workgroup (knob DL_BUDGET_KB, >= the 5.1 KB worst-case
 // table) and workgroups per CU (knob DL_WG)
+// (no-index pipeline, 4 contexts x batches of 8: 20 KB x 4 68.8 GB/s, 32 x 4 75.1, 48 x 3 78.6,
+// 64 x 2 73.7, 80 x 2 62.2; profiles/r06b/noix_pipeline_lds_budget_sweep.txt)
 static uint32_t dl_budget() {
-  const uint32_t kb = (uint32_t)HOH_KNOB(DL_BUDGET_KB, 20);
+  const uint32_t kb = (uint32_t)HOH_KNOB(DL_BUDGET_KB, 48);
   return std::max<uint32_t>(std::min<uint32_t>(kb, 150u) * 1024u, dl_bytes(15, 512));
 }
-static int dl_wg_per_cu() { return std::max(1, HOH_KNOB(DL_WG, 4)); }
+static int dl_wg_per_cu() { return std::max(1, HOH_KNOB(DL_WG, 3)); }
 
 static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s, const AsyncDec* as) {
   j.exp = (uint32_t)HOH_KNOB(EXP, 0);
