@@ -456,6 +456,7 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   if ((e = ensure(c->tab_gen, S * 512 * sizeof(EncGen)))) return e;
   if ((e = ensure(c->slabs, nslab * 4))) return e;
   if ((e = ensure(c->misc, 64 + (size_t)nimg * 16))) return e;   // gerr, total | batch: img_total[n], img_err[n]
+  j.cus = c->cus;                 // grids that stride over the tiles (k_lzsort, k_nuke)
   j.sym = (uint16_t*)c->sym.p;
   j.hist = (uint32_t*)c->hist.p;
   j.candbits = (uint64_t*)c->candbits.p;

@@ -205,7 +205,7 @@ struct EncodeJob {
                           //   hash16(fingerprint), ascending inside a group
   uint16_t* lzrank;       //   [tile][npix_cap] index of each position in lzsf (flat run-inner positions: their run start's)
   uint32_t lzs_hmask;     //   the posting hash's mask (0xffff; knob LZS_HMASK in measurement builds)
-  int cus;                //   compute units of the device (k_lzsort's grid: one tile workgroup per CU)
+  int cus;                // compute units of the device (k_lzsort's grid: one tile workgroup per CU; k_nuke's)
   uint16_t* lzend;        //   [tile][npix_cap] per lzsf entry: the last position of a flat run start's run, else the position
   uint64_t* lzsf;         //   [tile][npix_cap] the listed positions in order: key (pos | hash << 16) | fingerprint << 32
   PlaneInfo* pinfo;       // -s>=1: [tile][6]

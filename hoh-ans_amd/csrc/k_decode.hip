@@ -2759,7 +2759,11 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
       else hipLaunchKernelGGL(k_dunpred_lz<1024>, dim3(grid + gc), dim3(64), l, s, j, br, many, grid, ga, full1, full2);
     };
     launch(wf, (size_t)(br_few + 1) * rowb, br_few, 0);
-    if (j.ntiles > LZ_FEW) launch(j.ntiles, (size_t)(br_many + 1) * rowb, br_many, 1);
+    // the wavefront workgroups stride over the LZ tile list, so more of them than the CUs hold
+    // at once (their LDS bands: ~4 per CU) buy nothing; a grid of one per tile dispatched ~8,000
+    // workgroups per batch of eight 8192^2 images even when no tile has copies (knob LZ_WG_PER_CU)
+    const int wcap = HOH_KNOB(LZ_WG_PER_CU, 4) * ctx_cus(c);
+    if (j.ntiles > LZ_FEW) launch(wcap > 0 && wcap < j.ntiles ? wcap : j.ntiles, (size_t)(br_many + 1) * rowb, br_many, 1);
     hipLaunchKernelGGL(k_dcompose, dim3(gsmall), dim3(256), 0, s, j);   // the chain tiles' RGB
   }
   ctx_mark(c, s, "dunpred", false);

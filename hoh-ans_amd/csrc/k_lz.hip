@@ -625,13 +625,17 @@ void launch_lz(const EncodeJob& j, hipStream_t s) {
 }
 
 void launch_nuke(const EncodeJob& j, hipStream_t s) {
-  // one workgroup per tile (natural images: most tiles have copies); tiles without copies leave
+  // Workgroups stride over the tiles (KNOB NUKE_WG_PER_CU x CUs of them): a tile without copies
+  // leaves at once, and a grid of one workgroup per tile dispatched ~8,000 such workgroups per
+  // batch of eight 8192^2 images behind the other contexts' kernels.
   const size_t lds = ((size_t)j.npix_cap / 32 + 1 + (size_t)nuke_slots(j) * 512) * 4;
   const bool in_lds = lds <= NK_LDS_MAX;
   // -s0 (three or four planes): the 16-B walk (natural 8192^2 encode 7.78 -> 7.67 ms); -s>=1
   // (twelve planes): the 256-pixel walk, whose six waves per SIMD beat the 16-B walk's twelve
   // staged planes per block (1.42 against 1.64 ms alone per natural -s4 launch,
   // profiles/r06b/bench_closing.json speed_roofline_s4)
-  if (!in_lds || j.speed) hipLaunchKernelGGL(k_nuke, dim3(j.ntiles), dim3(256), in_lds ? lds : 0, s, j, (int)in_lds);
-  else hipLaunchKernelGGL(k_nuke_v<4>, dim3(j.ntiles), dim3(256), lds, s, j);
+  const int cap = HOH_KNOB(NUKE_WG_PER_CU, 8) * (j.cus > 0 ? j.cus : 256);
+  const dim3 grid(cap > 0 && cap < j.ntiles ? cap : j.ntiles);
+  if (!in_lds || j.speed) hipLaunchKernelGGL(k_nuke, grid, dim3(256), in_lds ? lds : 0, s, j, (int)in_lds);
+  else hipLaunchKernelGGL(k_nuke_v<4>, grid, dim3(256), lds, s, j);
 }

@@ -72,7 +72,8 @@ def test_batch_equals_single_and_roundtrips(hoh, W, H, n):
 
 
 def test_batch_8192_vs_reference_goldens(hoh):
-    """four bench seeds at 8192^2 in one batch: every file's SHA equals the reference choh's"""
+    """four bench seeds at 8192^2 in one batch: every file's SHA equals the reference choh's, and
+    the batch decodes losslessly with and without the side index"""
     import torch
     g = json.load(open(os.path.join(HERE, "golden", "golden_bench.json")))
     want = {r["spec"]["seed"]: (r["out"]["len"], r["out"]["sha256"]) for r in g["files"]
@@ -96,6 +97,15 @@ def test_batch_8192_vs_reference_goldens(hoh):
     ds = torch.zeros_like(st)
     torch.cuda.synchronize()
     hoh.decode_images_async(out, len(seeds), stride, W, H, dec, ds, ctx=ctx, index=idx)
+    torch.cuda.synchronize()
+    assert all(int(x) == 0 for x in ds.cpu().numpy()[0::2])
+    assert torch.equal(dec, rgb)
+    # the files alone (no side index): 12,288 plane chains, more than one round of k_drans_multi,
+    # so the adaptive choice takes k_drans_lanes (k_decode.hip, the one-round rule)
+    dec.zero_()
+    ds.zero_()
+    torch.cuda.synchronize()
+    hoh.decode_images_async(out, len(seeds), stride, W, H, dec, ds, ctx=ctx, index=None)
     torch.cuda.synchronize()
     assert all(int(x) == 0 for x in ds.cpu().numpy()[0::2])
     assert torch.equal(dec, rgb)
