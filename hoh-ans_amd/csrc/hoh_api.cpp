@@ -468,6 +468,7 @@ static int encode_tiles_impl(hoh_ctx* c, const uint8_t* d_rgb, int W, int H, int
   j.tiles = (TileInfo*)c->tiles.p;
   j.hdr = (uint8_t*)c->hdr.p;
   j.tab_fast = (EncFast*)c->tab_fast.p;
+  j.tab_wide = (size_t)S * HOH_FAST_STRIDE * sizeof(EncFast) > 0xffffffffull;
   j.tab_gen = (EncGen*)c->tab_gen.p;
   j.slabs = (uint32_t*)c->slabs.p;
   j.slab_words = nslab;
@@ -832,6 +833,7 @@ int encode_streams_impl(hoh_ctx* c, const uint16_t* d_syms, const uint64_t* off,
   j.hdr_cap = hcap;
   j.tab_gen = (EncGen*)c->tab_gen.p;
   j.tab_fast = fast ? (EncFast*)c->tab_fast.p : nullptr;
+  j.tab_wide = (size_t)nstreams * HOH_FAST_STRIDE * sizeof(EncFast) > 0xffffffffull;
   j.gen_stride = range;
   j.slabs = (uint32_t*)c->slabs.p;
   j.ckpt = nullptr;                           // stream-level decodes are serial: no checkpoints

@@ -218,6 +218,7 @@ struct EncodeJob {
   TileInfo* tiles;        // [ntiles]
   uint8_t* hdr;           // [stream][HOH_HDR_CAP]
   EncFast* tab_fast;      // [stream][HOH_FAST_STRIDE]
+  int tab_wide;           // tab_fast passes 4 GB: the chains address each lane's table through 64 bits
   EncGen* tab_gen;        // [stream][gen_stride] (generic streams)
   uint32_t gen_stride;    // entries per stream in tab_gen (>= range)
   uint32_t hdr_cap;       // bytes per stream in hdr

@@ -306,13 +306,13 @@ __device__ __forceinline__ void rans_fast_run(const EncodeJob& j, uint32_t sid, 
   j.streams[sid].widx_end = c.widx;
 }
 
-template <int KIND>
+template <int KIND, bool WIDE>
 __global__ __launch_bounds__(64) void k_rans_fast(EncodeJob j, int nplane, SidMap ma, int na, SidMap mb, int nblk,
                                                   int rot) {
   // the grid covers every CU; the working blocks are a window rotated per launch so that the
   // chains of images in flight land on different CUs instead of sharing the first ones
   const int blk = (int)((blockIdx.x + gridDim.x - rot) % gridDim.x);
-  if (blk < nblk) rans_fast_body<KIND, true>(j, nplane, ma, na, mb, blk);
+  if (blk < nblk) rans_fast_body<KIND, WIDE>(j, nplane, ma, na, mb, blk);
 }
 
 // The pb-15 plane chains and, in otherwise idle blocks of the same chip-wide grid, the LZ
@@ -333,13 +333,16 @@ __global__ __launch_bounds__(64 * CHAIN_WAVES) void k_rans_fast01(EncodeJob j, i
 // and the other real encodes (KIND 1: LZ / predictor-map streams) are independent, so they share
 // one launch: an image waits for one chain length instead of three.  One chain per SIMD (a 40 KB
 // request per one-wave workgroup: four per CU), the long chains first in the grid.
+// WIDE only for jobs whose tables pass 4 GB (j.tab_wide); otherwise 32-bit offsets from one base,
+// as the -s0 chain (one instruction per two gathers' addresses instead of two per gather)
+template <bool WIDE>
 __global__ __launch_bounds__(64) void k_rans_fast_s(EncodeJob j, int np0, SidMap a0, int na0, SidMap b0, int nblk0,
                                                     int np2, SidMap a2, int na2, int nblk2,
                                                     int np1, SidMap a1, int na1, int nblk1) {
   const int blk = (int)blockIdx.x;
-  if (blk < nblk0) rans_fast_body<0, true>(j, np0, a0, na0, b0, blk);
-  else if (blk - nblk0 < nblk2) rans_fast_body<2, true>(j, np2, a2, na2, SidMap{0, 0}, blk - nblk0);
-  else if (blk - nblk0 - nblk2 < nblk1) rans_fast_body<1, true>(j, np1, a1, na1, SidMap{0, 0}, blk - nblk0 - nblk2);
+  if (blk < nblk0) rans_fast_body<0, WIDE>(j, np0, a0, na0, b0, blk);
+  else if (blk - nblk0 < nblk2) rans_fast_body<2, WIDE>(j, np2, a2, na2, SidMap{0, 0}, blk - nblk0);
+  else if (blk - nblk0 - nblk2 < nblk1) rans_fast_body<1, WIDE>(j, np1, a1, na1, SidMap{0, 0}, blk - nblk0 - nblk2);
 }
 
 // Generic: one lane per stream, rans64.hpp:262-278 verbatim (64x64 high product).
@@ -443,12 +446,17 @@ void launch_rans_fast(const EncodeJob& j, int nplane, hipStream_t s, SidMap a, i
   // KIND 1 (LZ / map streams, the ladder's winners): short or few chains, no chip-wide grid
   const int grid = (nblk >= 1024 || kind == 1) ? nblk : 1024;
   const int rot = grid == nblk ? 0 : (int)((g_rot.fetch_add(1) * 8u * (unsigned)((nblk + 7) / 8)) % (unsigned)grid);
-  if (kind == 0)
-    hipLaunchKernelGGL(k_rans_fast<0>, dim3(grid), dim3(64), chain_lds(), s, j, nplane, a, na, b, nblk, rot);
-  else if (kind == 1)   // short or few chains (LZ / map streams, the ladder's winners): the window only
-    hipLaunchKernelGGL(k_rans_fast<1>, dim3(grid), dim3(64), WIN_PITCH * 4 * 64, s, j, nplane, a, na, b, nblk, rot);
-  else   // size-only trial encodes: no window; one chain per SIMD (40 KB), all at once
-    hipLaunchKernelGGL(k_rans_fast<2>, dim3(grid), dim3(64), 40 * 1024, s, j, nplane, a, na, b, nblk, rot);
+  const bool w = j.tab_wide != 0;
+  if (kind == 0) {
+    if (w) hipLaunchKernelGGL((k_rans_fast<0, true>), dim3(grid), dim3(64), chain_lds(), s, j, nplane, a, na, b, nblk, rot);
+    else hipLaunchKernelGGL((k_rans_fast<0, false>), dim3(grid), dim3(64), chain_lds(), s, j, nplane, a, na, b, nblk, rot);
+  } else if (kind == 1) {   // short or few chains (LZ / map streams, the ladder's winners): the window only
+    if (w) hipLaunchKernelGGL((k_rans_fast<1, true>), dim3(grid), dim3(64), WIN_PITCH * 4 * 64, s, j, nplane, a, na, b, nblk, rot);
+    else hipLaunchKernelGGL((k_rans_fast<1, false>), dim3(grid), dim3(64), WIN_PITCH * 4 * 64, s, j, nplane, a, na, b, nblk, rot);
+  } else {   // size-only trial encodes: no window; one chain per SIMD (40 KB), all at once
+    if (w) hipLaunchKernelGGL((k_rans_fast<2, true>), dim3(grid), dim3(64), 40 * 1024, s, j, nplane, a, na, b, nblk, rot);
+    else hipLaunchKernelGGL((k_rans_fast<2, false>), dim3(grid), dim3(64), 40 * 1024, s, j, nplane, a, na, b, nblk, rot);
+  }
 }
 
 void launch_rans_fast_s(const EncodeJob& j, hipStream_t s, int np0, SidMap a0, int na0, SidMap b0, int np2, SidMap a2,
@@ -456,8 +464,12 @@ void launch_rans_fast_s(const EncodeJob& j, hipStream_t s, int np0, SidMap a0, i
   const int nblk0 = (np0 + 63) / 64, nblk2 = (np2 + 63) / 64, nblk1 = (np1 + 63) / 64;
   if (nblk0 + nblk2 + nblk1 == 0) return;
   static_assert(WIN_PITCH * 4 * 64 <= 40 * 1024, "the window fits the 40 KB request");
-  hipLaunchKernelGGL(k_rans_fast_s, dim3(nblk0 + nblk2 + nblk1), dim3(64), 40 * 1024, s, j, np0, a0, na0, b0, nblk0,
-                     np2, a2, na2, nblk2, np1, a1, na1, nblk1);
+  if (j.tab_wide)
+    hipLaunchKernelGGL((k_rans_fast_s<true>), dim3(nblk0 + nblk2 + nblk1), dim3(64), 40 * 1024, s, j, np0, a0, na0, b0, nblk0,
+                       np2, a2, na2, nblk2, np1, a1, na1, nblk1);
+  else
+    hipLaunchKernelGGL((k_rans_fast_s<false>), dim3(nblk0 + nblk2 + nblk1), dim3(64), 40 * 1024, s, j, np0, a0, na0, b0, nblk0,
+                       np2, a2, na2, nblk2, np1, a1, na1, nblk1);
 }
 
 void launch_rans_gen(const EncodeJob& j, int nstreams, hipStream_t s, SidMap m) {
