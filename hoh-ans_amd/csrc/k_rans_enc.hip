@@ -464,11 +464,13 @@ void launch_rans_fast_s(const EncodeJob& j, hipStream_t s, int np0, SidMap a0, i
   const int nblk0 = (np0 + 63) / 64, nblk2 = (np2 + 63) / 64, nblk1 = (np1 + 63) / 64;
   if (nblk0 + nblk2 + nblk1 == 0) return;
   static_assert(WIN_PITCH * 4 * 64 <= 40 * 1024, "the window fits the 40 KB request");
+  // LDS request per chain workgroup (chains per CU; knob CHAIN_S_LDS_KB)
+  const size_t lds = (size_t)std::max(40, std::min(160, HOH_KNOB(CHAIN_S_LDS_KB, 40))) * 1024;
   if (j.tab_wide)
-    hipLaunchKernelGGL((k_rans_fast_s<true>), dim3(nblk0 + nblk2 + nblk1), dim3(64), 40 * 1024, s, j, np0, a0, na0, b0, nblk0,
+    hipLaunchKernelGGL((k_rans_fast_s<true>), dim3(nblk0 + nblk2 + nblk1), dim3(64), lds, s, j, np0, a0, na0, b0, nblk0,
                        np2, a2, na2, nblk2, np1, a1, na1, nblk1);
   else
-    hipLaunchKernelGGL((k_rans_fast_s<false>), dim3(nblk0 + nblk2 + nblk1), dim3(64), 40 * 1024, s, j, np0, a0, na0, b0, nblk0,
+    hipLaunchKernelGGL((k_rans_fast_s<false>), dim3(nblk0 + nblk2 + nblk1), dim3(64), lds, s, j, np0, a0, na0, b0, nblk0,
                        np2, a2, na2, nblk2, np1, a1, na1, nblk1);
 }
 
