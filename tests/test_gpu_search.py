@@ -57,6 +57,10 @@ def cases():
     half[128:] = 9
     out.append(("halfflat-s3", 3, half))
     out.append(("untiled200x100-s2", 2, synth_rgb(200, 100, 11, 3)))
+    # one tile of fewer than 65,536 positions at -s3/-s4 (k_lzsort's 512-thread shape: partial
+    # chunks, ranks built in parts of 16,384 with a partial last part)
+    out.append(("untiled200x100-s4", 4, synth_rgb(200, 100, 13, 3)))
+    out.append(("untiled250x250-s3", 3, synth_rgb(250, 250, 14, 3)))
     out.append(("tiny30x20-s1", 1, synth_rgb(30, 20, 12, 3)))
     return out
 
