@@ -5,7 +5,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 for rep in 1 2; do
-  for x in 16 4 64 1000000; do
+  for x in ${XROWS:-16 4 64 1000000}; do
     echo -n "rep $rep LZ_XROW=$x single: "; HOH_LIB=var/knobs.so HOH_LZ_XROW=$x timeout -k 10 100 python3 tools/scripts/natural_prof.py 8192 0 5 | sed 's/.*encode/encode/' || exit 1
     echo -n "rep $rep LZ_XROW=$x pipeline: "; HOH_LIB=var/knobs.so HOH_LZ_XROW=$x timeout -k 10 150 python3 tools/scripts/nat0_pipe.py 4 8 6 || exit 1
   done
