@@ -2580,8 +2580,14 @@ int decode_tiles_images_async_impl(hoh_ctx* c, int n, const uint8_t* d_blob, siz
   return decode_run(c, j, idx, s, &as);
 }
 
-// copies reading the row above that make an LZ tile a chain tile (knob LZ_XROW)
-static uint32_t lz_xrow() { return (uint32_t)HOH_KNOB(LZ_XROW, LZ_XROW); }
+// copies reading the row above that make an LZ tile a chain tile (knobs LZ_XROW, LZ_XROW_BATCH).
+// A batch decodes many images' LZ tiles at once, and there the raster chains (less work per tile
+// than the dynamic wavefront) pay from 2 such copies on: natural 8192^2 -s0 pipeline 50.1 -> 53.5
+// GB/s, while one image alone keeps 16 (its wavefront tiles finish sooner: 5.43 against 5.55 ms;
+// profiles/r06b/xrow_sweep.txt)
+static uint32_t lz_xrow(bool batch) {
+  return batch ? (uint32_t)HOH_KNOB(LZ_XROW_BATCH, 2) : (uint32_t)HOH_KNOB(LZ_XROW, LZ_XROW);
+}
 
 // No-index chain kernel choice (hoh_ctx_set_option HOH_OPT_NOIX_DECODER, default adaptive).
 // k_drans_multi (12 chains per CU, full tables) has the shorter step (~260 cycles against
@@ -2671,7 +2677,7 @@ static int decode_run(hoh_ctx* c, DecJob& j, const hoh_index* idx, hipStream_t s
 #else
   if ((e = dbuf(w, 15, (size_t)j.ntiles * j.th * ((j.tw + 15) & ~15) + 16, &q))) return e; j.bmap = (uint8_t*)q;
 #endif
-  j.lz_xrow = lz_xrow();
+  j.lz_xrow = lz_xrow(j.nimg > 1);
   if (idx) {                                   // a batch's index serves that batch's layout only
     uint64_t st = 0;
     const int ni = index_batch(idx, &st);
